@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of the DEAP population hot path on MI355X.
+
+Metric (BASELINE.json): individual-generations/sec @ pop = 2^20,
+Rastrigin-1000D fp64, 1-8 GPUs.  A *step* is one eaSimple generation over the
+whole population — select (selTournament t=3) -> clone -> varAnd (cxBlend
+alpha=0.5, cxpb 0.5; mutGaussian mu=0 sigma=1 indpb=0.05, mutpb 0.2) ->
+evaluate invalid — as ONE fused kernel (``dm_generation``), population resident
+in HBM, synthetic random-init genomes (U[-5.12, 5.12]).
+
+N=1: config C3 (one island of 2^20).  N>1 (torchrun, one rank per GPU): one
+2^20 island per GPU (weak scaling, config C4) with migRing every 5 gens (k=15,
+selBest, ring i -> i+1) exchanged with RCCL point-to-point; value = all ranks'
+individual-generations / max-over-ranks time.
+
+``roofline``: algorithmic bytes per individual-generation B = 2G + (t+1)F
+(2*8000 + 4*8 = 16,032 B for C3) x individuals per launch /
+average fused-kernel duration measured with HIP events on the launch stream;
+peak 8,000 GB/s (MI355X HBM3E).  ``traffic``: HBM bytes per launch from the
+rocprofv3 PMC pass committed under profiles/ (or null).
+``cpu_baseline``: DEAP-faithful pure-Python eaSimple (oracle/deap_port.py,
+array('d') genomes, deepcopy clone, multiprocessing.Pool map) on a bounded
+sample, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (problem, gtype, dim, cx, mut, weights, bytes per ind-gen)
+    "c3": ("rastrigin", "f64", 1000, "blend", "gaussian", (-1.0,), 2 * 8000 + 4 * 8),
+    "c3r": ("rosenbrock", "f64", 1000, "blend", "gaussian", (-1.0,), 2 * 8000 + 4 * 8),
+    "c2": ("onemax", "bits", 4096, "twopoint", "flipbit", (1.0,), 2 * 512 + 4 * 8),
+}
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--pop", type=int, default=1 << 20)
+    ap.add_argument("--mig-every", type=int, default=5)
+    ap.add_argument("--mig-k", type=int, default=15)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=8192)
+    ap.add_argument("--seed", type=int, default=1234)
+    return ap.parse_args()
+
+
+def cpu_baseline(problem, sample):
+    import multiprocessing
+    from oracle import deap_port
+    workers = max(1, min(os.cpu_count() or 1, 16))
+    dim = CONFIGS_DIM[problem]
+    rate, secs, used = deap_port.run(problem if problem != "onemax" else "onemax", n=sample,
+                                     dim=dim, ngen=2, workers=workers)
+    return {"value": rate, "unit": "individual-generations/sec", "cores": used, "kind": "port",
+            "sample": "DEAP-faithful eaSimple (oracle/deap_port.py: array genomes, deepcopy clone, "
+                      "Pool(%d).map evaluate), pop %d x %d genes, 2 timed generations (%.1f s)"
+                      % (used, sample, dim, secs)}
+
+
+CONFIGS_DIM = {"rastrigin": 1000, "rosenbrock": 1000, "onemax": 4096}
+
+
+def load_traffic(config):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(config)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+
+    problem, gtype, dim, cx, mut, weights, bpi = CONFIGS[args.config]
+    n = args.pop
+    stream = RandomStream(args.seed, island=rank)
+    low, high = {"rastrigin": (-5.12, 5.12), "rosenbrock": (-2.048, 2.048),
+                 "onemax": (0, 1)}[problem]
+    pop = tools.initPopulation(n=n, dim=dim, low=low, high=high, gtype=gtype, weights=weights,
+                               device=device, stream=stream)
+    tb = base.Toolbox()
+    tb.register("evaluate", getattr(benchmarks, problem))
+    tb.register("select", tools.selTournament, tournsize=3)
+    if cx == "blend":
+        tb.register("mate", tools.cxBlend, alpha=0.5)
+    else:
+        tb.register("mate", tools.cxTwoPoint)
+    if mut == "gaussian":
+        tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+    else:
+        tb.register("mutate", tools.mutFlipBit, indpb=0.05)
+    cxpb, mutpb = 0.5, 0.2
+    getattr(benchmarks, problem)(pop)  # generation 0: evaluate everyone
+    step = algorithms.GenerationStep(pop, tb, cxpb, mutpb)
+    off = pop.like(n, capacity=n)
+    nevals = torch.zeros(args.warmup + args.steps + 1, dtype=torch.int64, device=device)
+
+    def migrate():
+        from deap_amd.islands import migRingDistributed
+        migRingDistributed([pop], [rank], world, args.mig_k, tools.selBest, stream=stream)
+
+    def one_gen(g, ev_pair=None):
+        if ev_pair is not None:
+            ev_pair[0].record()
+        step.step(pop, off, stream, ctypes_ptr(nevals, g))
+        if ev_pair is not None:
+            ev_pair[1].record()
+        pop.swap_storage(off)
+        if world > 1 and (g + 1) % args.mig_every == 0:
+            migrate()
+
+    import ctypes
+
+    def ctypes_ptr(t, i):
+        return ctypes.c_void_p(t.data_ptr() + 8 * i)
+
+    for g in range(args.warmup):
+        one_gen(g)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        one_gen(args.warmup + s, events[s])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    if world > 1:
+        t = torch.tensor([kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        kern_ms = float(t.item())
+    nev = nevals.cpu().tolist()
+    # sanity: the population stays valid and finite
+    wv = pop.wvalues[:n]
+    assert bool(pop.valid[:n].bool().all()), "invalid fitness left after a generation"
+    assert bool(torch.isfinite(wv).all()), "non-finite fitness"
+
+    total = n * args.steps * world
+    value = total / elapsed
+    achieved = (n * bpi) / (kern_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic(args.config), "kernel": "gen_float_kernel/gen_bits_kernel",
+                "kernel_ms": round(kern_ms, 4), "bytes_per_ind_gen": bpi}
+    out = {"metric": "individual-generations/sec @pop=2^20 Rastrigin-1000D, 1-8 GPU; % HBM peak",
+           "value": round(value, 1), "unit": "individual-generations/sec", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None,
+           "dtype": {"f64": "f64", "f32": "f32", "bits": "u64"}[gtype], "data": "synthetic",
+           "config": {"workload": {"c3": "C3 Rastrigin-1000D fp64 eaSimple",
+                                   "c3r": "C3 Rosenbrock-1000D fp64 eaSimple",
+                                   "c2": "C2 OneMax-4096 packed-bit eaSimple"}[args.config]
+                      + (" islands (C4), migRing k=%d every %d gens" % (args.mig_k, args.mig_every)
+                         if world > 1 else ""),
+                      "pop_per_gpu": n, "genes": dim, "islands": world,
+                      "operators": "selTournament(t=3) cx%s mut%s cxpb=0.5 mutpb=0.2 indpb=0.05"
+                                   % (cx.capitalize(), mut.capitalize()),
+                      "parallelism": "islands%d" % world},
+           "roofline": roofline,
+           "nevals_mean": round(sum(nev[args.warmup:args.warmup + args.steps]) / args.steps, 1)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(problem, args.cpu_sample)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

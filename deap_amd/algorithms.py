@@ -1,0 +1,353 @@
+"""Generational drivers on device-resident populations (``deap/algorithms.py``).
+
+Signatures and return values follow the reference; the population argument is
+a :class:`~deap_amd.device.DevicePopulation` and every registered operator must
+be a ``deap_amd`` device operator (there is no host fallback: a plain Python
+function in the toolbox raises ``TypeError``).  Each generation is one fused
+kernel launch (select -> clone -> varAnd -> evaluate, ``dm_generation``) for
+``eaSimple``; ``eaMuPlusLambda`` runs ``varOr`` (``dm_var_or``) then the
+selection over ``population + offspring``.  Per-generation bookkeeping
+(``nevals``, statistics) is accumulated on the device and read back once at
+the end unless ``verbose`` asks for a line per generation.
+
+Extra keyword-only arguments (not in DEAP) control the random decisions:
+``stream`` (a :class:`~deap_amd.ops.RandomStream`, default the global one),
+``mode`` ("native" | "inject" | "dump") and ``decisions`` (a list with one
+:class:`~deap_amd.decisions.Decisions` per generation: read in inject mode,
+appended to in dump mode).
+"""
+import ctypes
+
+from . import _lib
+from .decisions import Decisions
+from .device import DevicePopulation
+from .ops import default_stream, mode_code, resolve
+from .tools.support import Logbook
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _check_pop(population):
+    if not isinstance(population, DevicePopulation):
+        raise TypeError("deap_amd drivers operate on a DevicePopulation (got %r); build one with "
+                        "deap_amd.tools.initPopulation or DevicePopulation.from_individuals"
+                        % type(population))
+
+
+def _variation(population, mate, mutate, cxpb, mutpb):
+    var = _lib.Variation()
+    var.cxpb = float(cxpb)
+    var.mutpb = float(mutpb)
+    var.sigma = 1.0
+    if mate is not None:
+        op, a, kw = mate
+        op.fill(var, a, kw)
+    if mutate is not None:
+        op, a, kw = mutate
+        op.fill(var, a, kw, population)
+    return var
+
+
+def _eval(population, evaluate):
+    if evaluate is None:
+        e = _lib.Eval()
+        e.fn = _lib.DM_EVAL_NONE
+        return e
+    op, a, kw = evaluate
+    return op.eval_struct(population.weights, a, kw)
+
+
+def _mode_and_decisions(mode, decisions, gen_index, k, population, tournsize, var, varor=False):
+    """Decide the RNG mode of one launch and its decisions buffer."""
+    if mode is None:
+        mode = "native"
+    code = mode_code(mode)
+    if code == _lib.DM_RNG_NATIVE:
+        return code, None
+    if code == _lib.DM_RNG_INJECT:
+        d = decisions[gen_index] if isinstance(decisions, (list, tuple)) else decisions
+        if d is None:
+            raise ValueError("inject mode needs decisions")
+        return code, d
+    d = Decisions.allocate(k, population.dim, population.device, tournsize=tournsize,
+                           cx=var.cx != _lib.DM_CX_NONE, blend=var.cx == _lib.DM_CX_BLEND,
+                           mut=var.mut != _lib.DM_MUT_NONE,
+                           gauss=var.mut == _lib.DM_MUT_GAUSSIAN, varor=varor)
+    if isinstance(decisions, list):
+        decisions.append(d)
+    return code, d
+
+
+def _apply_variation(population, mate_op, mate_args, mate_kw, mut_op, mut_args, mut_kw, cxpb,
+                     mutpb, decisions=None, mode=None, stream=None):
+    """Direct call of a crossover / mutation operator on a population."""
+    _check_pop(population)
+    mate = (mate_op, mate_args, mate_kw) if mate_op is not None else None
+    mutate = (mut_op, mut_args, mut_kw) if mut_op is not None else None
+    return _var_and(population, mate, mutate, cxpb, mutpb, decisions, mode, stream)
+
+
+def _var_and(population, mate, mutate, cxpb, mutpb, decisions, mode, stream):
+    stream = stream or default_stream()
+    var = _variation(population, mate, mutate, cxpb, mutpb)
+    offspring = population.like()
+    code, d = _mode_and_decisions(mode, decisions, 0, len(population), population, 0, var)
+    ev = _eval(population, None)
+    ctx = population.ctx.bind()
+    dec = d.c_struct() if d is not None else None
+    _lib.call("dm_generation", ctx, ctypes.byref(population.c_pop()),
+              ctypes.byref(offspring.c_pop()), _lib.DM_SEL_IDENTITY, 0, None, ctypes.byref(var),
+              ctypes.byref(ev), stream.next(), code,
+              ctypes.byref(dec) if dec is not None else None, None)
+    return offspring
+
+
+def varAnd(population, toolbox, cxpb, mutpb, *, decisions=None, mode=None, stream=None):
+    """Crossover AND mutation on a cloned population (``deap/algorithms.py:33-82``).
+
+    Pairs ``(2i-1... )``: for i = 1, 3, 5, ... ``random() < cxpb`` mates
+    offspring[i-1] and offspring[i]; then every offspring is mutated when
+    ``random() < mutpb``.  Modified individuals have their fitness invalidated.
+    Returns a new population; the input is untouched."""
+    _check_pop(population)
+    mate = resolve(toolbox.mate)
+    mutate = resolve(toolbox.mutate)
+    return _var_and(population, mate, mutate, cxpb, mutpb, decisions, mode, stream)
+
+
+def _selection_spec(toolbox):
+    op, a, kw = resolve(toolbox.select)
+    return op, a, kw
+
+
+class _Bookkeeping:
+    """nevals + statistics recorded per generation, on device when possible."""
+
+    def __init__(self, population, ngen, stats, halloffame, verbose):
+        torch = _torch()
+        self.nevals = torch.zeros((ngen + 1,), dtype=torch.int64, device=population.device)
+        self.stats = stats
+        self.hof = halloffame
+        self.verbose = verbose
+        self.records = []
+        self.logbook = Logbook()
+        self.logbook.header = ["gen", "nevals"] + (stats.fields if stats else [])
+
+    def nevals_ptr(self, gen):
+        return ctypes.c_void_p(self.nevals.data_ptr() + 8 * gen)
+
+    def record(self, gen, population):
+        if self.hof is not None:
+            self.hof.update(population)
+        rec = self.stats.compile(population) if self.stats else {}
+        self.records.append((gen, rec))
+        if self.verbose:
+            self._flush_one(gen, rec)
+
+    def _flush_one(self, gen, rec):
+        nev = int(self.nevals[gen].item())
+        self.logbook.record(gen=gen, nevals=nev, **_materialise(rec))
+        print(self.logbook.stream)
+
+    def finish(self):
+        if not self.verbose:
+            nev = self.nevals.cpu().tolist()
+            for gen, rec in self.records:
+                self.logbook.record(gen=gen, nevals=nev[gen], **_materialise(rec))
+        return self.logbook
+
+
+def _materialise(rec):
+    out = {}
+    for k, v in rec.items():
+        out[k] = v() if callable(v) else v
+    return out
+
+
+class GenerationStep:
+    """One eaSimple generation body bound to a toolbox: ``step(parents,
+    children)`` launches the fused select -> clone -> varAnd -> evaluate
+    kernel (``dm_generation``) on the current stream.  eaSimple is a loop of
+    these; ``bench.py`` times them."""
+
+    def __init__(self, population, toolbox, cxpb, mutpb, evaluate=True):
+        from .tools.selection import selRandom, selTournament
+        self._selTournament, self._selRandom = selTournament, selRandom
+        self.mate = resolve(toolbox.mate)
+        self.mutate = resolve(toolbox.mutate)
+        self.evaluate = resolve(toolbox.evaluate) if evaluate else None
+        self.sel = _selection_spec(toolbox)
+        self.var = _variation(population, self.mate, self.mutate, cxpb, mutpb)
+        self.ev = _eval(population, self.evaluate)
+
+    def step(self, parents, children, stream, nevals_ptr=None, mode=None, decisions=None,
+             gen_index=0):
+        sel_op, sel_args, sel_kw = self.sel
+        n = len(parents)
+        sel_kind, tournsize, sel_index = _fused_selection(sel_op, sel_args, sel_kw, parents,
+                                                          self._selTournament, self._selRandom,
+                                                          stream)
+        code, d = _mode_and_decisions(mode, decisions, gen_index, n, parents,
+                                      tournsize if sel_kind in (_lib.DM_SEL_TOURNAMENT,
+                                                                _lib.DM_SEL_RANDOM) else 0,
+                                      self.var)
+        dec = d.c_struct() if d is not None else None
+        children.resize(n)
+        _lib.call("dm_generation", parents.ctx.bind(), ctypes.byref(parents.c_pop()),
+                  ctypes.byref(children.c_pop()), sel_kind, tournsize,
+                  ctypes.c_void_p(sel_index.data_ptr()) if sel_index is not None else None,
+                  ctypes.byref(self.var), ctypes.byref(self.ev), stream.next(), code,
+                  ctypes.byref(dec) if dec is not None else None, nevals_ptr)
+
+
+def eaSimple(population, toolbox, cxpb, mutpb, ngen, stats=None, halloffame=None,
+             verbose=__debug__, *, decisions=None, mode=None, stream=None):
+    """The simple generational GA (``deap/algorithms.py:85-189``).
+
+    gen 0 evaluates invalid individuals; each later generation is
+    ``select(population, len(population))`` -> ``varAnd`` -> evaluate invalid
+    -> ``population[:] = offspring``, fused into one kernel when the selection
+    is ``selTournament``/``selRandom``.  Returns ``(population, logbook)``."""
+    _check_pop(population)
+    stream = stream or default_stream()
+    step = GenerationStep(population, toolbox, cxpb, mutpb)
+    book = _Bookkeeping(population, ngen, stats, halloffame, verbose)
+    ctx = population.ctx.bind()
+
+    # generation 0: evaluate the invalid individuals                      :149-160
+    _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(step.ev), 1,
+              book.nevals_ptr(0))
+    book.record(0, population)
+
+    offspring = population.like(len(population), capacity=population.capacity)
+    for gen in range(1, ngen + 1):
+        step.step(population, offspring, stream, book.nevals_ptr(gen), mode, decisions, gen - 1)
+        population.swap_storage(offspring)                                 # :181
+        book.record(gen, population)
+    return population, book.finish()
+
+
+def _fused_selection(sel_op, sel_args, sel_kw, population, selTournament, selRandom, stream):
+    n = len(population)
+    if sel_op is selTournament:
+        k, tournsize = _tournament_args(sel_args, sel_kw, n)
+        if k == n and sel_kw.get("fit_attr", "fitness") == "fitness":
+            return _lib.DM_SEL_TOURNAMENT, tournsize, None
+    if sel_op is selRandom and not sel_args and "k" not in sel_kw:
+        return _lib.DM_SEL_RANDOM, 1, None
+    idx = sel_op(population, n, *sel_args, stream=stream, **sel_kw)
+    return _lib.DM_SEL_INDEX, 0, idx
+
+
+def _tournament_args(args, kw, n):
+    # select(population, len(population)) with tournsize bound in the toolbox
+    if "tournsize" in kw:
+        return n, int(kw["tournsize"])
+    if args:
+        return n, int(args[0])
+    raise TypeError("selTournament() missing required argument: 'tournsize'")
+
+
+def varOr(population, toolbox, lambda_, cxpb, mutpb, *, decisions=None, mode=None, stream=None,
+          evaluate=False, out=None):
+    """Crossover OR mutation OR reproduction (``deap/algorithms.py:192-245``).
+    Returns a population of ``lambda_`` offspring."""
+    _check_pop(population)
+    assert (cxpb + mutpb) <= 1.0, (
+        "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
+    stream = stream or default_stream()
+    mate = resolve(toolbox.mate)
+    mutate = resolve(toolbox.mutate)
+    var = _variation(population, mate, mutate, cxpb, mutpb)
+    ev = _eval(population, resolve(toolbox.evaluate) if evaluate else None)
+    offspring = out if out is not None else population.like(lambda_, capacity=lambda_)
+    code, d = _mode_and_decisions(mode, decisions, 0, lambda_, population, 0, var, varor=True)
+    dec = d.c_struct() if d is not None else None
+    ctx = population.ctx.bind()
+    _lib.call("dm_var_or", ctx, ctypes.byref(population.c_pop()),
+              ctypes.byref(offspring.c_pop(0, lambda_)), ctypes.byref(var), ctypes.byref(ev),
+              stream.next(), code, ctypes.byref(dec) if dec is not None else None, None)
+    return offspring
+
+
+def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=None,
+                   halloffame=None, verbose=__debug__, *, decisions=None, mode=None,
+                   stream=None):
+    """(mu + lambda) evolution (``deap/algorithms.py:248-337``): varOr ->
+    evaluate invalid -> ``population[:] = select(population + offspring, mu)``.
+    The concatenation keeps parents first, then offspring, as in the reference
+    (the order matters to NSGA-II's front order)."""
+    _check_pop(population)
+    stream = stream or default_stream()
+    mate = resolve(toolbox.mate)
+    mutate = resolve(toolbox.mutate)
+    evaluate = resolve(toolbox.evaluate)
+    sel_op, sel_args, sel_kw = _selection_spec(toolbox)
+    var = _variation(population, mate, mutate, cxpb, mutpb)
+    assert (cxpb + mutpb) <= 1.0, (
+        "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
+    ev = _eval(population, evaluate)
+    book = _Bookkeeping(population, ngen, stats, halloffame, verbose)
+    ctx = population.ctx.bind()
+
+    _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(ev), 1,
+              book.nevals_ptr(0))
+    book.record(0, population)
+
+    n0 = len(population)
+    cap = max(n0, mu) + lambda_
+    combined = population.like(n0 + lambda_, capacity=cap)
+    nxt = population.like(mu, capacity=cap)
+    # combined rows [0, n) = population
+    _lib.call("dm_gather", ctx, ctypes.byref(population.c_pop()), None,
+              ctypes.byref(combined.c_pop(0, n0)))
+    n = n0
+    for gen in range(1, ngen + 1):
+        code, d = _mode_and_decisions(mode, decisions, gen - 1, lambda_, population, 0, var,
+                                      varor=True)
+        dec = d.c_struct() if d is not None else None
+        _lib.call("dm_var_or", ctx, ctypes.byref(combined.c_pop(0, n)),
+                  ctypes.byref(combined.c_pop(n, lambda_)), ctypes.byref(var), ctypes.byref(ev),
+                  stream.next(), code, ctypes.byref(dec) if dec is not None else None,
+                  book.nevals_ptr(gen))
+        combined.resize(n + lambda_)
+        if halloffame is not None:
+            halloffame.update(_View(combined, n, lambda_))
+        idx = sel_op(combined, mu, *sel_args, stream=stream, **sel_kw)
+        nxt.resize(mu)
+        _lib.call("dm_gather", ctx, ctypes.byref(combined.c_pop()),
+                  ctypes.c_void_p(idx.data_ptr()), ctypes.byref(nxt.c_pop(0, mu)))
+        if getattr(combined, "crowding_dist", None) is not None:
+            nxt.crowding_dist = combined.crowding_dist[idx.long()]
+        combined.swap_storage(nxt)
+        n = mu
+        combined.resize(mu)
+        rec = stats.compile(combined) if stats else {}
+        book.records.append((gen, rec))
+        if verbose:
+            book._flush_one(gen, rec)
+    # hand the final population back in place
+    final = population.like(mu, capacity=max(mu, 1))
+    _lib.call("dm_gather", ctx, ctypes.byref(combined.c_pop(0, mu)), None,
+              ctypes.byref(final.c_pop()))
+    final.crowding_dist = combined.crowding_dist
+    population.swap_storage(final)
+    return population, book.finish()
+
+
+class _View(DevicePopulation):
+    """Row range of a population, sharing its buffers (no copy)."""
+
+    def __init__(self, base, start, count):  # pylint: disable=super-init-not-called
+        self.__dict__.update(base.__dict__)
+        self.genes = base.genes[start:start + count]
+        self.wvalues = base.wvalues[start:start + count]
+        self.valid = base.valid[start:start + count]
+        self.n = count
+        self.capacity = count
+
+
+__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda"]

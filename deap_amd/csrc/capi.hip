@@ -1,0 +1,587 @@
+// capi.hip — context, errors, validation, RNG/init, evaluation, selection
+// and gather entry points of libdeapmi.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.hpp"
+#include "evals.hpp"
+
+namespace dm {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+void* scratch_slot(dm_ctx* ctx, int slot, size_t bytes) {
+    bytes = align_up(std::max<size_t>(bytes, 256), 256);
+    if (bytes <= ctx->scratch_bytes[slot]) return ctx->scratch[slot];
+    if (ctx->scratch[slot]) {
+        // the stream may still use the old arena
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+            hipFree(ctx->scratch[slot]) != hipSuccess) {
+            set_error("scratch release failed");
+            return nullptr;
+        }
+        ctx->scratch[slot] = nullptr;
+        ctx->scratch_bytes[slot] = 0;
+    }
+    if (hipMalloc(&ctx->scratch[slot], bytes) != hipSuccess) {
+        set_error("hipMalloc(%zu) for scratch slot %d failed", bytes, slot);
+        ctx->scratch[slot] = nullptr;
+        return nullptr;
+    }
+    ctx->scratch_bytes[slot] = bytes;
+    return ctx->scratch[slot];
+}
+
+void* pinned(dm_ctx* ctx, size_t bytes) {
+    bytes = align_up(std::max<size_t>(bytes, 256), 256);
+    if (bytes <= ctx->pinned_bytes) return ctx->pinned;
+    if (ctx->pinned) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+    }
+    if (hipHostMalloc(&ctx->pinned, bytes, hipHostMallocDefault) != hipSuccess) {
+        set_error("hipHostMalloc(%zu) failed", bytes);
+        ctx->pinned = nullptr;
+        return nullptr;
+    }
+    ctx->pinned_bytes = bytes;
+    return ctx->pinned;
+}
+
+int validate_pop(const dm_pop* p, const char* what) {
+    DM_CHECK_ARG(p != nullptr, "%s: null population", what);
+    DM_CHECK_ARG(p->n >= 0, "%s: negative size", what);
+    DM_CHECK_ARG(p->gtype == DM_BITS || p->gtype == DM_F32 || p->gtype == DM_F64,
+                 "%s: bad genome type %d", what, p->gtype);
+    DM_CHECK_ARG(p->dim >= 1, "%s: dim must be >= 1", what);
+    DM_CHECK_ARG(p->nobj >= 1 && p->nobj <= DM_MAX_OBJ, "%s: nobj must be in [1, %d]", what,
+                 DM_MAX_OBJ);
+    DM_CHECK_ARG(p->stride % 16 == 0, "%s: row stride must be a multiple of 16", what);
+    const int64_t need = p->gtype == DM_BITS ? (int64_t)((p->dim + 63) / 64) * 8
+                         : p->gtype == DM_F32 ? (int64_t)((p->dim + 3) / 4) * 16
+                                              : (int64_t)((p->dim + 3) / 4) * 32;
+    DM_CHECK_ARG(p->stride >= need, "%s: row stride %lld < %lld bytes needed", what,
+                 (long long)p->stride, (long long)need);
+    if (p->n > 0)
+        DM_CHECK_ARG(p->genes && p->wvalues && p->valid, "%s: null device buffer", what);
+    return DM_OK;
+}
+
+int validate_eval(const dm_eval* ev, const dm_pop* p) {
+    if (ev->fn == DM_EVAL_NONE) return DM_OK;
+    DM_CHECK_ARG(ev->fn >= DM_EVAL_ONEMAX && ev->fn <= DM_EVAL_SPHERE, "bad eval fn %d", ev->fn);
+    if (p->gtype == DM_BITS)
+        DM_CHECK_ARG(ev->fn == DM_EVAL_ONEMAX, "packed-bit genomes support only OneMax");
+    const int m = eval_nobj(*ev);
+    DM_CHECK_ARG(m == p->nobj, "objective returns %d values but the fitness has %d weights", m,
+                 p->nobj);
+    if (ev->fn >= DM_EVAL_DTLZ1 && ev->fn <= DM_EVAL_DTLZ4) {
+        DM_CHECK_ARG(ev->obj >= 2 && ev->obj <= DM_MAX_OBJ, "DTLZ obj must be in [2, %d]",
+                     DM_MAX_OBJ);
+        DM_CHECK_ARG(p->dim >= ev->obj, "DTLZ needs at least obj genes");
+        DM_CHECK_ARG(ev->obj - 1 <= 8, "DTLZ supports at most 9 objectives");
+    }
+    if (ev->fn >= DM_EVAL_ZDT1 && ev->fn <= DM_EVAL_ZDT6)
+        DM_CHECK_ARG(p->dim >= 2, "ZDT needs at least 2 genes");
+    return DM_OK;
+}
+
+int validate_variation(const dm_variation* v, const dm_pop* p) {
+    DM_CHECK_ARG(v->cx >= DM_CX_NONE && v->cx <= DM_CX_BLEND, "bad crossover %d", v->cx);
+    DM_CHECK_ARG(v->mut >= DM_MUT_NONE && v->mut <= DM_MUT_GAUSSIAN, "bad mutation %d", v->mut);
+    if (p->gtype == DM_BITS) {
+        DM_CHECK_ARG(v->cx != DM_CX_BLEND, "cxBlend needs real-valued genomes");
+        DM_CHECK_ARG(v->mut != DM_MUT_GAUSSIAN, "mutGaussian needs real-valued genomes");
+    } else {
+        DM_CHECK_ARG(v->mut != DM_MUT_FLIPBIT, "mutFlipBit needs packed-bit genomes");
+    }
+    if (v->cx == DM_CX_TWOPOINT) DM_CHECK_ARG(p->dim >= 2, "cxTwoPoint needs at least 2 genes");
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RNG blocks (known-answer tests) and initialisation
+// ---------------------------------------------------------------------------
+__global__ void philox_blocks_kernel(u32x4 c0, uint32_t k0, uint32_t k1, int64_t n, uint32_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        u32x4 c = c0;
+        c.x += (uint32_t)i;
+        const u32x4 r = philox4x32_10(c, k0, k1);
+        reinterpret_cast<uint4*>(out)[i] = make_uint4(r.x, r.y, r.z, r.w);
+    }
+}
+
+__global__ void init_bits_kernel(uint64_t* genes, int64_t n, int64_t stride_words, int words,
+                                 int dim, Rng rng, uint8_t* valid) {
+    const int64_t total = n * words;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / words;
+        const int w = (int)(i % words);
+        const u32x4 v = rng(ST_INIT, (uint32_t)r, (uint32_t)w);
+        uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        const int nb = dim - w * 64;
+        if (nb < 64) x &= (1ull << nb) - 1;
+        genes[r * stride_words + w] = x;
+        if (w == 0) valid[r] = 0;
+    }
+}
+
+template <typename T>
+__global__ void init_float_kernel(char* genes, int64_t n, int64_t stride, int dim, double low,
+                                  double high, Rng rng, uint8_t* valid) {
+    const int q = (dim + 3) / 4;
+    const int64_t total = n * q;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / q;
+        const int g = (int)(i % q) * 4;
+        const u32x4 v = rng(ST_INIT, (uint32_t)r, (uint32_t)(g >> 2));
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        T* row = reinterpret_cast<T*>(genes + r * stride);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // random.uniform(a, b) = a + (b - a) * random()
+            const double u = u01_32(ws[j]);
+            row[g + j] = (g + j < dim) ? (T)(low + (high - low) * u) : (T)0;
+        }
+        if (g == 0) valid[r] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Batch evaluation: one lane group per row.
+// ---------------------------------------------------------------------------
+template <typename T, int G, int EC>
+__global__ __launch_bounds__(256) void eval_float_kernel(const char* genes, int64_t stride,
+                                                         double* wv, uint8_t* valid, int64_t n,
+                                                         int dim, int nobj, dm_eval ev,
+                                                         int only_invalid, int64_t* nevals) {
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & (G - 1);
+    const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / G);
+    int64_t cnt = 0;
+    for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; r < n; r += gstride) {
+        const bool todo = !only_invalid || !valid[r];
+        if (!todo) continue;  // uniform within the group
+        const char* row = genes + r * stride;
+        EvalState st;
+        eval_init(st);
+        for (int cbase = 0; cbase < dim; cbase += 4 * G) {
+            const int g = cbase + 4 * sub;
+            double y[4] = {0, 0, 0, 0};
+            if (g < dim) {
+                if constexpr (sizeof(T) == 8) {
+                    const double2* p = reinterpret_cast<const double2*>(row + (size_t)g * 8);
+                    const double2 a = p[0], b = p[1];
+                    y[0] = a.x;
+                    y[1] = a.y;
+                    y[2] = b.x;
+                    y[3] = b.y;
+                } else {
+                    const float4 a = *reinterpret_cast<const float4*>(row + (size_t)g * 4);
+                    y[0] = a.x;
+                    y[1] = a.y;
+                    y[2] = a.z;
+                    y[3] = a.w;
+                }
+            }
+            eval_chunk<G, EC>(ev, dim, g, cbase, y, true, st);
+        }
+        double f[DM_MAX_OBJ];
+        eval_finish<G, EC>(ev, dim, st, f);
+        if (sub == 0) {
+            for (int o = 0; o < nobj; ++o) wv[r * nobj + o] = f[o] * ev.weights[o];
+            valid[r] = 1;
+            ++cnt;
+        }
+    }
+    if (nevals) {
+        int64_t tot = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd((unsigned long long*)nevals, (unsigned long long)tot);
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void eval_bits_kernel(const char* genes, int64_t stride,
+                                                        double* wv, uint8_t* valid, int64_t n,
+                                                        int words, int nobj, dm_eval ev,
+                                                        int only_invalid, int64_t* nevals) {
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & (G - 1);
+    const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / G);
+    int64_t cnt = 0;
+    for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; r < n; r += gstride) {
+        if (only_invalid && valid[r]) continue;
+        const uint64_t* row = reinterpret_cast<const uint64_t*>(genes + r * stride);
+        int64_t pc = 0;
+        for (int w = sub; w < words; w += G) pc += __popcll(row[w]);
+        pc = group_sum_i<G>(pc);
+        if (sub == 0) {
+            for (int o = 0; o < nobj; ++o) wv[r * nobj + o] = (double)pc * ev.weights[o];
+            valid[r] = 1;
+            ++cnt;
+        }
+    }
+    if (nevals) {
+        int64_t tot = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd((unsigned long long*)nevals, (unsigned long long)tot);
+    }
+}
+
+template <typename T, int G>
+static void launch_eval_float(const dm_pop* p, const dm_eval* ev, int oi, int64_t* ne,
+                              dim3 grid, hipStream_t s) {
+    const int ec = eval_class(ev->fn);
+    if (ec == EC_SUM)
+        eval_float_kernel<T, G, EC_SUM><<<grid, 256, 0, s>>>((const char*)p->genes, p->stride,
+                                                            p->wvalues, p->valid, p->n, p->dim,
+                                                            p->nobj, *ev, oi, ne);
+    else
+        eval_float_kernel<T, G, EC_MO><<<grid, 256, 0, s>>>((const char*)p->genes, p->stride,
+                                                           p->wvalues, p->valid, p->n, p->dim,
+                                                           p->nobj, *ev, oi, ne);
+}
+
+static dim3 grid_for(dm_ctx* ctx, int64_t items, int per_block) {
+    int64_t b = (items + per_block - 1) / per_block;
+    b = std::min<int64_t>(std::max<int64_t>(b, 1), (int64_t)ctx->num_cus * 16);
+    return dim3((unsigned)b);
+}
+
+// ---------------------------------------------------------------------------
+// Selection (standalone) and gather
+// ---------------------------------------------------------------------------
+__global__ void sel_tournament_kernel(const double* wv, int nobj, int64_t n, int64_t k, int t,
+                                      Rng rng, int mode, int32_t* asp, int32_t* out) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < k;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        int64_t best = 0;
+        for (int j = 0; j < t; ++j) {
+            int64_t cand;
+            if (mode == DM_RNG_INJECT) {
+                cand = asp[c * t + j];
+            } else {
+                const u32x4 w = rng(ST_SEL, (uint32_t)c, (uint32_t)(j >> 1));
+                cand = (j & 1) ? bounded64(w.z, w.w, (uint32_t)n) : bounded64(w.x, w.y, (uint32_t)n);
+                if (mode == DM_RNG_DUMP) asp[c * t + j] = (int32_t)cand;
+            }
+            if (j == 0 || fit_gt(wv + cand * nobj, wv + best * nobj, nobj)) best = cand;
+        }
+        out[c] = (int32_t)best;
+    }
+}
+
+template <int VEC>
+__global__ void gather_kernel(const char* sg, const double* swv, const uint8_t* sv, int64_t sstride,
+                              char* dg, double* dwv, uint8_t* dv, int64_t dstride,
+                              const int32_t* idx, int64_t k, int64_t row_bytes, int nobj) {
+    // one wave per row; rows copied in 16-B pieces
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t q = row_bytes / 16;
+    for (int64_t r = wave; r < k; r += nw) {
+        const int64_t s = idx ? idx[r] : r;
+        const uint4* src = reinterpret_cast<const uint4*>(sg + s * sstride);
+        uint4* dst = reinterpret_cast<uint4*>(dg + r * dstride);
+        for (int64_t i = lane; i < q; i += 64) dst[i] = src[i];
+        if (lane < nobj) dwv[r * nobj + lane] = swv[s * nobj + lane];
+        if (lane == 0) dv[r] = sv[s];
+    }
+}
+
+// Fitness statistics: per-objective min/max/sum/sumsq/argmin/argmax of values.
+struct StatAcc {
+    double mn, mx, sum, sq;
+    int64_t amn, amx;
+};
+__global__ void stats_kernel(const double* wv, const uint8_t* valid, int64_t n, int nobj,
+                             dm_eval w, double* part, int64_t nparts) {
+    // w.weights used as weights; one block per partial, obj = blockIdx.y
+    const int o = blockIdx.y;
+    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, -1, -1};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (!valid[i]) continue;
+        const double v = wv[i * nobj + o] / w.weights[o];
+        if (v < a.mn || a.amn < 0) {
+            a.mn = v;
+            a.amn = i;
+        }
+        if (v > a.mx || a.amx < 0) {
+            a.mx = v;
+            a.amx = i;
+        }
+        a.sum += v;
+        a.sq += v * v;
+    }
+    __shared__ StatAcc sh[256];
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            StatAcc& x = sh[threadIdx.x];
+            const StatAcc& y = sh[threadIdx.x + s];
+            // first-occurrence argmin/argmax (numpy semantics): lower index wins ties
+            if (y.amn >= 0 && (x.amn < 0 || y.mn < x.mn || (y.mn == x.mn && y.amn < x.amn))) {
+                x.mn = y.mn;
+                x.amn = y.amn;
+            }
+            if (y.amx >= 0 && (x.amx < 0 || y.mx > x.mx || (y.mx == x.mx && y.amx < x.amx))) {
+                x.mx = y.mx;
+                x.amx = y.amx;
+            }
+            x.sum += y.sum;
+            x.sq += y.sq;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        double* p = part + ((int64_t)o * nparts + blockIdx.x) * 6;
+        p[0] = sh[0].mn;
+        p[1] = sh[0].mx;
+        p[2] = sh[0].sum;
+        p[3] = sh[0].sq;
+        p[4] = (double)sh[0].amn;
+        p[5] = (double)sh[0].amx;
+    }
+}
+__global__ void stats_combine_kernel(const double* part, int64_t nparts, int nobj, double* out) {
+    const int o = threadIdx.x;
+    if (o >= nobj) return;
+    double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0, amn = -1, amx = -1;
+    for (int64_t b = 0; b < nparts; ++b) {  // in block order: deterministic
+        const double* p = part + ((int64_t)o * nparts + b) * 6;
+        if (p[4] >= 0 && (amn < 0 || p[0] < mn)) {
+            mn = p[0];
+            amn = p[4];
+        }
+        if (p[5] >= 0 && (amx < 0 || p[1] > mx)) {
+            mx = p[1];
+            amx = p[5];
+        }
+        sum += p[2];
+        sq += p[3];
+    }
+    double* q = out + o * 6;
+    q[0] = mn;
+    q[1] = mx;
+    q[2] = sum;
+    q[3] = sq;
+    q[4] = amn;
+    q[5] = amx;
+}
+
+}  // namespace dm
+
+using namespace dm;
+
+extern "C" {
+
+const char* dm_last_error(void) { return dm::g_err; }
+const char* dm_version(void) { return "deapmi 0.1 gfx950"; }
+
+int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
+    DM_CHECK_ARG(out != nullptr, "null out");
+    DM_HIP(hipSetDevice(device));
+    dm_ctx* c = new dm_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)hip_stream;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        c->num_cus = cus;
+    *out = c;
+    return DM_OK;
+}
+
+int dm_ctx_destroy(dm_ctx* ctx) {
+    if (!ctx) return DM_OK;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < dm_ctx::kSlots; ++i)
+        if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    delete ctx;
+    return DM_OK;
+}
+
+int dm_ctx_set_stream(dm_ctx* ctx, void* hip_stream) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    ctx->stream = (hipStream_t)hip_stream;
+    return DM_OK;
+}
+
+int dm_ctx_sync(dm_ctx* ctx) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    return DM_OK;
+}
+
+int dm_philox_blocks(dm_ctx* ctx, const uint32_t ctr0[4], const uint32_t key[2], int64_t nblocks,
+                     uint32_t* out) {
+    DM_CHECK_ARG(ctx && ctr0 && key && out && nblocks >= 0, "bad argument");
+    if (nblocks == 0) return DM_OK;
+    philox_blocks_kernel<<<grid_for(ctx, nblocks, 256), 256, 0, ctx->stream>>>(
+        u32x4{ctr0[0], ctr0[1], ctr0[2], ctr0[3]}, key[0], key[1], nblocks, out);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_init_uniform(dm_ctx* ctx, dm_pop* pop, double low, double high, dm_rng rng) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    if (pop->n == 0) return DM_OK;
+    if (pop->gtype == DM_BITS) {
+        const int words = (pop->dim + 63) / 64;
+        init_bits_kernel<<<grid_for(ctx, pop->n * words, 256), 256, 0, ctx->stream>>>(
+            (uint64_t*)pop->genes, pop->n, pop->stride / 8, words, pop->dim, Rng(rng), pop->valid);
+    } else {
+        const int64_t items = pop->n * ((pop->dim + 3) / 4);
+        if (pop->gtype == DM_F64)
+            init_float_kernel<double><<<grid_for(ctx, items, 256), 256, 0, ctx->stream>>>(
+                (char*)pop->genes, pop->n, pop->stride, pop->dim, low, high, Rng(rng), pop->valid);
+        else
+            init_float_kernel<float><<<grid_for(ctx, items, 256), 256, 0, ctx->stream>>>(
+                (char*)pop->genes, pop->n, pop->stride, pop->dim, low, high, Rng(rng), pop->valid);
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_evaluate(dm_ctx* ctx, dm_pop* pop, const dm_eval* ev, int only_invalid, int64_t* nevals) {
+    DM_CHECK_ARG(ctx && ev, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(ev->fn != DM_EVAL_NONE, "no objective function");
+    if ((rc = validate_eval(ev, pop))) return rc;
+    if (pop->n == 0) return DM_OK;
+    hipStream_t s = ctx->stream;
+    if (pop->gtype == DM_BITS) {
+        const int words = (pop->dim + 63) / 64;
+        const int G = words <= 2 ? 2 : words <= 8 ? 8 : words <= 32 ? 32 : 64;
+        dim3 grid = grid_for(ctx, pop->n, 256 / G);
+        switch (G) {
+            case 2: eval_bits_kernel<2><<<grid, 256, 0, s>>>((const char*)pop->genes, pop->stride, pop->wvalues, pop->valid, pop->n, words, pop->nobj, *ev, only_invalid, nevals); break;
+            case 8: eval_bits_kernel<8><<<grid, 256, 0, s>>>((const char*)pop->genes, pop->stride, pop->wvalues, pop->valid, pop->n, words, pop->nobj, *ev, only_invalid, nevals); break;
+            case 32: eval_bits_kernel<32><<<grid, 256, 0, s>>>((const char*)pop->genes, pop->stride, pop->wvalues, pop->valid, pop->n, words, pop->nobj, *ev, only_invalid, nevals); break;
+            default: eval_bits_kernel<64><<<grid, 256, 0, s>>>((const char*)pop->genes, pop->stride, pop->wvalues, pop->valid, pop->n, words, pop->nobj, *ev, only_invalid, nevals); break;
+        }
+    } else {
+        const int q = (pop->dim + 3) / 4;
+        const int G = q <= 2 ? 2 : q <= 4 ? 4 : q <= 8 ? 8 : q <= 16 ? 16 : q <= 32 ? 32 : 64;
+        dim3 grid = grid_for(ctx, pop->n, 256 / G);
+        const int oi = only_invalid;
+        if (pop->gtype == DM_F64) {
+            switch (G) {
+                case 2: launch_eval_float<double, 2>(pop, ev, oi, nevals, grid, s); break;
+                case 4: launch_eval_float<double, 4>(pop, ev, oi, nevals, grid, s); break;
+                case 8: launch_eval_float<double, 8>(pop, ev, oi, nevals, grid, s); break;
+                case 16: launch_eval_float<double, 16>(pop, ev, oi, nevals, grid, s); break;
+                case 32: launch_eval_float<double, 32>(pop, ev, oi, nevals, grid, s); break;
+                default: launch_eval_float<double, 64>(pop, ev, oi, nevals, grid, s); break;
+            }
+        } else {
+            switch (G) {
+                case 2: launch_eval_float<float, 2>(pop, ev, oi, nevals, grid, s); break;
+                case 4: launch_eval_float<float, 4>(pop, ev, oi, nevals, grid, s); break;
+                case 8: launch_eval_float<float, 8>(pop, ev, oi, nevals, grid, s); break;
+                case 16: launch_eval_float<float, 16>(pop, ev, oi, nevals, grid, s); break;
+                case 32: launch_eval_float<float, 32>(pop, ev, oi, nevals, grid, s); break;
+                default: launch_eval_float<float, 64>(pop, ev, oi, nevals, grid, s); break;
+            }
+        }
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_sel_tournament(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t tournsize, dm_rng rng,
+                      int32_t mode, const dm_decisions* dec, int32_t* out_idx) {
+    DM_CHECK_ARG(ctx && out_idx, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0 && tournsize >= 1, "bad k / tournsize");
+    DM_CHECK_ARG(pop->n > 0 || k == 0, "cannot select from an empty population");
+    DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    int32_t* asp = nullptr;
+    if (mode != DM_RNG_NATIVE) {
+        DM_CHECK_ARG(dec && dec->aspirants, "decisions.aspirants required");
+        asp = dec->aspirants;
+    }
+    if (k == 0) return DM_OK;
+    sel_tournament_kernel<<<grid_for(ctx, k, 256), 256, 0, ctx->stream>>>(
+        pop->wvalues, pop->nobj, pop->n, k, tournsize, Rng(rng), mode, asp, out_idx);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_sel_random(dm_ctx* ctx, int64_t n, int64_t k, dm_rng rng, int32_t mode,
+                  const dm_decisions* dec, int32_t* out_idx) {
+    DM_CHECK_ARG(ctx && out_idx, "null argument");
+    DM_CHECK_ARG(k >= 0 && n >= 0 && n < (1ll << 31), "bad sizes");
+    DM_CHECK_ARG(n > 0 || k == 0, "cannot select from an empty population");
+    int32_t* asp = nullptr;
+    if (mode != DM_RNG_NATIVE) {
+        DM_CHECK_ARG(dec && dec->aspirants, "decisions.aspirants required");
+        asp = dec->aspirants;
+    }
+    if (k == 0) return DM_OK;
+    // a one-aspirant tournament never compares: it is selRandom
+    sel_tournament_kernel<<<grid_for(ctx, k, 256), 256, 0, ctx->stream>>>(
+        nullptr, 1, n, k, 1, Rng(rng), mode, asp, out_idx);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_gather(dm_ctx* ctx, const dm_pop* src, const int32_t* idx, dm_pop* dst) {
+    DM_CHECK_ARG(ctx && src && dst, "null argument");
+    int rc;
+    if ((rc = validate_pop(src, "src")) || (rc = validate_pop(dst, "dst"))) return rc;
+    DM_CHECK_ARG(src->gtype == dst->gtype && src->dim == dst->dim && src->nobj == dst->nobj,
+                 "src/dst layout mismatch");
+    if (!idx) DM_CHECK_ARG(dst->n <= src->n, "identity gather needs dst.n <= src.n");
+    if (dst->n == 0) return DM_OK;
+    const int64_t row_bytes = std::min(src->stride, dst->stride);
+    gather_kernel<16><<<grid_for(ctx, dst->n, 4), 256, 0, ctx->stream>>>(
+        (const char*)src->genes, src->wvalues, src->valid, src->stride, (char*)dst->genes,
+        dst->wvalues, dst->valid, dst->stride, idx, dst->n, row_bytes, src->nobj);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights, double* out) {
+    DM_CHECK_ARG(ctx && weights && out, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    dm_eval w{};
+    for (int o = 0; o < pop->nobj; ++o) {
+        DM_CHECK_ARG(weights[o] != 0.0, "zero fitness weight");
+        w.weights[o] = weights[o];
+    }
+    const int64_t nparts = std::min<int64_t>(std::max<int64_t>((pop->n + 4095) / 4096, 1), 512);
+    double* part = (double*)scratch(ctx, (size_t)nparts * pop->nobj * 6 * sizeof(double));
+    if (!part) return DM_ERR_NOMEM;
+    stats_kernel<<<dim3((unsigned)nparts, pop->nobj), 256, 0, ctx->stream>>>(
+        pop->wvalues, pop->valid, pop->n, pop->nobj, w, part, nparts);
+    stats_combine_kernel<<<1, 64, 0, ctx->stream>>>(part, nparts, pop->nobj, out);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+// common.hpp — shared device/host helpers for libdeapmi (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/deapmi.h"
+
+// ---------------------------------------------------------------------------
+// Error plumbing: thread-local message + status codes (no exceptions cross the
+// C ABI; the ctypes layer maps codes back to DEAP's Python exception types).
+// ---------------------------------------------------------------------------
+namespace dm {
+
+void set_error(const char* fmt, ...);
+
+#define DM_CHECK_ARG(cond, ...)                 \
+    do {                                        \
+        if (!(cond)) {                          \
+            ::dm::set_error(__VA_ARGS__);       \
+            return DM_ERR_INVALID;              \
+        }                                       \
+    } while (0)
+
+#define DM_HIP(expr)                                                          \
+    do {                                                                      \
+        hipError_t e_ = (expr);                                               \
+        if (e_ != hipSuccess) {                                               \
+            ::dm::set_error("HIP error %s at %s:%d: %s", hipGetErrorName(e_), \
+                            __FILE__, __LINE__, #expr);                       \
+            return DM_ERR_HIP;                                                \
+        }                                                                     \
+    } while (0)
+
+#define DM_LAUNCH_CHECK() DM_HIP(hipGetLastError())
+
+}  // namespace dm
+
+// Opaque context: one device, one stream, grow-only scratch arena.
+struct dm_ctx {
+    static constexpr int kSlots = 4;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* scratch[kSlots] = {nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[kSlots] = {0, 0, 0, 0};
+    void* pinned = nullptr;  // small host staging area for host-synchronising calls
+    size_t pinned_bytes = 0;
+    int num_cus = 256;
+};
+
+namespace dm {
+// Grow-only scratch arenas; returns nullptr on failure (error set).  Growing
+// a slot discards its contents.  Slot 0 = general temporaries, 1 = NSGA-II
+// dominance matrix, 2 = NSGA-II order buffers, 3 = migration.
+void* scratch_slot(dm_ctx* ctx, int slot, size_t bytes);
+inline void* scratch(dm_ctx* ctx, size_t bytes) { return scratch_slot(ctx, 0, bytes); }
+void* pinned(dm_ctx* ctx, size_t bytes);
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace dm
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  Counter layout of the whole library
+// (DESIGN.md §RNG): ctr = {item, sub, gen, (stage << 16) | island},
+// key = {seed lo, seed hi}.
+// ---------------------------------------------------------------------------
+namespace dm {
+
+enum Stage : uint32_t {
+    ST_SEL = 1,     // tournament / selRandom aspirants: item = child, sub = draw/2
+    ST_CX = 2,      // pair flag + cxTwoPoint raw cut draws: item = pair
+    ST_BLEND = 3,   // cxBlend per-gene u: item = pair, sub = gene/4
+    ST_MUT = 4,     // per-individual mutation flag: item = child
+    ST_MASK = 5,    // per-gene Bernoulli(indpb) (float genomes): sub = gene/4
+    ST_GAUSS = 6,   // per-gene normal: sub = gene
+    ST_FLIP = 7,    // packed-bit geometric skips: sub = (word << 8) | call
+    ST_VAROR = 8,   // varOr op choice + indices: item = child
+    ST_INIT = 9,    // initial population
+};
+
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c.x;
+        const uint64_t p1 = (uint64_t)M1 * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+struct Rng {
+    uint32_t k0 = 0, k1 = 0, gen = 0, island = 0;
+    Rng() = default;
+    __host__ __device__ Rng(const dm_rng& r)
+        : k0((uint32_t)r.seed), k1((uint32_t)(r.seed >> 32)), gen(r.gen), island(r.island) {}
+    __host__ __device__ __forceinline__ u32x4 operator()(uint32_t stage, uint32_t item,
+                                                         uint32_t sub) const {
+        return philox4x32_10(u32x4{item, sub, gen, (stage << 16) | (island & 0xFFFFu)}, k0, k1);
+    }
+};
+
+// Bernoulli threshold: P(w < thr) = thr / 2^32 = floor(p * 2^32) / 2^32.
+__host__ __device__ __forceinline__ uint64_t prob_threshold(double p) {
+    if (!(p > 0.0)) return 0;
+    if (p >= 1.0) return 1ull << 32;
+    return (uint64_t)(p * 4294967296.0);
+}
+// Bounded integer in [0, n) from a 64-bit word: floor(v * n / 2^64).
+// Exactly uniform when n is a power of two; otherwise bias <= n / 2^64.
+__host__ __device__ __forceinline__ uint32_t bounded64(uint32_t lo, uint32_t hi, uint32_t n) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+#ifdef __HIP_DEVICE_COMPILE__
+    return (uint32_t)__umul64hi(v, (uint64_t)n);
+#else
+    return (uint32_t)(((unsigned __int128)v * n) >> 64);
+#endif
+}
+// 32-bit uniform in [0,1): exact in fp64.
+__host__ __device__ __forceinline__ double u01_32(uint32_t w) { return (double)w * 2.3283064365386963e-10; }
+// 53-bit uniform in [0,1) from two words.
+__host__ __device__ __forceinline__ double u01_53(uint32_t lo, uint32_t hi) {
+    const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+    return (double)v * 1.1102230246251565e-16;
+}
+
+}  // namespace dm
+
+// ---------------------------------------------------------------------------
+// Wave helpers (wave64).
+// ---------------------------------------------------------------------------
+namespace dm {
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ int64_t group_sum_i(int64_t v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// DEAP Fitness.__gt__ (base.py:234-235) = not (a.wvalues <= b.wvalues), with
+// Python tuple semantics: first index whose elements are not ==, then <=.
+__host__ __device__ __forceinline__ bool fit_gt(const double* a, const double* b, int m) {
+    for (int j = 0; j < m; ++j) {
+        if (!(a[j] == b[j])) return !(a[j] <= b[j]);
+    }
+    return false;  // equal tuples: a <= b holds
+}
+// a < b lexicographic (tuple __lt__).
+__host__ __device__ __forceinline__ bool fit_lt(const double* a, const double* b, int m) {
+    for (int j = 0; j < m; ++j) {
+        if (!(a[j] == b[j])) return a[j] < b[j];
+    }
+    return false;
+}
+}  // namespace dm

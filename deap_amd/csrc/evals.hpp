@@ -1,0 +1,268 @@
+// evals.hpp — device restatements of the DEAP objective functions
+// (deap/benchmarks/__init__.py) for rows distributed over a lane group.
+//
+// Layout contract: a group of G lanes owns one genome row; in chunk c, lane
+// `sub` holds genes [c*4G + 4*sub, +4) as doubles (float rows are widened
+// exactly, as CPython does for array('f') items).  Each per-gene term below
+// evaluates the reference expression in the reference's operation order
+// (every binary op left to right, no FMA contraction: built with
+// -ffp-contract=off); only the order of the final sum differs (tree vs
+// left-to-right), which the 1e-12 relative tolerance of the parity tests
+// covers.
+#pragma once
+#include "common.hpp"
+
+namespace dm {
+
+constexpr double PI = 3.141592653589793;  // math.pi
+
+// Classification of objectives by the evaluation template they need.
+enum EvalClass { EC_NONE = 0, EC_SUM = 1, EC_MO = 2 };
+
+__host__ __device__ inline int eval_class(int fn) {
+    switch (fn) {
+        case DM_EVAL_NONE: return EC_NONE;
+        case DM_EVAL_ONEMAX:
+        case DM_EVAL_RASTRIGIN:
+        case DM_EVAL_ROSENBROCK:
+        case DM_EVAL_SPHERE: return EC_SUM;
+        default: return EC_MO;
+    }
+}
+__host__ __device__ inline int eval_nobj(const dm_eval& ev) {
+    switch (ev.fn) {
+        case DM_EVAL_NONE: return 0;
+        case DM_EVAL_ONEMAX:
+        case DM_EVAL_RASTRIGIN:
+        case DM_EVAL_ROSENBROCK:
+        case DM_EVAL_SPHERE: return 1;
+        case DM_EVAL_ZDT1:
+        case DM_EVAL_ZDT2:
+        case DM_EVAL_ZDT3:
+        case DM_EVAL_ZDT4:
+        case DM_EVAL_ZDT6: return 2;
+        default: return ev.obj;
+    }
+}
+// First gene index that enters the tail sum of a multi-objective function.
+__host__ __device__ inline int mo_tail_start(const dm_eval& ev) {
+    switch (ev.fn) {
+        case DM_EVAL_ZDT1:
+        case DM_EVAL_ZDT2:
+        case DM_EVAL_ZDT3:
+        case DM_EVAL_ZDT4:
+        case DM_EVAL_ZDT6: return 1;
+        default: return ev.obj - 1;  // DTLZ: xm = individual[obj-1:]
+    }
+}
+
+// Per-gene term of a single-objective sum (EC_SUM) for gene x.
+__device__ __forceinline__ double sum_term(int fn, double x) {
+    switch (fn) {
+        case DM_EVAL_RASTRIGIN:  // gene*gene - 10*cos(2*pi*gene)          :239-240
+            return x * x - 10.0 * cos((2.0 * PI) * x);
+        case DM_EVAL_SPHERE:  // gene*gene                                   :77
+            return x * x;
+        default:  // ONEMAX on real-valued genes: sum(individual)
+            return x;
+    }
+}
+// Rosenbrock pair term: 100*(x*x - y)**2 + (1. - x)**2                  :117-118
+__device__ __forceinline__ double rosen_term(double x, double y) {
+    const double a = x * x - y;
+    const double b = 1.0 - x;
+    return 100.0 * (a * a) + b * b;
+}
+// Tail term of the multi-objective functions.
+__device__ __forceinline__ double mo_term(int fn, double x) {
+    switch (fn) {
+        case DM_EVAL_ZDT4: {  // xi**2 - 10*cos(4*pi*xi)                    :447
+            return x * x - 10.0 * cos((4.0 * PI) * x);
+        }
+        case DM_EVAL_DTLZ1:
+        case DM_EVAL_DTLZ3: {  // (xi-0.5)**2 - cos(20*pi*(xi-0.5))    :489,:544
+            const double d = x - 0.5;
+            return d * d - cos((20.0 * PI) * d);
+        }
+        case DM_EVAL_DTLZ2:
+        case DM_EVAL_DTLZ4: {  // (xi-0.5)**2                           :518,:574
+            const double d = x - 0.5;
+            return d * d;
+        }
+        default:  // ZDT1/2/3/6: sum(individual[1:])
+            return x;
+    }
+}
+
+// Final fitness of a multi-objective function from its tail sum S and the
+// head genes x[0..7] (values, unweighted).  Writes nobj values into f.
+__device__ inline void mo_finalize(const dm_eval& ev, int n, double S, const double* h,
+                                   double* f) {
+    switch (ev.fn) {
+        case DM_EVAL_ZDT1: {  // :400-403
+            const double g = 1.0 + 9.0 * S / (double)(n - 1);
+            f[0] = h[0];
+            f[1] = g * (1.0 - sqrt(h[0] / g));
+            return;
+        }
+        case DM_EVAL_ZDT2: {  // :416-419
+            const double g = 1.0 + 9.0 * S / (double)(n - 1);
+            const double r = h[0] / g;
+            f[0] = h[0];
+            f[1] = g * (1.0 - r * r);
+            return;
+        }
+        case DM_EVAL_ZDT3: {  // :432-435
+            const double g = 1.0 + 9.0 * S / (double)(n - 1);
+            const double r = h[0] / g;
+            f[0] = h[0];
+            f[1] = g * (1.0 - sqrt(r) - r * sin((10.0 * PI) * h[0]));
+            return;
+        }
+        case DM_EVAL_ZDT4: {  // :447-450  (1 + 10*(n-1) is an int in Python)
+            const double g = (double)(1 + 10 * (n - 1)) + S;
+            f[0] = h[0];
+            f[1] = g * (1.0 - sqrt(h[0] / g));
+            return;
+        }
+        case DM_EVAL_ZDT6: {  // :462-465
+            const double g = 1.0 + 9.0 * pow(S / (double)(n - 1), 0.25);
+            const double f1 = 1.0 - exp(-4.0 * h[0]) * pow(sin((6.0 * PI) * h[0]), 6.0);
+            const double r = f1 / g;
+            f[0] = f1;
+            f[1] = g * (1.0 - r * r);
+            return;
+        }
+        case DM_EVAL_DTLZ1: {  // :489-492
+            const int M = ev.obj;
+            const double g = 100.0 * ((double)(n - (M - 1)) + S);
+            double P = 1.0;
+            for (int j = 0; j < M - 1; ++j) P = P * h[j];
+            f[0] = 0.5 * P * (1.0 + g);
+            int o = 1;
+            for (int m = M - 2; m >= 0; --m) {
+                double Pm = 1.0;
+                for (int j = 0; j < m; ++j) Pm = Pm * h[j];
+                f[o++] = 0.5 * Pm * (1.0 - h[m]) * (1.0 + g);
+            }
+            return;
+        }
+        default: {  // DTLZ2 / DTLZ3 / DTLZ4                 :516-520, :544-547, :574-576
+            const int M = ev.obj;
+            double g = S;
+            if (ev.fn == DM_EVAL_DTLZ3) g = 100.0 * ((double)(n - (M - 1)) + S);
+            double c[DM_MAX_OBJ], s[DM_MAX_OBJ];
+            for (int j = 0; j < M - 1; ++j) {
+                const double xj = (ev.fn == DM_EVAL_DTLZ4) ? pow(h[j], ev.alpha) : h[j];
+                const double ang = 0.5 * xj * PI;
+                c[j] = cos(ang);
+                s[j] = sin(ang);
+            }
+            double P = 1.0;
+            for (int j = 0; j < M - 1; ++j) P = P * c[j];
+            f[0] = (1.0 + g) * P;
+            int o = 1;
+            for (int m = M - 2; m >= 0; --m) {
+                double Pm = 1.0;
+                for (int j = 0; j < m; ++j) Pm = Pm * c[j];
+                f[o++] = (1.0 + g) * Pm * s[m];
+            }
+            return;
+        }
+    }
+}
+
+// Per-row evaluation state carried across the chunks of one row.
+struct EvalState {
+    double s;      // running per-lane partial sum
+    double carry;  // last gene of the previous chunk (Rosenbrock)
+    double head[8];
+};
+
+__device__ __forceinline__ void eval_init(EvalState& st) {
+    st.s = 0.0;
+    st.carry = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st.head[j] = 0.0;
+}
+
+// Feed one chunk of 4 genes per lane.  gbase = index of y[0] for this lane,
+// cbase = index of the chunk's first gene.  All G lanes of the group must
+// call this together (shuffles), `active` gates accumulation only.
+template <int G, int EC>
+__device__ __forceinline__ void eval_chunk(const dm_eval& ev, int dim, int gbase, int cbase,
+                                           const double (&y)[4], bool active, EvalState& st) {
+    const int lane = threadIdx.x & 63;
+    const int gl0 = lane & ~(G - 1);  // first lane of this group
+    const int sub = lane & (G - 1);
+    if constexpr (EC == EC_SUM) {
+        if (ev.fn == DM_EVAL_ROSENBROCK) {
+            const double nb = __shfl(y[0], gl0 + ((sub + 1) & (G - 1)), 64);
+            const double last = __shfl(y[3], gl0 + G - 1, 64);
+            if (active) {
+                double acc = 0.0;
+                if (sub == 0 && cbase > 0 && cbase < dim) acc += rosen_term(st.carry, y[0]);
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    if (gbase + j + 1 < dim) acc += rosen_term(y[j], y[j + 1]);
+                if (sub < G - 1 && gbase + 4 < dim) acc += rosen_term(y[3], nb);
+                st.s += acc;
+            }
+            st.carry = last;
+        } else {
+            if (active) {
+                // one (not four) inlined copy of the transcendental: keeps VGPRs low
+                double acc = 0.0;
+                const int nj = min(4, dim - gbase);
+#pragma unroll 1
+                for (int j = 0; j < nj; ++j) {
+                    const double x = j == 0 ? y[0] : j == 1 ? y[1] : j == 2 ? y[2] : y[3];
+                    acc += sum_term(ev.fn, x);
+                }
+                st.s += acc;
+            }
+        }
+    } else if constexpr (EC == EC_MO) {
+        if (cbase == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                double v;
+                switch (j & 3) {
+                    case 0: v = y[0]; break;
+                    case 1: v = y[1]; break;
+                    case 2: v = y[2]; break;
+                    default: v = y[3]; break;
+                }
+                st.head[j] = __shfl(v, gl0 + ((j >> 2) & (G - 1)), 64);
+            }
+        }
+        if (active) {
+            const int t0 = mo_tail_start(ev);
+            double acc = 0.0;
+            const int nj = min(4, dim - gbase);
+#pragma unroll 1
+            for (int j = 0; j < nj; ++j) {
+                const double x = j == 0 ? y[0] : j == 1 ? y[1] : j == 2 ? y[2] : y[3];
+                if (gbase + j >= t0) acc += mo_term(ev.fn, x);
+            }
+            st.s += acc;
+        }
+    }
+}
+
+// Reduce + finalize.  Returns nobj unweighted values in f (valid in every lane).
+template <int G, int EC>
+__device__ __forceinline__ void eval_finish(const dm_eval& ev, int dim, EvalState& st,
+                                            double* f) {
+    const double S = group_sum<G>(st.s);
+    if constexpr (EC == EC_SUM) {
+        if (ev.fn == DM_EVAL_RASTRIGIN)
+            f[0] = (double)(10 * (int64_t)dim) + S;  // 10*len(individual) + sum(...)
+        else
+            f[0] = S;
+    } else if constexpr (EC == EC_MO) {
+        mo_finalize(ev, dim, S, st.head, f);
+    }
+}
+
+}  // namespace dm

@@ -1,0 +1,136 @@
+// generation.hip — host side of the fused generation (see generation.hpp for
+// the kernels; per-genome-type instantiations live in generation_{f64,f32,bits}.hip
+// so they compile in parallel).
+#include "generation.hpp"
+
+namespace dm {
+
+// Lanes per offspring pair: enough lanes to cover the row in few chunks.
+static int pick_group_float(int dim) {
+    const int q = (dim + 3) / 4;  // lane-slots of 4 genes
+    if (q <= 4) return 4;
+    if (q <= 16) return 16;
+    return 64;
+}
+static int pick_group_bits(int words) {
+    if (words <= 2) return 2;
+    if (words <= 8) return 8;
+    return 64;
+}
+
+int validate_pop(const dm_pop* p, const char* what);
+int validate_eval(const dm_eval* ev, const dm_pop* p);
+int validate_variation(const dm_variation* v, const dm_pop* p);
+
+int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int32_t sel,
+                      int32_t tournsize, const int32_t* sel_index, const dm_variation* var,
+                      const dm_eval* ev, dm_rng rng, int32_t mode, const dm_decisions* dec,
+                      int64_t* nevals) {
+    int rc;
+    if ((rc = validate_pop(parents, "parents"))) return rc;
+    if ((rc = validate_pop(children, "children"))) return rc;
+    DM_CHECK_ARG(parents->gtype == children->gtype && parents->dim == children->dim &&
+                     parents->nobj == children->nobj,
+                 "parents and children must share genome type, dim and nobj");
+    DM_CHECK_ARG(parents->genes != children->genes, "children must not alias parents");
+    DM_CHECK_ARG(sel >= DM_SEL_IDENTITY && sel <= DM_SEL_RANDOM, "bad selection kind %d", sel);
+    if (sel == DM_SEL_IDENTITY)
+        DM_CHECK_ARG(children->n <= parents->n, "identity selection needs k <= n");
+    if (sel == DM_SEL_INDEX) DM_CHECK_ARG(sel_index != nullptr, "sel_index required");
+    if (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) {
+        DM_CHECK_ARG(parents->n > 0 && parents->n < (1ll << 31), "population size out of range");
+        if (sel == DM_SEL_TOURNAMENT) DM_CHECK_ARG(tournsize >= 1, "tournsize must be >= 1");
+        else tournsize = 1;
+    }
+    DM_CHECK_ARG(var != nullptr, "variation required");
+    if ((rc = validate_variation(var, parents))) return rc;
+    dm_eval none{};
+    if (!ev) ev = &none;
+    if ((rc = validate_eval(ev, parents))) return rc;
+    DM_CHECK_ARG(mode >= DM_RNG_NATIVE && mode <= DM_RNG_DUMP, "bad rng mode");
+    dm_decisions d{};
+    if (dec) d = *dec;
+    if (mode != DM_RNG_NATIVE) {
+        DM_CHECK_ARG(dec != nullptr, "decisions required for inject/dump");
+        if (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM)
+            DM_CHECK_ARG(d.aspirants, "decisions.aspirants required");
+        if (var->cx != DM_CX_NONE) DM_CHECK_ARG(d.cx_flag, "decisions.cx_flag required");
+        if (var->cx == DM_CX_TWOPOINT && mode == DM_RNG_INJECT)
+            DM_CHECK_ARG(d.cx_raw, "decisions.cx_raw required");
+        if (var->cx == DM_CX_BLEND) DM_CHECK_ARG(d.blend_u, "decisions.blend_u required");
+        if (var->mut != DM_MUT_NONE)
+            DM_CHECK_ARG(d.mut_flag && d.mut_mask, "decisions.mut_flag/mut_mask required");
+        if (var->mut == DM_MUT_GAUSSIAN) DM_CHECK_ARG(d.gauss, "decisions.gauss required");
+    }
+    if (children->n == 0) return DM_OK;
+    if (mode == DM_RNG_DUMP && var->mut == DM_MUT_GAUSSIAN) {
+        DM_HIP(hipMemsetAsync(d.mut_mask, 0,
+                              (size_t)children->n * ((parents->dim + 63) / 64) * 8, ctx->stream));
+    }
+
+    GenArgs a{};
+    a.pgenes = (const char*)parents->genes;
+    a.pwv = parents->wvalues;
+    a.pvalid = parents->valid;
+    a.np = parents->n;
+    a.pstride = parents->stride;
+    a.cgenes = (char*)children->genes;
+    a.cwv = children->wvalues;
+    a.cvalid = children->valid;
+    a.nc = children->n;
+    a.cstride = children->stride;
+    a.dim = parents->dim;
+    a.nobj = parents->nobj;
+    a.words64 = (parents->dim + 63) / 64;
+    a.sel = sel;
+    a.tournsize = tournsize;
+    a.sel_index = sel_index;
+    a.cx = var->cx;
+    a.mut = var->mut;
+    a.thr_cx = prob_threshold(var->cxpb);
+    a.thr_mut = prob_threshold(var->mutpb);
+    a.thr_ind = prob_threshold(var->indpb);
+    a.alpha = var->alpha;
+    a.indpb = var->indpb;
+    a.mu = var->mu;
+    a.sigma = var->sigma;
+    a.mu_vec = var->mu_vec;
+    a.sigma_vec = var->sigma_vec;
+    a.flip_inv_log2 = (var->indpb > 0.0 && var->indpb < 1.0)
+                          ? (float)(1.0 / std::log2(1.0 - var->indpb))
+                          : 0.0f;
+    a.eval_fn = ev->fn;
+    a.ev = *ev;
+    a.rng = Rng(rng);
+    a.mode = mode;
+    a.dec = d;
+    a.nevals = nevals;
+
+    const int ec = eval_class(ev->fn);
+    const int64_t npairs = (children->n + 1) / 2;
+    const int G = parents->gtype == DM_BITS ? pick_group_bits(a.words64)
+                                            : pick_group_float(parents->dim);
+    const int64_t groups_per_block = 256 / G;
+    int64_t blocks = (npairs + groups_per_block - 1) / groups_per_block;
+    blocks = std::min<int64_t>(blocks, (int64_t)ctx->num_cus * 16);
+    const dim3 grid((unsigned)std::max<int64_t>(blocks, 1));
+    if (parents->gtype == DM_BITS)
+        launch_gen_bits(a, ec, G, grid, ctx->stream);
+    else if (parents->gtype == DM_F64)
+        launch_gen_f64(a, ec, G, grid, ctx->stream);
+    else
+        launch_gen_f32(a, ec, G, grid, ctx->stream);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+}  // namespace dm
+
+extern "C" int dm_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int32_t sel,
+                             int32_t tournsize, const int32_t* sel_index,
+                             const dm_variation* var, const dm_eval* ev, dm_rng rng,
+                             int32_t mode, const dm_decisions* dec, int64_t* nevals) {
+    DM_CHECK_ARG(ctx && parents && children, "null argument");
+    return dm::launch_generation(ctx, parents, children, sel, tournsize, sel_index, var, ev, rng,
+                                 mode, dec, nevals);
+}

@@ -1,0 +1,472 @@
+// generation.hpp — fused eaSimple generation body for gfx950:
+//   selTournament / selRandom / index / identity  (selection.py:12-24, 51-69)
+//   -> toolbox.clone                              (base.py:49, algorithms.py:68)
+//   -> varAnd: pair crossover + per-child mutation (algorithms.py:33-82)
+//   -> evaluate invalid children                  (algorithms.py:171-174)
+//
+// One lane group of G lanes produces one offspring pair (children 2p, 2p+1),
+// streaming the two parent rows through registers in chunks of 4 genes per
+// lane (floats: 2x16-B or 16-B loads per lane; packed bits: one u64 word per
+// lane) so each individual-generation reads its parent genome once and writes
+// the child genome once: B = 2G + (t+1)F algorithmic bytes.
+// Randomness: Philox4x32-10 keyed by (seed, island, gen) with the counter
+// layout in common.hpp, or injected / dumped decisions (DM_RNG_INJECT/_DUMP).
+#pragma once
+#include "common.hpp"
+#include "evals.hpp"
+
+namespace dm {
+
+struct GenArgs {
+    const char* pgenes;
+    const double* pwv;
+    const uint8_t* pvalid;
+    int64_t np, pstride;
+    char* cgenes;
+    double* cwv;
+    uint8_t* cvalid;
+    int64_t nc, cstride;
+    int32_t dim, nobj, words64;  // words64 = ceil(dim/64)
+    int32_t sel, tournsize;
+    const int32_t* sel_index;
+    int32_t cx, mut;
+    uint64_t thr_cx, thr_mut, thr_ind;
+    double alpha, indpb, mu, sigma;
+    const double* mu_vec;
+    const double* sigma_vec;
+    float flip_inv_log2;  // 1 / log2(1 - indpb) for geometric skips
+    int32_t eval_fn;
+    dm_eval ev;
+    Rng rng;
+    int32_t mode;
+    dm_decisions dec;
+    int64_t* nevals;
+};
+
+// ---------------------------------------------------------------------------
+// Selection of the parent of child c (all lanes of the group compute the same
+// value; only the group leader writes dumped decisions).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t parent_of(const GenArgs& a, int64_t c, bool leader) {
+    if (a.sel == DM_SEL_IDENTITY) return c;
+    if (a.sel == DM_SEL_INDEX) return a.sel_index[c];
+    const int t = a.tournsize;
+    const int m = a.nobj;
+    int64_t best = 0;
+    for (int j = 0; j < t; ++j) {
+        int64_t cand;
+        if (a.mode == DM_RNG_INJECT) {
+            cand = a.dec.aspirants[c * t + j];
+        } else {
+            const u32x4 w = a.rng(ST_SEL, (uint32_t)c, (uint32_t)(j >> 1));
+            cand = (j & 1) ? bounded64(w.z, w.w, (uint32_t)a.np) : bounded64(w.x, w.y, (uint32_t)a.np);
+            if (a.mode == DM_RNG_DUMP && leader) a.dec.aspirants[c * t + j] = (int32_t)cand;
+        }
+        if (a.sel == DM_SEL_RANDOM) return cand;  // selRandom: k draws of one aspirant
+        if (j == 0) {
+            best = cand;
+        } else if (fit_gt(a.pwv + cand * m, a.pwv + best * m, m)) {
+            best = cand;  // max(): replace only when strictly greater  (selection.py:68)
+        }
+    }
+    return best;
+}
+
+struct PairDecisions {
+    bool cx;
+    int32_t c1, c2;  // cxTwoPoint slice [c1, c2)
+    bool mut0, mut1;
+};
+
+__device__ __forceinline__ PairDecisions pair_decisions(const GenArgs& a, int64_t p, bool has1,
+                                                        bool leader) {
+    PairDecisions d{};
+    const int64_t c0 = 2 * p, c1i = 2 * p + 1;
+    int32_t r1 = 0, r2 = 0;
+    if (has1 && a.cx != DM_CX_NONE) {
+        if (a.mode == DM_RNG_INJECT) {
+            d.cx = a.dec.cx_flag[p] != 0;
+            if (a.cx == DM_CX_TWOPOINT && d.cx) {
+                r1 = a.dec.cx_raw[2 * p];
+                r2 = a.dec.cx_raw[2 * p + 1];
+            }
+        } else {
+            const u32x4 w = a.rng(ST_CX, (uint32_t)p, 0);
+            d.cx = (uint64_t)w.x < a.thr_cx;
+            if (a.cx == DM_CX_TWOPOINT && d.cx) {
+                // randint(1, size); randint(1, size - 1)       (crossover.py:50-51)
+                const u32x4 w2 = a.rng(ST_CX, (uint32_t)p, 1);
+                r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
+                r2 = 1 + (int32_t)bounded64(w2.x, w2.y, (uint32_t)(a.dim - 1));
+            }
+            if (a.mode == DM_RNG_DUMP && leader) {
+                a.dec.cx_flag[p] = d.cx;
+                if (a.dec.cx_raw) {
+                    a.dec.cx_raw[2 * p] = r1;
+                    a.dec.cx_raw[2 * p + 1] = r2;
+                }
+            }
+        }
+        if (a.cx == DM_CX_TWOPOINT && d.cx) {
+            // if cxpoint2 >= cxpoint1: cxpoint2 += 1 else swap      (crossover.py:52-55)
+            if (r2 >= r1) {
+                r2 += 1;
+            } else {
+                const int32_t t = r1;
+                r1 = r2;
+                r2 = t;
+            }
+            d.c1 = r1;
+            d.c2 = r2;
+        }
+    }
+    if (a.mut != DM_MUT_NONE) {
+        if (a.mode == DM_RNG_INJECT) {
+            d.mut0 = a.dec.mut_flag[c0] != 0;
+            d.mut1 = has1 && a.dec.mut_flag[c1i] != 0;
+        } else {
+            d.mut0 = (uint64_t)a.rng(ST_MUT, (uint32_t)c0, 0).x < a.thr_mut;
+            d.mut1 = has1 && (uint64_t)a.rng(ST_MUT, (uint32_t)c1i, 0).x < a.thr_mut;
+            if (a.mode == DM_RNG_DUMP && leader) {
+                a.dec.mut_flag[c0] = d.mut0;
+                if (has1) a.dec.mut_flag[c1i] = d.mut1;
+            }
+        }
+    }
+    return d;
+}
+
+// ---------------------------------------------------------------------------
+// Float genomes (T = float | double): chunk = 4 genes per lane.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct Vec4;
+template <>
+struct Vec4<double> {
+    __device__ __forceinline__ static void load(const char* row, int g, double (&x)[4]) {
+        const double2* p = reinterpret_cast<const double2*>(row + (size_t)g * 8);
+        const double2 a = p[0], b = p[1];
+        x[0] = a.x;
+        x[1] = a.y;
+        x[2] = b.x;
+        x[3] = b.y;
+    }
+    __device__ __forceinline__ static void store(char* row, int g, const double (&x)[4]) {
+        double2* p = reinterpret_cast<double2*>(row + (size_t)g * 8);
+        p[0] = make_double2(x[0], x[1]);
+        p[1] = make_double2(x[2], x[3]);
+    }
+};
+template <>
+struct Vec4<float> {
+    __device__ __forceinline__ static void load(const char* row, int g, double (&x)[4]) {
+        const float4 a = *reinterpret_cast<const float4*>(row + (size_t)g * 4);
+        x[0] = a.x;
+        x[1] = a.y;
+        x[2] = a.z;
+        x[3] = a.w;
+    }
+    __device__ __forceinline__ static void store(char* row, int g, const double (&x)[4]) {
+        // array('f') semantics: fp64 arithmetic, round-to-nearest on store.
+        *reinterpret_cast<float4*>(row + (size_t)g * 4) =
+            make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
+    }
+};
+
+// Per-gene Gaussian mutation of one child's chunk (mutation.py:44-46).
+// Returns the 4-bit mask of mutated genes; the normal draws happen in
+// gauss_apply so only one inlined copy of log/cos/sqrt exists.
+__device__ __forceinline__ uint32_t gauss_mask(const GenArgs& a, int64_t c, int g) {
+    uint32_t bits = 0;
+    if (a.mode == DM_RNG_INJECT) {
+        const uint64_t word = a.dec.mut_mask[c * a.words64 + (g >> 6)];
+        bits = (uint32_t)(word >> (g & 63)) & 0xFu;
+    } else {
+        const u32x4 w = a.rng(ST_MASK, (uint32_t)c, (uint32_t)(g >> 2));
+        bits = ((uint64_t)w.x < a.thr_ind ? 1u : 0u) | ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
+               ((uint64_t)w.z < a.thr_ind ? 4u : 0u) | ((uint64_t)w.w < a.thr_ind ? 8u : 0u);
+        if (a.mode == DM_RNG_DUMP && bits) {
+            atomicOr((unsigned long long*)&a.dec.mut_mask[c * a.words64 + (g >> 6)],
+                     (unsigned long long)bits << (g & 63));
+        }
+    }
+    const int valid = a.dim - g;  // genes of this lane inside the row
+    if (valid < 4) bits &= (1u << max(valid, 0)) - 1u;
+    return bits;
+}
+__device__ __forceinline__ double gauss_value(const GenArgs& a, int64_t c, int gi) {
+    if (a.mode == DM_RNG_INJECT) return a.dec.gauss[c * a.dim + gi];
+    const u32x4 z = a.rng(ST_GAUSS, (uint32_t)c, (uint32_t)gi);
+    const double u1 = u01_53(z.x, z.y);
+    const double u2 = u01_53(z.z, z.w);
+    const double nrm = cos((2.0 * PI) * u1) * sqrt(-2.0 * log(1.0 - u2));
+    const double m = a.mu_vec ? a.mu_vec[gi] : a.mu;
+    const double s = a.sigma_vec ? a.sigma_vec[gi] : a.sigma;
+    const double gv = m + nrm * s;  // random.gauss(mu, sigma) = mu + z*sigma
+    if (a.mode == DM_RNG_DUMP) a.dec.gauss[c * a.dim + gi] = gv;
+    return gv;
+}
+// Apply the Gaussian steps of both children: bits 0-3 child 0, 4-7 child 1.
+__device__ __forceinline__ void gauss_apply(const GenArgs& a, int64_t c0, int g, uint32_t bits,
+                                            double (&y0)[4], double (&y1)[4]) {
+#pragma unroll 1
+    while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const int j = b & 3;
+        const double gv = gauss_value(a, c0 + (b >> 2), g + j);
+        if (b < 4) {
+            y0[0] = j == 0 ? y0[0] + gv : y0[0];
+            y0[1] = j == 1 ? y0[1] + gv : y0[1];
+            y0[2] = j == 2 ? y0[2] + gv : y0[2];
+            y0[3] = j == 3 ? y0[3] + gv : y0[3];
+        } else {
+            y1[0] = j == 0 ? y1[0] + gv : y1[0];
+            y1[1] = j == 1 ? y1[1] + gv : y1[1];
+            y1[2] = j == 2 ? y1[2] + gv : y1[2];
+            y1[3] = j == 3 ? y1[3] + gv : y1[3];
+        }
+    }
+}
+
+template <typename T, int G, int CX, int MUT, int EC>
+__global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & (G - 1);
+    const bool leader = sub == 0;
+    const int64_t npairs = (a.nc + 1) / 2;
+    const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / G);
+    int64_t evals = 0;
+    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; p < npairs;
+         p += gstride) {
+        const int64_t c0 = 2 * p, c1 = 2 * p + 1;
+        const bool has1 = c1 < a.nc;
+        const int64_t s0 = parent_of(a, c0, leader);
+        const int64_t s1 = has1 ? parent_of(a, c1, leader) : s0;
+        const PairDecisions d = pair_decisions(a, p, has1, leader);
+        const bool inv0 = d.cx || d.mut0 || !a.pvalid[s0];
+        const bool inv1 = has1 && (d.cx || d.mut1 || !a.pvalid[s1]);
+        const bool do_eval = EC != EC_NONE;
+
+        const char* r0 = a.pgenes + s0 * a.pstride;
+        const char* r1 = a.pgenes + s1 * a.pstride;
+        char* w0 = a.cgenes + c0 * a.cstride;
+        char* w1 = a.cgenes + c1 * a.cstride;
+        EvalState e0, e1;
+        eval_init(e0);
+        eval_init(e1);
+        const double gamma_scale = 1.0 + 2.0 * a.alpha;  // (1. + 2. * alpha)
+
+        for (int cbase = 0; cbase < a.dim; cbase += 4 * G) {
+            const int g = cbase + 4 * sub;
+            double y0[4] = {0, 0, 0, 0}, y1[4] = {0, 0, 0, 0};
+            const bool in = g < a.dim;
+            if (in) {
+                Vec4<T>::load(r0, g, y0);
+                if (has1) Vec4<T>::load(r1, g, y1);
+            }
+            if (CX == DM_CX_BLEND && d.cx && in) {
+                // gamma = (1. + 2.*alpha)*random() - alpha ; y1/y2 blend  (crossover.py:255-258)
+                double u[4];
+                if (a.mode == DM_RNG_INJECT) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        u[j] = (g + j < a.dim) ? a.dec.blend_u[p * a.dim + g + j] : 0.0;
+                } else {
+                    const u32x4 w = a.rng(ST_BLEND, (uint32_t)p, (uint32_t)(g >> 2));
+                    u[0] = u01_32(w.x);
+                    u[1] = u01_32(w.y);
+                    u[2] = u01_32(w.z);
+                    u[3] = u01_32(w.w);
+                    if (a.mode == DM_RNG_DUMP) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (g + j < a.dim) a.dec.blend_u[p * a.dim + g + j] = u[j];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (g + j < a.dim) {
+                        const double gm = gamma_scale * u[j] - a.alpha;
+                        const double x1 = y0[j], x2 = y1[j];
+                        y0[j] = (1.0 - gm) * x1 + gm * x2;
+                        y1[j] = gm * x1 + (1.0 - gm) * x2;
+                    }
+                }
+            } else if (CX == DM_CX_TWOPOINT && d.cx && in) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int gi = g + j;
+                    if (gi >= d.c1 && gi < d.c2) {
+                        const double t = y0[j];
+                        y0[j] = y1[j];
+                        y1[j] = t;
+                    }
+                }
+            }
+            if (MUT == DM_MUT_GAUSSIAN && in) {
+                uint32_t bits = 0;
+                if (d.mut0) bits |= gauss_mask(a, c0, g);
+                if (d.mut1) bits |= gauss_mask(a, c1, g) << 4;
+                gauss_apply(a, c0, g, bits, y0, y1);
+            }
+            if (in) {
+                Vec4<T>::store(w0, g, y0);
+                if (has1) Vec4<T>::store(w1, g, y1);
+            }
+            if constexpr (sizeof(T) == 4) {
+                // Evaluate the stored (fp32-rounded) genes, as DEAP reads array('f').
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    y0[j] = (double)(float)y0[j];
+                    y1[j] = (double)(float)y1[j];
+                }
+            }
+            if (do_eval) {
+                eval_chunk<G, EC>(a.ev, a.dim, g, cbase, y0, inv0, e0);
+                eval_chunk<G, EC>(a.ev, a.dim, g, cbase, y1, inv1, e1);
+            }
+        }
+        double f0[DM_MAX_OBJ], f1[DM_MAX_OBJ];
+        if (do_eval) {
+            eval_finish<G, EC>(a.ev, a.dim, e0, f0);
+            eval_finish<G, EC>(a.ev, a.dim, e1, f1);
+        }
+        if (leader) {
+            const int m = a.nobj;
+            for (int o = 0; o < m; ++o) {
+                a.cwv[c0 * m + o] = (do_eval && inv0) ? f0[o] * a.ev.weights[o] : a.pwv[s0 * m + o];
+                if (has1)
+                    a.cwv[c1 * m + o] =
+                        (do_eval && inv1) ? f1[o] * a.ev.weights[o] : a.pwv[s1 * m + o];
+            }
+            a.cvalid[c0] = do_eval ? 1 : (inv0 ? 0 : 1);
+            if (has1) a.cvalid[c1] = do_eval ? 1 : (inv1 ? 0 : 1);
+            evals += (int64_t)inv0 + (int64_t)inv1;
+        }
+    }
+    if (a.nevals && EC != EC_NONE) {
+        // one atomic per wave: sum the leaders' counts
+        int64_t tot = evals;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd((unsigned long long*)a.nevals, (unsigned long long)tot);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Packed-bit genomes: chunk = one u64 word per lane (64 genes).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, hi) of a word
+    if (hi <= lo) return 0;
+    const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+    const uint64_t dn = lo <= 0 ? 0ull : ((1ull << lo) - 1);
+    return up & ~dn;
+}
+
+// mutFlipBit on one word (mutation.py:139-141): Bernoulli(indpb) per gene.
+__device__ __forceinline__ uint64_t flip_mask_word(const GenArgs& a, int64_t c, int wi) {
+    if (a.mode == DM_RNG_INJECT) return a.dec.mut_mask[c * a.words64 + wi];
+    const int nbits = min(64, a.dim - wi * 64);
+    uint64_t mask = 0;
+    if (a.thr_ind >= (1ull << 32)) {
+        mask = nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
+    } else if (a.thr_ind > 0) {
+        // geometric skips: gap ~ floor(log2(u) / log2(1 - p)), u in (0, 1]
+        int pos = -1;
+        for (uint32_t call = 0;; ++call) {
+            const u32x4 w = a.rng(ST_FLIP, (uint32_t)c, ((uint32_t)wi << 8) | call);
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+            bool done = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!done) {
+                    const float u = ((float)ws[j] + 1.0f) * 2.3283064365386963e-10f;
+                    const float gap = floorf(__log2f(fminf(u, 1.0f)) * a.flip_inv_log2);
+                    pos += 1 + (int)fminf(gap, 64.0f);
+                    if (pos >= nbits) done = true;
+                    else mask |= 1ull << pos;
+                }
+            }
+            if (done || call >= 255) break;
+        }
+    }
+    if (a.mode == DM_RNG_DUMP) a.dec.mut_mask[c * a.words64 + wi] = mask;
+    return mask;
+}
+
+template <int G, int CX, int MUT, int EC>
+__global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & (G - 1);
+    const bool leader = sub == 0;
+    const int64_t npairs = (a.nc + 1) / 2;
+    const int64_t gstride = (int64_t)gridDim.x * (blockDim.x / G);
+    int64_t evals = 0;
+    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; p < npairs;
+         p += gstride) {
+        const int64_t c0 = 2 * p, c1 = 2 * p + 1;
+        const bool has1 = c1 < a.nc;
+        const int64_t s0 = parent_of(a, c0, leader);
+        const int64_t s1 = has1 ? parent_of(a, c1, leader) : s0;
+        const PairDecisions d = pair_decisions(a, p, has1, leader);
+        const bool inv0 = d.cx || d.mut0 || !a.pvalid[s0];
+        const bool inv1 = has1 && (d.cx || d.mut1 || !a.pvalid[s1]);
+        const uint64_t* r0 = reinterpret_cast<const uint64_t*>(a.pgenes + s0 * a.pstride);
+        const uint64_t* r1 = reinterpret_cast<const uint64_t*>(a.pgenes + s1 * a.pstride);
+        uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
+        uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
+        int64_t pc0 = 0, pc1 = 0;
+        for (int wb = 0; wb < a.words64; wb += G) {
+            const int wi = wb + sub;
+            if (wi < a.words64) {
+                uint64_t x0 = r0[wi];
+                uint64_t x1 = has1 ? r1[wi] : 0ull;
+                if (CX == DM_CX_TWOPOINT && d.cx) {
+                    const uint64_t m = range_mask(d.c1 - wi * 64, d.c2 - wi * 64);
+                    const uint64_t t = (x0 ^ x1) & m;
+                    x0 ^= t;
+                    x1 ^= t;
+                }
+                if (MUT == DM_MUT_FLIPBIT) {
+                    if (d.mut0) x0 ^= flip_mask_word(a, c0, wi);
+                    if (d.mut1) x1 ^= flip_mask_word(a, c1, wi);
+                }
+                w0[wi] = x0;
+                if (has1) w1[wi] = x1;
+                pc0 += __popcll(x0);
+                pc1 += __popcll(x1);
+            }
+        }
+        if (EC != EC_NONE) {
+            pc0 = group_sum_i<G>(pc0);
+            pc1 = group_sum_i<G>(pc1);
+        }
+        if (leader) {
+            const int m = a.nobj;
+            const bool do_eval = EC != EC_NONE;
+            for (int o = 0; o < m; ++o) {
+                a.cwv[c0 * m + o] =
+                    (do_eval && inv0) ? (double)pc0 * a.ev.weights[o] : a.pwv[s0 * m + o];
+                if (has1)
+                    a.cwv[c1 * m + o] =
+                        (do_eval && inv1) ? (double)pc1 * a.ev.weights[o] : a.pwv[s1 * m + o];
+            }
+            a.cvalid[c0] = do_eval ? 1 : (inv0 ? 0 : 1);
+            if (has1) a.cvalid[c1] = do_eval ? 1 : (inv1 ? 0 : 1);
+            evals += (int64_t)inv0 + (int64_t)inv1;
+        }
+    }
+    if (a.nevals && EC != EC_NONE) {
+        int64_t tot = evals;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0 && tot) atomicAdd((unsigned long long*)a.nevals, (unsigned long long)tot);
+    }
+}
+
+void launch_gen_f64(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_f32(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_bits(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+
+}  // namespace dm

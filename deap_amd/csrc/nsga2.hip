@@ -1,0 +1,647 @@
+// nsga2.hip — sortNondominated / assignCrowdingDist / selNSGA2
+// (deap/tools/emo.py:15-143) for gfx950.
+//
+// sortNondominated reproduces DEAP's exact front order:
+//   1. equal fitnesses are grouped (dict keyed by Fitness, first-appearance
+//      order) -> unique fits U in order of their first individual;
+//   2. the dominance relation over U is materialised as a bit matrix
+//      D[u][v] = fit_u dominates fit_v  (U x ceil(U/64) words, LDS-tiled
+//      O(M*U^2) pass) together with count[v] = #dominators of v;
+//   3. front 0 = {count == 0} in U order; front r+1 = the v whose last
+//      remaining dominators are in front r, ordered by (position in front r
+//      of the *last* dominator that releases v, U index) — the order in which
+//      the reference's peel loop appends them (emo.py:106-115).  Each peel
+//      reads the D rows of the front's members once: a wave transposes 64x64
+//      bit blocks (64 members x one 64-wide word of v) with lane shuffles and
+//      accumulates per-v dominator counts and last positions;
+//   4. unique fits expand to their individuals in population order, fronts are
+//      emitted until >= min(n, k) individuals are sorted.
+// assignCrowdingDist reproduces the reference's chained stable sorts: for
+// objective i the order is lexicographic in (v_i, v_{i-1}, ..., v_0, front
+// position), distances accumulate in objective order with IEEE division.
+#include "sort.hpp"
+
+namespace dm {
+
+int validate_pop(const dm_pop* p, const char* what);
+int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool desc,
+                    int32_t* vals_out);
+
+// ---------------------------------------------------------------------------
+// Workspace bump allocator over the context scratch
+// ---------------------------------------------------------------------------
+struct Bump {
+    char* base;
+    size_t off = 0;
+    template <typename T>
+    T* take(int64_t count) {
+        T* p = reinterpret_cast<T*>(base + off);
+        off += align_up((size_t)std::max<int64_t>(count, 1) * sizeof(T), 256);
+        return p;
+    }
+};
+
+static dim3 g1(int64_t n) {
+    return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65535)));
+}
+
+#define GRID_LOOP(i, n)                                                          \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); \
+         i += (int64_t)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------------------
+// 1. grouping of equal fitnesses
+// ---------------------------------------------------------------------------
+__global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, int64_t n,
+                                int32_t* segstart_in, int32_t* isrep) {
+    GRID_LOOP(j, n) {
+        bool start = j == 0;
+        if (!start) {
+            const double* a = wv + (int64_t)perm[j] * m;
+            const double* b = wv + (int64_t)perm[j - 1] * m;
+            for (int o = 0; o < m; ++o)
+                if (!(a[o] == b[o])) start = true;
+        }
+        segstart_in[j] = start ? (int32_t)j : 0;
+        if (start) isrep[perm[j]] = 1;
+    }
+}
+__global__ void zero_i32_kernel(int32_t* p, int64_t n) {
+    GRID_LOOP(i, n) p[i] = 0;
+}
+__global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
+    GRID_LOOP(i, n) p[i] = v;
+}
+// ui[i] = unique index of individual i; ufit / useg / gsize per unique fit.
+__global__ void unique_kernel(const double* wv, int m, const int32_t* perm, const int32_t* segstart,
+                              const int32_t* uidx_of_rep, int64_t n, int32_t* ui, double* ufit,
+                              int32_t* useg, int32_t* gsize) {
+    GRID_LOOP(j, n) {
+        const int32_t s = segstart[j];
+        const int32_t rep = perm[s];
+        const int32_t u = uidx_of_rep[rep];
+        const int32_t i = perm[j];
+        ui[i] = u;
+        atomicAdd(&gsize[u], 1);
+        if (s == j) {
+            useg[u] = (int32_t)j;
+            for (int o = 0; o < m; ++o) ufit[(int64_t)u * m + o] = wv[(int64_t)i * m + o];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2. dominance bit matrix + dominator counts
+// ---------------------------------------------------------------------------
+constexpr int DT_WORDS = 32;   // words of v per tile -> 2048 v
+constexpr int DT_ROWS = 256;   // rows u per block
+
+__global__ __launch_bounds__(256) void dom_build_kernel(const double* ufit, int m, int64_t U,
+                                                        int64_t W, uint64_t* D, int32_t* count) {
+    extern __shared__ __attribute__((aligned(16))) double sfit[];  // [m][64][DT_WORDS]
+    const int64_t w0 = (int64_t)blockIdx.x * DT_WORDS;
+    for (int e = threadIdx.x; e < m * 64 * DT_WORDS; e += blockDim.x) {
+        const int o = e / (64 * DT_WORDS);
+        const int b = (e / DT_WORDS) % 64;
+        const int wl = e % DT_WORDS;
+        const int64_t v = (w0 + wl) * 64 + b;
+        sfit[e] = v < U ? ufit[v * m + o] : __builtin_nan("");
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wl = lane & 31;
+    const int half = lane >> 5;
+    const int64_t w = w0 + wl;
+    const int64_t u_begin = (int64_t)blockIdx.y * DT_ROWS;
+    const int64_t u_end = std::min<int64_t>(U, u_begin + DT_ROWS);
+    for (int64_t u = u_begin + wave * 2 + half; u < u_end; u += 8) {
+        double fu[DM_MAX_OBJ];
+        for (int o = 0; o < m; ++o) fu[o] = ufit[u * m + o];
+        uint64_t bits = 0;
+        int cnt = 0;
+        for (int b = 0; b < 64; ++b) {
+            bool ge = true, le = true, gt = false, lt = false;
+            for (int o = 0; o < m; ++o) {
+                const double x = fu[o];
+                const double y = sfit[(o * 64 + b) * DT_WORDS + wl];
+                ge &= x >= y;
+                le &= x <= y;
+                gt |= x > y;
+                lt |= x < y;
+            }
+            bits |= (uint64_t)(ge && gt) << b;  // u dominates v     (base.py:209-224)
+            cnt += (le && lt) ? 1 : 0;          // v dominates u
+        }
+        if (w < W) D[u * W + w] = bits;
+        // reduce cnt over the 32 lanes of this half-wave
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        if (wl == 0 && cnt) atomicAdd(&count[u], cnt);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3. fronts
+// ---------------------------------------------------------------------------
+__global__ void flag_zero_count_kernel(const int32_t* count, int64_t U, int32_t* flag) {
+    GRID_LOOP(u, U) flag[u] = count[u] == 0 ? 1 : 0;
+}
+// Compaction: members in U order.  keys (optional) from key_src.
+__global__ void compact_kernel(const int32_t* flag, const int32_t* pos, int64_t U, int32_t* out,
+                               const int32_t* key_src, uint64_t* keys_out, int32_t* rankU,
+                               int32_t rank) {
+    GRID_LOOP(u, U) {
+        if (flag[u]) {
+            out[pos[u]] = (int32_t)u;
+            if (keys_out) keys_out[pos[u]] = (uint64_t)(uint32_t)key_src[u];
+            rankU[u] = rank;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int m) {
+    const uint32_t lo = __shfl_xor((uint32_t)x, m, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+// 64x64 bit transpose across the wave: in lane i bit j = A[i][j]; out lane j
+// bit i = A[i][j].
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
+    const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull,
+                               0x00FF00FF00FF00FFull, 0x0F0F0F0F0F0F0F0Full,
+                               0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const int s = 32 >> st;
+        const uint64_t mlo = masks[st];
+        const uint64_t y = shfl_xor64(x, s);
+        if (lane & s)
+            x = (x & ~mlo) | ((y & ~mlo) >> s);
+        else
+            x = (x & mlo) | ((y & mlo) << s);
+    }
+    return x;
+}
+
+constexpr int PEEL_WORDS = 16;
+
+// part_dec[c][v] = #members of chunk c dominating v; part_last[c][v] = last
+// (max) front position among them, or -1.
+__global__ __launch_bounds__(256) void peel_kernel(const uint64_t* D, int64_t W, int64_t U,
+                                                   const int32_t* members, int64_t F,
+                                                   int64_t chunk, int64_t tiles, int64_t nchunks,
+                                                   int32_t* part_dec, int32_t* part_last) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (wid >= tiles * nchunks) return;
+    const int64_t t = wid % tiles;
+    const int64_t c = wid / tiles;
+    const int64_t wbase = t * PEEL_WORDS;
+    int32_t dec[PEEL_WORDS], last[PEEL_WORDS];
+#pragma unroll
+    for (int k = 0; k < PEEL_WORDS; ++k) {
+        dec[k] = 0;
+        last[k] = -1;
+    }
+    const int64_t jb = c * chunk, je = std::min<int64_t>(F, jb + chunk);
+    for (int64_t j0 = jb; j0 < je; j0 += 64) {
+        const int64_t j = j0 + lane;
+        const bool ok = j < je;
+        const int64_t u = ok ? members[j] : 0;
+        const uint64_t* row = D + u * W;
+#pragma unroll
+        for (int k = 0; k < PEEL_WORDS; ++k) {
+            const int64_t w = wbase + k;
+            const uint64_t x = (ok && w < W) ? row[w] : 0ull;
+            const uint64_t tcol = transpose64(x, lane);  // lane b: bit i = member j0+i dominates v
+            dec[k] += __popcll(tcol);
+            if (tcol) last[k] = (int32_t)(j0 + 63 - __clzll(tcol));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PEEL_WORDS; ++k) {
+        const int64_t v = (wbase + k) * 64 + lane;
+        if (v < U) {
+            part_dec[c * U + v] = dec[k];
+            part_last[c * U + v] = last[k];
+        }
+    }
+}
+
+__global__ void peel_combine_kernel(const int32_t* part_dec, const int32_t* part_last,
+                                    int64_t nchunks, int64_t U, int32_t* count,
+                                    const int32_t* rankU, int32_t* flag, int32_t* lastpos) {
+    GRID_LOOP(v, U) {
+        int32_t dec = 0, last = -1;
+        for (int64_t c = 0; c < nchunks; ++c) {
+            dec += part_dec[c * U + v];
+            last = max(last, part_last[c * U + v]);
+        }
+        int32_t f = 0;
+        if (dec > 0 && rankU[v] < 0) {
+            const int32_t left = count[v] - dec;
+            count[v] = left;
+            if (left == 0) f = 1;
+        }
+        flag[v] = f;
+        lastpos[v] = last;
+    }
+}
+
+__global__ void sum_gsize_kernel(const int32_t* members, int64_t F, const int32_t* gsize,
+                                 int64_t* total) {
+    __shared__ int64_t sh[256];
+    int64_t acc = 0;
+    GRID_LOOP(j, F) acc += gsize[members[j]];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && sh[0]) atomicAdd((unsigned long long*)total, (unsigned long long)sh[0]);
+}
+
+// ---------------------------------------------------------------------------
+// 4. expansion to individuals
+// ---------------------------------------------------------------------------
+__global__ void member_sizes_kernel(const int32_t* ulist, int64_t T, const int32_t* gsize,
+                                    int32_t* sizes) {
+    GRID_LOOP(j, T) sizes[j] = gsize[ulist[j]];
+}
+__global__ void expand_kernel(const int32_t* ulist, int64_t T, const int32_t* outpos,
+                              const int32_t* useg, const int32_t* gsize, const int32_t* perm,
+                              int32_t* order) {
+    GRID_LOOP(j, T) {
+        const int32_t u = ulist[j];
+        const int32_t s = useg[u], g = gsize[u], o = outpos[j];
+        for (int32_t t = 0; t < g; ++t) order[o + t] = perm[s + t];
+    }
+}
+__global__ void ind_rank_kernel(const int32_t* ui, const int32_t* rankU, int64_t n, int32_t* rank) {
+    GRID_LOOP(i, n) rank[i] = rankU[ui[i]];
+}
+__global__ void front_start_kernel(const int32_t* ufront_start, int32_t nfronts,
+                                   const int32_t* outpos, int64_t T, int32_t total,
+                                   int32_t* fstart) {
+    GRID_LOOP(f, (int64_t)nfronts + 1) {
+        const int32_t us = ufront_start[f];
+        fstart[f] = us < T ? outpos[us] : total;
+    }
+}
+
+// Host-side driver ----------------------------------------------------------
+struct SortResult {
+    int64_t nsorted = 0;
+    int32_t nfronts = 0;
+};
+
+static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, bool first_only,
+                                  int32_t* order, int32_t* front_start, int32_t* rank,
+                                  SortResult* res) {
+    hipStream_t s = ctx->stream;
+    const int64_t n = pop->n;
+    const int m = pop->nobj;
+    const double* wv = pop->wvalues;
+    if (n == 0 || k == 0) {
+        res->nsorted = 0;
+        res->nfronts = 0;
+        if (rank && n) fill_i32_kernel<<<g1(n), 256, 0, s>>>(rank, n, -1);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    // ---- workspace: everything O(n) in slot 0 (U <= n), D in slot 1 ----
+    const int64_t max_chunks = 64;
+    const size_t nb8 = align_up((size_t)n * 8, 256), nb4 = align_up((size_t)(n + 2) * 4, 256);
+    const size_t need = 2 * nb8 + 16 * nb4 + align_up((size_t)n * m * 8, 256) +
+                        2 * align_up((size_t)max_chunks * n * 4, 256) +
+                        radix_sort_temp_bytes(n) + scan_temp_bytes(n) + 8192;
+    char* base = (char*)scratch(ctx, need);
+    if (!base) return DM_ERR_NOMEM;
+    int32_t* hostv = (int32_t*)pinned(ctx, 64);
+    if (!hostv) return DM_ERR_NOMEM;
+    Bump bp{base};
+    uint64_t* keys = bp.take<uint64_t>(n);
+    uint64_t* ktmp = bp.take<uint64_t>(n);
+    int32_t* perm = bp.take<int32_t>(n + 2);
+    int32_t* vtmp = bp.take<int32_t>(n + 2);
+    int32_t* segin = bp.take<int32_t>(n + 2);
+    int32_t* segstart = bp.take<int32_t>(n + 2);
+    int32_t* isrep = bp.take<int32_t>(n + 2);
+    int32_t* uidx = bp.take<int32_t>(n + 2);
+    int32_t* ui = bp.take<int32_t>(n + 2);
+    int32_t* small = bp.take<int32_t>(n + 2);  // scalars
+    void* rtemp = bp.take<char>(radix_sort_temp_bytes(n));
+    void* stemp = bp.take<char>(scan_temp_bytes(n));
+    int32_t* utotal = small;
+    int32_t* ftotal = small + 4;
+    int64_t* dtotal = (int64_t*)(small + 8);
+    // lexicographic ascending sort of wvalues (ties by index: stable)
+    int rc = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp);
+    if (rc) return rc;
+    zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
+    seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
+    if ((rc = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return rc;
+    if ((rc = exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp))) return rc;
+    DM_HIP(hipMemcpyAsync(hostv, utotal, 4, hipMemcpyDeviceToHost, s));
+    DM_HIP(hipStreamSynchronize(s));
+    const int64_t U = hostv[0];
+    const int64_t W = (U + 63) / 64;
+    const int64_t tiles = (W + PEEL_WORDS - 1) / PEEL_WORDS;
+    const double dbytes = (double)U * (double)W * 8.0;
+    DM_CHECK_ARG(dbytes < 120e9, "too many distinct fitnesses for the dominance matrix (%lld)",
+                 (long long)U);
+    double* ufit = bp.take<double>(U * m);
+    int32_t* useg = bp.take<int32_t>(U);
+    int32_t* gsize = bp.take<int32_t>(U);
+    int32_t* count = bp.take<int32_t>(U);
+    int32_t* rankU = bp.take<int32_t>(U);
+    int32_t* flag = bp.take<int32_t>(U);
+    int32_t* fpos = bp.take<int32_t>(U);
+    int32_t* lastpos = bp.take<int32_t>(U);
+    int32_t* ulist = bp.take<int32_t>(U + 2);  // unique fits in front order
+    int32_t* ufs = bp.take<int32_t>(U + 2);    // front starts in ulist
+    int32_t* outpos = bp.take<int32_t>(U + 2);
+    uint64_t* ukeys = keys;  // the n-sized key buffers are free again
+    uint64_t* uktmp = ktmp;
+    int32_t* part_dec = bp.take<int32_t>(max_chunks * U);
+    int32_t* part_last = bp.take<int32_t>(max_chunks * U);
+    void* urtemp = rtemp;
+    void* ustemp = stemp;
+    if (bp.off > need) {
+        set_error("internal workspace overflow");
+        return DM_ERR_INVALID;
+    }
+    uint64_t* D = (uint64_t*)scratch_slot(ctx, 1, (size_t)U * W * 8);
+    if (!D) return DM_ERR_NOMEM;
+
+    zero_i32_kernel<<<g1(U), 256, 0, s>>>(gsize, U);
+    zero_i32_kernel<<<g1(U), 256, 0, s>>>(count, U);
+    fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
+    unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
+    {
+        dim3 grid((unsigned)((W + DT_WORDS - 1) / DT_WORDS), (unsigned)((U + DT_ROWS - 1) / DT_ROWS));
+        const size_t lds = (size_t)m * 64 * DT_WORDS * sizeof(double);
+        dom_build_kernel<<<grid, 256, lds, s>>>(ufit, m, U, W, D, count);
+    }
+    // front 0
+    flag_zero_count_kernel<<<g1(U), 256, 0, s>>>(count, U, flag);
+    if ((rc = exclusive_scan_i32(s, flag, fpos, U, ftotal, ustemp))) return rc;
+    compact_kernel<<<g1(U), 256, 0, s>>>(flag, fpos, U, ulist, nullptr, nullptr, rankU, 0);
+    DM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
+    DM_HIP(hipMemcpyAsync(hostv, ftotal, 4, hipMemcpyDeviceToHost, s));
+    DM_HIP(hipStreamSynchronize(s));
+    int64_t F = hostv[0];
+    std::vector<int32_t> ufront{0};
+    int64_t ustart = 0;  // start of the current front in ulist
+    sum_gsize_kernel<<<g1(F), 256, 0, s>>>(ulist, F, gsize, dtotal);
+    int64_t* hostd = (int64_t*)(hostv + 8);
+    DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
+    DM_HIP(hipStreamSynchronize(s));
+    int64_t sorted_inds = hostd[0];
+    ufront.push_back((int32_t)F);
+    const int64_t N = std::min<int64_t>(n, k);
+    int32_t rnk = 0;
+    while (!first_only && sorted_inds < N && ustart + F < U && F > 0) {
+        // peel front `rnk` (ulist[ustart, ustart+F)) -> front rnk+1
+        const int64_t waves_target = 8192;
+        int64_t nchunks = std::max<int64_t>(1, std::min<int64_t>(max_chunks, waves_target / tiles));
+        nchunks = std::min<int64_t>(nchunks, (F + 63) / 64);
+        int64_t chunk = (F + nchunks - 1) / nchunks;
+        chunk = (chunk + 63) / 64 * 64;
+        nchunks = (F + chunk - 1) / chunk;
+        const int64_t waves = tiles * nchunks;
+        peel_kernel<<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(D, W, U, ulist + ustart, F, chunk,
+                                                                tiles, nchunks, part_dec,
+                                                                part_last);
+        peel_combine_kernel<<<g1(U), 256, 0, s>>>(part_dec, part_last, nchunks, U, count, rankU,
+                                                  flag, lastpos);
+        if ((rc = exclusive_scan_i32(s, flag, fpos, U, ftotal, ustemp))) return rc;
+        const int64_t nstart = ustart + F;
+        compact_kernel<<<g1(U), 256, 0, s>>>(flag, fpos, U, ulist + nstart, lastpos, ukeys, rankU,
+                                             rnk + 1);
+        DM_HIP(hipMemcpyAsync(hostv, ftotal, 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        const int64_t F2 = hostv[0];
+        if (F2 == 0) break;
+        // stable order by position of the releasing dominator (candidates are in U order)
+        int bits = 8;
+        while (bits < 32 && (1ll << bits) <= F) bits += 8;
+        if ((rc = radix_sort_pairs(s, ukeys, ulist + nstart, uktmp, vtmp, F2, 0, bits, urtemp)))
+            return rc;
+        DM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
+        sum_gsize_kernel<<<g1(F2), 256, 0, s>>>(ulist + nstart, F2, gsize, dtotal);
+        DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        sorted_inds += hostd[0];
+        ustart = nstart;
+        F = F2;
+        ++rnk;
+        ufront.push_back((int32_t)(ustart + F));
+    }
+    const int32_t nfronts = (int32_t)ufront.size() - 1;
+    const int64_t T = ufront.back();  // unique fits in emitted fronts
+    // expansion
+    DM_HIP(hipMemcpyAsync(ufs, ufront.data(), ufront.size() * 4, hipMemcpyHostToDevice, s));
+    member_sizes_kernel<<<g1(T), 256, 0, s>>>(ulist, T, gsize, flag);
+    if ((rc = exclusive_scan_i32(s, flag, outpos, T, ftotal, ustemp))) return rc;
+    expand_kernel<<<g1(T), 256, 0, s>>>(ulist, T, outpos, useg, gsize, perm, order);
+    front_start_kernel<<<g1(nfronts + 1), 256, 0, s>>>(ufs, nfronts, outpos, T,
+                                                        (int32_t)sorted_inds, front_start);
+    if (rank) {
+        // individuals outside the emitted fronts keep rankU = -1
+        ind_rank_kernel<<<g1(n), 256, 0, s>>>(ui, rankU, n, rank);
+    }
+    DM_HIP(hipStreamSynchronize(s));  // ufront host vector goes out of scope
+    res->nsorted = sorted_inds;
+    res->nfronts = nfronts;
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// crowding distance
+// ---------------------------------------------------------------------------
+__global__ void front_id_kernel(const int32_t* fstart, int32_t nf, int64_t T, int32_t* fid) {
+    GRID_LOOP(j, T) {
+        int lo = 0, hi = nf - 1;  // last f with fstart[f] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (fstart[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        fid[j] = lo;
+    }
+}
+struct Weights {
+    double w[DM_MAX_OBJ];
+};
+__global__ void crowd_key_kernel(const double* wv, int m, int obj, Weights wt, const int32_t* order,
+                                 const int32_t* pos, uint64_t* keys, int64_t T) {
+    GRID_LOOP(j, T) {
+        const int32_t ind = order[pos[j]];
+        keys[j] = ordered_key(wv[(int64_t)ind * m + obj] / wt.w[obj]);
+    }
+}
+__global__ void fid_key_kernel(const int32_t* fid, const int32_t* pos, uint64_t* keys, int64_t T) {
+    GRID_LOOP(j, T) keys[j] = (uint64_t)(uint32_t)fid[pos[j]];
+}
+__global__ void iota32_kernel(int32_t* v, int64_t n) {
+    GRID_LOOP(i, n) v[i] = (int32_t)i;
+}
+__global__ void crowd_init_kernel(const int32_t* order, int64_t T, double* crowd) {
+    GRID_LOOP(j, T) crowd[order[j]] = 0.0;
+}
+__global__ void crowd_update_kernel(const double* wv, int m, int obj, Weights wt,
+                                    const int32_t* order, const int32_t* spos,
+                                    const int32_t* fid_of_pos, const int32_t* fstart, int64_t T,
+                                    double* crowd) {
+    GRID_LOOP(j, T) {
+        const int32_t f = fid_of_pos[j];  // fronts occupy the same ranges after the sort
+        const int64_t first = fstart[f], last = fstart[f + 1] - 1;
+        const int32_t ind = order[spos[j]];
+        const double w = wt.w[obj];
+        if (j == first || j == last) {
+            crowd[ind] = INFINITY;  // distances[crowd[0][1]] = inf   (emo.py:134-135)
+            continue;
+        }
+        const double vmin = wv[(int64_t)order[spos[first]] * m + obj] / w;
+        const double vmax = wv[(int64_t)order[spos[last]] * m + obj] / w;
+        if (vmax == vmin) continue;  // emo.py:136-137
+        const double norm = (double)m * (vmax - vmin);
+        const double nxt = wv[(int64_t)order[spos[j + 1]] * m + obj] / w;
+        const double prv = wv[(int64_t)order[spos[j - 1]] * m + obj] / w;
+        crowd[ind] = crowd[ind] + (nxt - prv) / norm;
+    }
+}
+
+static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                         const int32_t* order, const int32_t* fstart_dev, int32_t nfronts,
+                         int64_t T, double* crowd) {
+    hipStream_t s = ctx->stream;
+    const int m = pop->nobj;
+    if (T <= 0 || nfronts <= 0) return DM_OK;
+    Weights wt{};
+    for (int o = 0; o < m; ++o) wt.w[o] = weights[o];
+    char* base = (char*)scratch(ctx, 2 * align_up((size_t)T * 8, 256) +
+                                         3 * align_up((size_t)T * 4, 256) +
+                                         radix_sort_temp_bytes(T) + 4096);
+    if (!base) return DM_ERR_NOMEM;
+    Bump bp{base};
+    uint64_t* keys = bp.take<uint64_t>(T);
+    uint64_t* ktmp = bp.take<uint64_t>(T);
+    int32_t* pos = bp.take<int32_t>(T);
+    int32_t* vtmp = bp.take<int32_t>(T);
+    int32_t* fid = bp.take<int32_t>(T);
+    void* rtemp = bp.take<char>(radix_sort_temp_bytes(T));
+    front_id_kernel<<<g1(T), 256, 0, s>>>(fstart_dev, nfronts, T, fid);
+    crowd_init_kernel<<<g1(T), 256, 0, s>>>(order, T, crowd);
+    int fbits = 8;
+    while (fbits < 32 && (1ll << fbits) <= nfronts) fbits += 8;
+    for (int i = 0; i < m; ++i) {
+        iota32_kernel<<<g1(T), 256, 0, s>>>(pos, T);
+        for (int o = 0; o <= i; ++o) {  // stable sorts by v_0, v_1, ..., v_i
+            crowd_key_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, o, wt, order, pos, keys, T);
+            int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, 64, rtemp);
+            if (rc) return rc;
+        }
+        fid_key_kernel<<<g1(T), 256, 0, s>>>(fid, pos, keys, T);
+        int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, fbits, rtemp);
+        if (rc) return rc;
+        crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
+                                                  fstart_dev, T, crowd);
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+__global__ void crowd_desc_key_kernel(const double* crowd, const int32_t* vals, uint64_t* keys,
+                                      int64_t T) {
+    GRID_LOOP(j, T) keys[j] = ~ordered_key(crowd[vals[j]]);
+}
+
+}  // namespace dm
+
+using namespace dm;
+
+extern "C" int dm_sort_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
+                                    int32_t first_front_only, int32_t* order,
+                                    int32_t* front_start, int32_t* rank, int64_t* nsorted,
+                                    int32_t* nfronts) {
+    DM_CHECK_ARG(ctx && order && front_start && nsorted && nfronts, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0, "negative k");
+    DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    SortResult r;
+    rc = sort_nondominated_impl(ctx, pop, k, first_front_only != 0, order, front_start, rank, &r);
+    if (rc) return rc;
+    *nsorted = r.nsorted;
+    *nfronts = r.nfronts;
+    return DM_OK;
+}
+
+extern "C" int dm_crowding_dist(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                                const int32_t* order, const int32_t* front_start, int32_t nfronts,
+                                double* crowd) {
+    DM_CHECK_ARG(ctx && pop && weights && crowd, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    if (nfronts <= 0) return DM_OK;
+    DM_CHECK_ARG(order && front_start, "null order/front_start");
+    int32_t last = 0;
+    DM_HIP(hipMemcpyAsync(&last, front_start + nfronts, 4, hipMemcpyDeviceToHost, ctx->stream));
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    return crowding_impl(ctx, pop, weights, order, front_start, nfronts, last, crowd);
+}
+
+extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weights, int64_t k,
+                            int32_t* out_idx, double* crowd) {
+    DM_CHECK_ARG(ctx && pop && weights && out_idx && crowd, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0, "negative k");
+    const int64_t n = pop->n;
+    if (n == 0 || k == 0) return DM_OK;
+    // order / front starts outlive the sort's slot-0 workspace: slot 2
+    int32_t* order = (int32_t*)scratch_slot(ctx, 2, (size_t)(2 * n + 2) * 4);
+    if (!order) return DM_ERR_NOMEM;
+    int32_t* fstart = order + n;
+    SortResult r;
+    rc = sort_nondominated_impl(ctx, pop, k, false, order, fstart, nullptr, &r);
+    if (rc) return rc;
+    rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd);
+    if (rc) return rc;
+    // host copy of front starts (small)
+    std::vector<int32_t> fs(r.nfronts + 1);
+    DM_HIP(hipMemcpyAsync(fs.data(), fstart, fs.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t chosen = r.nfronts > 0 ? fs[r.nfronts - 1] : 0;
+    if (chosen > 0)
+        DM_HIP(hipMemcpyAsync(out_idx, order, (size_t)std::min(chosen, k) * 4,
+                              hipMemcpyDeviceToDevice, ctx->stream));
+    const int64_t rem = k - chosen;
+    if (rem > 0 && r.nfronts > 0) {
+        const int64_t L = fs[r.nfronts] - chosen;  // last front size
+        char* base = (char*)scratch(ctx, 2 * align_up((size_t)L * 8, 256) +
+                                             2 * align_up((size_t)L * 4, 256) +
+                                             radix_sort_temp_bytes(L) + 4096);
+        if (!base) return DM_ERR_NOMEM;
+        Bump bp{base};
+        uint64_t* keys = bp.take<uint64_t>(L);
+        uint64_t* ktmp = bp.take<uint64_t>(L);
+        int32_t* vals = bp.take<int32_t>(L);
+        int32_t* vtmp = bp.take<int32_t>(L);
+        void* rtemp = bp.take<char>(radix_sort_temp_bytes(L));
+        DM_HIP(hipMemcpyAsync(vals, order + chosen, (size_t)L * 4, hipMemcpyDeviceToDevice,
+                              ctx->stream));
+        crowd_desc_key_kernel<<<g1(L), 256, 0, ctx->stream>>>(crowd, vals, keys, L);
+        rc = radix_sort_pairs(ctx->stream, keys, vals, ktmp, vtmp, L, 0, 64, rtemp);
+        if (rc) return rc;
+        DM_HIP(hipMemcpyAsync(out_idx + chosen, vals, (size_t)std::min(rem, L) * 4,
+                              hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}

@@ -1,0 +1,300 @@
+// sort.hip — stable LSD radix sort + scans (see sort.hpp), and the selBest /
+// selWorst entry points (deap/tools/selection.py:27-48) built on them.
+#include "sort.hpp"
+
+namespace dm {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 16;                      // rounds of 256 elements per tile
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;    // 4096 elements per block
+constexpr int RS_BINS = 256;
+
+size_t radix_sort_temp_bytes(int64_t n) {
+    const int64_t blocks = (n + RS_TILE - 1) / RS_TILE;
+    return align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256) + scan_temp_bytes(blocks * RS_BINS) +
+           align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
+}
+
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* keys, int64_t n,
+                                                             int shift, int32_t* counts,
+                                                             int64_t blocks) {
+    __shared__ int32_t h[RS_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t i = base + r * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1);
+    }
+    __syncthreads();
+    counts[(int64_t)threadIdx.x * blocks + blockIdx.x] = h[threadIdx.x];  // digit-major
+}
+
+// Stable scatter: ranks inside a round come from wave ballots; rounds are
+// processed in element order, so equal digits keep their input order.
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(
+    const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out, int32_t* vals_out,
+    int64_t n, int shift, const int32_t* offsets, int64_t blocks) {
+    __shared__ int32_t base_off[RS_BINS];
+    __shared__ int32_t wave_cnt[RS_THREADS / 64][RS_BINS];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    base_off[tid] = offsets[(int64_t)tid * blocks + blockIdx.x];
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        for (int w = 0; w < RS_THREADS / 64; ++w) wave_cnt[w][tid] = 0;
+        __syncthreads();
+        const int64_t i = base + r * RS_THREADS + tid;
+        const bool ok = i < n;
+        uint64_t k = 0;
+        int32_t v = 0;
+        int d = 0;
+        if (ok) {
+            k = keys_in[i];
+            v = vals_in[i];
+            d = (int)((k >> shift) & 0xFF);
+        }
+        // lanes with the same digit: intersect the 8 bit-planes of the digit
+        uint64_t same = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t plane = __ballot(ok && ((d >> b) & 1));
+            same &= ((d >> b) & 1) ? plane : ~plane;
+        }
+        const int rank_in_wave = __popcll(same & below);
+        const int cnt_in_wave = __popcll(same);
+        // the lowest lane of each digit group publishes the group count
+        if (ok && rank_in_wave == 0) wave_cnt[wave][d] = cnt_in_wave;
+        __syncthreads();
+        if (ok) {
+            int pos = base_off[d] + rank_in_wave;
+            for (int w = 0; w < wave; ++w) pos += wave_cnt[w][d];
+            keys_out[pos] = k;
+            vals_out[pos] = v;
+        }
+        __syncthreads();
+        // advance the per-digit running offset by this round's total
+        int add = 0;
+        for (int w = 0; w < RS_THREADS / 64; ++w) add += wave_cnt[w][tid];
+        base_off[tid] += add;
+        __syncthreads();
+    }
+}
+
+int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                     int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp) {
+    if (n <= 1) return DM_OK;
+    const int64_t blocks = (n + RS_TILE - 1) / RS_TILE;
+    char* t = (char*)temp;
+    int32_t* counts = (int32_t*)t;
+    t += align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
+    int32_t* offsets = (int32_t*)t;
+    t += align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
+    void* scan_tmp = t;
+    uint64_t* kin = keys;
+    int32_t* vin = vals;
+    uint64_t* kout = keys_tmp;
+    int32_t* vout = vals_tmp;
+    int passes = 0;
+    for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
+        rs_hist_kernel<<<(unsigned)blocks, RS_THREADS, 0, s>>>(kin, n, shift, counts, blocks);
+        int rc = exclusive_scan_i32(s, counts, offsets, blocks * RS_BINS, nullptr, scan_tmp);
+        if (rc) return rc;
+        rs_scatter_kernel<<<(unsigned)blocks, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift,
+                                                                  offsets, blocks);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+    }
+    if (passes & 1) {
+        DM_HIP(hipMemcpyAsync(keys, kin, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
+        DM_HIP(hipMemcpyAsync(vals, vin, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Scans: block-local scan -> scan of block sums -> add back.
+// ---------------------------------------------------------------------------
+constexpr int SC_THREADS = 256;
+constexpr int SC_ITEMS = 8;
+constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+
+size_t scan_temp_bytes(int64_t n) {
+    int64_t blocks = (n + SC_TILE - 1) / SC_TILE;
+    size_t b = 0;
+    while (blocks > 1) {
+        b += align_up((size_t)blocks * 8, 256) * 2;
+        blocks = (blocks + SC_TILE - 1) / SC_TILE;
+    }
+    return b + 512;
+}
+
+template <bool MAX>
+__device__ __forceinline__ int32_t op2(int32_t a, int32_t b) {
+    return MAX ? max(a, b) : a + b;
+}
+
+// Each block scans its tile; writes block aggregate.  INCL: inclusive.
+template <bool MAX, bool INCL>
+__global__ __launch_bounds__(SC_THREADS) void scan_tile_kernel(const int32_t* in, int32_t* out,
+                                                               int64_t n, int32_t* block_sums) {
+    __shared__ int32_t sh[SC_THREADS];
+    const int64_t base = (int64_t)blockIdx.x * SC_TILE + (int64_t)threadIdx.x * SC_ITEMS;
+    const int32_t ident = MAX ? INT32_MIN : 0;
+    int32_t v[SC_ITEMS];
+    int32_t acc = ident;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j;
+        v[j] = i < n ? in[i] : ident;
+        acc = op2<MAX>(acc, v[j]);
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 1; o < SC_THREADS; o <<= 1) {
+        const int32_t x = threadIdx.x >= o ? sh[threadIdx.x - o] : ident;
+        __syncthreads();
+        sh[threadIdx.x] = op2<MAX>(sh[threadIdx.x], x);
+        __syncthreads();
+    }
+    int32_t run = threadIdx.x > 0 ? sh[threadIdx.x - 1] : ident;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j;
+        const int32_t nxt = op2<MAX>(run, v[j]);
+        if (i < n) out[i] = INCL ? nxt : run;
+        run = nxt;
+    }
+    if (threadIdx.x == SC_THREADS - 1 && block_sums) block_sums[blockIdx.x] = sh[SC_THREADS - 1];
+}
+
+template <bool MAX>
+__global__ void scan_add_kernel(int32_t* out, int64_t n, const int32_t* block_prefix) {
+    const int64_t i = (int64_t)blockIdx.x * SC_TILE + (int64_t)threadIdx.x * SC_ITEMS;
+    const int32_t p = block_prefix[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j)
+        if (i + j < n) out[i + j] = op2<MAX>(out[i + j], p);
+}
+
+__global__ void scan_total_kernel(const int32_t* in, const int32_t* ex, int64_t n, int32_t* total) {
+    *total = n > 0 ? ex[n - 1] + in[n - 1] : 0;
+}
+
+template <bool MAX, bool INCL>
+static int scan_impl(hipStream_t s, const int32_t* in, int32_t* out, int64_t n, void* temp) {
+    if (n <= 0) return DM_OK;
+    const int64_t blocks = (n + SC_TILE - 1) / SC_TILE;
+    if (blocks == 1) {
+        scan_tile_kernel<MAX, INCL><<<1, SC_THREADS, 0, s>>>(in, out, n, nullptr);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    int32_t* sums = (int32_t*)temp;
+    int32_t* pref = (int32_t*)((char*)temp + align_up((size_t)blocks * 8, 256));
+    void* next = (char*)temp + 2 * align_up((size_t)blocks * 8, 256);
+    scan_tile_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums);
+    // exclusive scan of block aggregates
+    int rc = scan_impl<MAX, false>(s, sums, pref, blocks, next);
+    if (rc) return rc;
+    scan_add_kernel<MAX><<<(unsigned)blocks, SC_THREADS, 0, s>>>(out, n, pref);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int exclusive_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
+                       int32_t* total, void* temp) {
+    int rc = scan_impl<false, false>(s, in, out, n, temp);
+    if (rc) return rc;
+    if (total) {
+        if (n > 0)
+            scan_total_kernel<<<1, 1, 0, s>>>(in, out, n, total);
+        else
+            DM_HIP(hipMemsetAsync(total, 0, 4, s));
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int inclusive_max_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
+                           void* temp) {
+    return scan_impl<true, true>(s, in, out, n, temp);
+}
+
+// ---------------------------------------------------------------------------
+// selBest / selWorst: sorted(individuals, key=fitness, reverse=best)[:k]
+// ---------------------------------------------------------------------------
+__global__ void key_obj_kernel(const double* wv, int nobj, int obj, const int32_t* vals,
+                               uint64_t* keys, int64_t n, bool desc) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ordered_key(wv[(int64_t)vals[i] * nobj + obj]);
+        keys[i] = desc ? ~k : k;
+    }
+}
+__global__ void iota_kernel(int32_t* v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = (int32_t)i;
+}
+
+int validate_pop(const dm_pop* p, const char* what);
+
+// Stable lexicographic sort of rows by wvalues (asc or desc) with caller
+// buffers; the permutation ends in vals.
+int lex_sort_rows(hipStream_t s, const double* wv, int nobj, int64_t n, bool desc, uint64_t* keys,
+                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp) {
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    iota_kernel<<<g, 256, 0, s>>>(vals, n);
+    for (int o = nobj - 1; o >= 0; --o) {  // LSD over objectives: last objective first
+        key_obj_kernel<<<g, 256, 0, s>>>(wv, nobj, o, vals, keys, n, desc);
+        int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, n, 0, 64, rtemp);
+        if (rc) return rc;
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+// Same on the context scratch (slot 0); vals_out must not live in slot 0.
+int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool desc,
+                    int32_t* vals_out) {
+    const size_t kb = align_up((size_t)n * 8, 256), vb = align_up((size_t)n * 4, 256);
+    char* s = (char*)scratch(ctx, 2 * kb + vb + radix_sort_temp_bytes(n));
+    if (!s) return DM_ERR_NOMEM;
+    return lex_sort_rows(ctx->stream, wv, nobj, n, desc, (uint64_t*)s, (uint64_t*)(s + kb),
+                         vals_out, (int32_t*)(s + 2 * kb), s + 2 * kb + vb);
+}
+
+}  // namespace dm
+
+using namespace dm;
+
+static int sel_sorted(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx, bool best) {
+    DM_CHECK_ARG(ctx && out_idx, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0, "negative k");
+    k = std::min(k, pop->n);
+    if (k == 0) return DM_OK;
+    DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    int32_t* full = out_idx;
+    if (k < pop->n) {
+        full = (int32_t*)scratch_slot(ctx, 3, (size_t)pop->n * 4);
+        if (!full) return DM_ERR_NOMEM;
+    }
+    rc = sort_by_fitness(ctx, pop->wvalues, pop->nobj, pop->n, best, full);
+    if (rc) return rc;
+    if (full != out_idx)
+        DM_HIP(hipMemcpyAsync(out_idx, full, (size_t)k * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    return DM_OK;
+}
+
+extern "C" int dm_sel_best(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx) {
+    return sel_sorted(ctx, pop, k, out_idx, true);
+}
+extern "C" int dm_sel_worst(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx) {
+    return sel_sorted(ctx, pop, k, out_idx, false);
+}

@@ -1,0 +1,40 @@
+// sort.hpp — device sort / scan primitives used by selBest, NSGA-II and
+// migration: a stable LSD radix sort of (uint64 key, int32 value) pairs with
+// 8-bit digits, and int32 prefix scans.  All launches are asynchronous on the
+// given stream; temporaries come from the caller.
+#pragma once
+#include "common.hpp"
+
+namespace dm {
+
+// Order-preserving map double -> uint64 (ascending); -0.0 == +0.0 as in
+// Python's float comparison.
+__host__ __device__ __forceinline__ uint64_t ordered_key(double x) {
+    if (x == 0.0) x = 0.0;
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// Scratch needed by radix_sort_pairs for n elements.
+size_t radix_sort_temp_bytes(int64_t n);
+
+// Stable sort of (keys, vals) by keys bits [begin_bit, end_bit).  Results end
+// in keys/vals (the tmp buffers are ping-pong storage of n elements each).
+// `temp` must hold radix_sort_temp_bytes(n) bytes.
+int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                     int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp);
+
+size_t scan_temp_bytes(int64_t n);
+// out[i] = sum_{j<i} in[j] (exclusive); *total (device, may be null) = sum.
+int exclusive_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
+                       int32_t* total, void* temp);
+// out[i] = max_{j<=i} in[j] (inclusive).
+int inclusive_max_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
+                           void* temp);
+
+// Stable lexicographic sort of rows by wvalues with caller buffers.
+int lex_sort_rows(hipStream_t s, const double* wv, int nobj, int64_t n, bool desc, uint64_t* keys,
+                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp);
+
+}  // namespace dm

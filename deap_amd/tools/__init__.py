@@ -1,0 +1,20 @@
+"""Operators of ``deap.tools`` on the hot path, as device operators.
+
+Crossover: ``cxTwoPoint``, ``cxBlend``; mutation: ``mutFlipBit``,
+``mutGaussian``; selection: ``selTournament``, ``selRandom``, ``selBest``,
+``selWorst``, ``selNSGA2``, ``sortNondominated`` (``emo.assignCrowdingDist``);
+migration: ``migRing``; bookkeeping: ``Statistics``, ``MultiStatistics``,
+``Logbook``, ``HallOfFame``; initialisation: ``initPopulation``.
+"""
+from .crossover import cxBlend, cxTwoPoint
+from .emo import selNSGA2, sortNondominated
+from . import emo
+from .init import initPopulation
+from .migration import migRing
+from .mutation import mutFlipBit, mutGaussian
+from .selection import selBest, selRandom, selTournament, selWorst
+from .support import HallOfFame, Logbook, MultiStatistics, Statistics
+
+__all__ = ["cxTwoPoint", "cxBlend", "mutFlipBit", "mutGaussian", "selTournament", "selRandom",
+           "selBest", "selWorst", "selNSGA2", "sortNondominated", "migRing", "Statistics",
+           "MultiStatistics", "Logbook", "HallOfFame", "initPopulation", "emo"]

@@ -1,0 +1,127 @@
+"""NSGA-II selection core (``deap/tools/emo.py:15-143``) on device.
+
+Results are device ``int32`` index tensors in the reference's order:
+
+* :func:`sortNondominated` returns the list of fronts, each a tensor of row
+  indices in DEAP's front order (grouping of equal fitnesses by first
+  appearance, dominance peel order), truncated once ``min(n, k)`` individuals
+  are sorted;
+* :func:`assignCrowdingDist` writes ``population.crowding_dist`` (float64
+  tensor, ``fitness.crowding_dist`` of the reference);
+* :func:`selNSGA2` returns the chosen indices (fronts but the last, then the
+  last front by decreasing crowding distance, stable).
+"""
+import ctypes
+
+from .. import _lib
+from ..ops import DeviceOperator
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _check(individuals):
+    from ..device import DevicePopulation
+    if not isinstance(individuals, DevicePopulation):
+        raise TypeError("deap_amd NSGA-II operators work on a DevicePopulation, got %r"
+                        % type(individuals))
+
+
+def _weights(pop):
+    return (ctypes.c_double * pop.nobj)(*pop.weights)
+
+
+def _sort(individuals, k, first_front_only):
+    torch = _torch()
+    n = len(individuals)
+    order = torch.empty((max(n, 1),), dtype=torch.int32, device=individuals.device)
+    fstart = torch.empty((max(n, 1) + 1,), dtype=torch.int32, device=individuals.device)
+    rank = torch.empty((max(n, 1),), dtype=torch.int32, device=individuals.device)
+    nsorted = ctypes.c_int64(0)
+    nfronts = ctypes.c_int32(0)
+    ctx = individuals.ctx.bind()
+    _lib.call("dm_sort_nondominated", ctx, ctypes.byref(individuals.c_pop()), int(k),
+              int(bool(first_front_only)), ctypes.c_void_p(order.data_ptr()),
+              ctypes.c_void_p(fstart.data_ptr()), ctypes.c_void_p(rank.data_ptr()),
+              ctypes.byref(nsorted), ctypes.byref(nfronts))
+    return order, fstart, rank, nsorted.value, nfronts.value
+
+
+class _SortNondominated(DeviceOperator):
+    kind = "sort"
+
+    def __call__(self, individuals, k, first_front_only=False):
+        _check(individuals)
+        if k == 0 or len(individuals) == 0:
+            return []
+        order, fstart, _rank, _ns, nf = _sort(individuals, k, first_front_only)
+        bounds = fstart[: nf + 1].cpu().tolist()
+        return [order[bounds[f]:bounds[f + 1]] for f in range(nf)]
+
+
+class _CrowdingDist(DeviceOperator):
+    kind = "crowding"
+
+    def __call__(self, individuals, fronts=None):
+        """Crowding distance of ``individuals`` taken as one front (reference
+        semantics), or of every front in ``fronts`` (index tensors)."""
+        _check(individuals)
+        torch = _torch()
+        n = len(individuals)
+        if n == 0:
+            return
+        dev = individuals.device
+        if fronts is None:
+            order = torch.arange(n, dtype=torch.int32, device=dev)
+            fstart = torch.tensor([0, n], dtype=torch.int32, device=dev)
+            nf = 1
+        else:
+            order = torch.cat([f.to(torch.int32) for f in fronts]) if fronts else \
+                torch.empty((0,), dtype=torch.int32, device=dev)
+            sizes = [0] + [len(f) for f in fronts]
+            fstart = torch.tensor(sizes, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+            nf = len(fronts)
+        if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
+            individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
+                                                    device=dev)
+        ctx = individuals.ctx.bind()
+        _lib.call("dm_crowding_dist", ctx, ctypes.byref(individuals.c_pop()), _weights(individuals),
+                  ctypes.c_void_p(order.data_ptr()), ctypes.c_void_p(fstart.data_ptr()), nf,
+                  ctypes.c_void_p(individuals.crowding_dist.data_ptr()))
+        return individuals.crowding_dist[:n]
+
+
+class _SelNSGA2(DeviceOperator):
+    kind = "select"
+
+    def __call__(self, individuals, k, nd="standard", *, stream=None, **_):
+        _check(individuals)
+        if nd != "standard":
+            if nd == "log":
+                raise NotImplementedError("selNSGA2(nd='log') (sortLogNondominated) is not on "
+                                          "the device yet; use nd='standard'")
+            raise Exception('selNSGA2: The choice of non-dominated sorting '
+                            'method "{0}" is invalid.'.format(nd))
+        torch = _torch()
+        n = len(individuals)
+        k = int(k)
+        out = torch.empty((max(k, 1),), dtype=torch.int32, device=individuals.device)
+        if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
+            individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
+                                                    device=individuals.device)
+        if k == 0 or n == 0:
+            return out[:0]
+        ctx = individuals.ctx.bind()
+        _lib.call("dm_sel_nsga2", ctx, ctypes.byref(individuals.c_pop()), _weights(individuals), k,
+                  ctypes.c_void_p(out.data_ptr()),
+                  ctypes.c_void_p(individuals.crowding_dist.data_ptr()))
+        return out[: min(k, n)]
+
+
+sortNondominated = _SortNondominated("sortNondominated", "deap/tools/emo.py:53-117")
+assignCrowdingDist = _CrowdingDist("assignCrowdingDist", "deap/tools/emo.py:119-143")
+selNSGA2 = _SelNSGA2("selNSGA2", "deap/tools/emo.py:15-50")
+
+__all__ = ["selNSGA2", "sortNondominated"]  # assignCrowdingDist is not exported (emo.py:842-843)

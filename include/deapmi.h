@@ -1,0 +1,257 @@
+/*
+ * deapmi.h — C ABI of libdeapmi.so, the MI355X (gfx950) engine for DEAP's
+ * per-generation population hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, returns an
+ * int status (DM_OK = 0) and never throws.  On failure `dm_last_error()` holds
+ * a thread-local message.  Device buffers are owned by the caller (PyTorch
+ * tensors in the Python host layer); the library never frees or retains them.
+ * Scratch lives in the opaque `dm_ctx`, bound to one device and one stream.
+ * Every launch is asynchronous on the context's stream; no entry point below
+ * synchronises the host unless its comment says so.
+ *
+ * Each function cites the DEAP 1.3.1 interface (file:line under the reference
+ * tree) whose behaviour it reproduces at population granularity.  Randomness
+ * comes either from the counter-based Philox RNG (mode DM_RNG_NATIVE; stream
+ * layout in DESIGN.md §RNG), from caller-supplied decisions (DM_RNG_INJECT —
+ * the same pre-drawn decisions replayed into the DEAP reference give the same
+ * offspring), or natively with every decision written out (DM_RNG_DUMP).
+ */
+#ifndef DEAPMI_H
+#define DEAPMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+enum dm_status {
+    DM_OK = 0,
+    DM_ERR_INVALID = 1,   /* bad argument: maps to ValueError / TypeError  */
+    DM_ERR_INDEX = 2,     /* short mu/sigma/low/up sequence: IndexError     */
+    DM_ERR_HIP = 3,       /* HIP runtime error                               */
+    DM_ERR_NOMEM = 4,     /* scratch allocation failed                       */
+    DM_ERR_UNSUPPORTED = 5
+};
+
+/* ---- genome / operator enums -------------------------------------------- */
+enum dm_gtype { DM_BITS = 0, DM_F32 = 1, DM_F64 = 2 };
+
+enum dm_cx { DM_CX_NONE = 0, DM_CX_TWOPOINT = 1, DM_CX_BLEND = 2 };
+enum dm_mut { DM_MUT_NONE = 0, DM_MUT_FLIPBIT = 1, DM_MUT_GAUSSIAN = 2 };
+
+enum dm_sel {
+    DM_SEL_IDENTITY = 0,   /* child k <- parent k (varAnd on a population)   */
+    DM_SEL_INDEX = 1,      /* child k <- parent index[k] (any select + clone) */
+    DM_SEL_TOURNAMENT = 2, /* child k <- selTournament winner (fused)         */
+    DM_SEL_RANDOM = 3      /* child k <- selRandom draw (fused)               */
+};
+
+enum dm_eval_fn {
+    DM_EVAL_NONE = 0,
+    DM_EVAL_ONEMAX = 1,      /* README.md:85-86 sum(individual)                 */
+    DM_EVAL_RASTRIGIN = 2,   /* deap/benchmarks/__init__.py:220-240             */
+    DM_EVAL_ROSENBROCK = 3,  /* deap/benchmarks/__init__.py:98-118              */
+    DM_EVAL_ZDT1 = 4,        /* deap/benchmarks/__init__.py:391-403             */
+    DM_EVAL_ZDT2 = 5,        /* :405-419 */
+    DM_EVAL_ZDT3 = 6,        /* :421-435 */
+    DM_EVAL_ZDT4 = 7,        /* :437-450 */
+    DM_EVAL_ZDT6 = 8,        /* :452-465 */
+    DM_EVAL_DTLZ1 = 9,       /* :467-493 */
+    DM_EVAL_DTLZ2 = 10,      /* :495-521 */
+    DM_EVAL_DTLZ3 = 11,      /* :523-548 */
+    DM_EVAL_DTLZ4 = 12,      /* :550-577 */
+    DM_EVAL_SPHERE = 13      /* :62-78 (sum of squares; cheap test objective)   */
+};
+
+enum dm_rng_mode { DM_RNG_NATIVE = 0, DM_RNG_INJECT = 1, DM_RNG_DUMP = 2 };
+
+#define DM_MAX_OBJ 8
+
+/* ---- structures (all pointers are device pointers unless noted) --------- */
+
+/* Structure-of-arrays population (deap/base.py:125-270 Fitness + creator
+ * Individual types deap/creator.py:76-93).  Genome row r starts at
+ * (char*)genes + r*stride.  DM_BITS rows hold ceil(dim/64) uint64 words, gene
+ * i at word i>>6, bit i&63 (LSB first); bits >= dim are zero.  wvalues holds
+ * the *weighted* fitness (values*weights, base.py:187-198), valid[r] != 0
+ * iff the fitness is valid (base.py:226-229). */
+typedef struct dm_pop {
+    void* genes;
+    double* wvalues;   /* [n][nobj] */
+    uint8_t* valid;    /* [n]       */
+    int64_t n;
+    int64_t stride;    /* bytes per genome row, multiple of 16 */
+    int32_t dim;
+    int32_t gtype;     /* enum dm_gtype */
+    int32_t nobj;
+    int32_t reserved;
+} dm_pop;
+
+/* Objective function + the fitness weights it is stored under. */
+typedef struct dm_eval {
+    int32_t fn;        /* enum dm_eval_fn */
+    int32_t obj;       /* number of objectives for DTLZ (its `obj` argument) */
+    double alpha;      /* DTLZ4 alpha */
+    double weights[DM_MAX_OBJ];
+} dm_eval;
+
+/* Variation parameters: varAnd/varOr probabilities plus the registered
+ * mate/mutate partial keywords (crossover.py:37-60,241-260;
+ * mutation.py:17-48,124-142). */
+typedef struct dm_variation {
+    int32_t cx;        /* enum dm_cx  */
+    int32_t mut;       /* enum dm_mut */
+    double cxpb;
+    double mutpb;
+    double alpha;      /* cxBlend */
+    double indpb;      /* mutFlipBit / mutGaussian */
+    double mu;         /* mutGaussian scalar mean  (used when mu_vec == NULL)    */
+    double sigma;      /* mutGaussian scalar sigma (used when sigma_vec == NULL) */
+    const double* mu_vec;    /* optional device [dim] */
+    const double* sigma_vec; /* optional device [dim] */
+} dm_variation;
+
+/* Counter-based RNG coordinates: (seed, island, generation) select the
+ * stream; stage/individual/gene select the word. */
+typedef struct dm_rng {
+    uint64_t seed;
+    uint32_t island;
+    uint32_t gen;
+} dm_rng;
+
+/* Pre-drawn random decisions in DEAP's vocabulary.  INJECT reads them,
+ * DUMP writes them; any pointer may be NULL when the operator is unused.
+ * Shapes refer to the number of children k and genes dim. */
+typedef struct dm_decisions {
+    int32_t* aspirants; /* [k][tournsize] selRandom indices (selection.py:24) */
+    uint8_t* cx_flag;   /* [k/2] random() < cxpb           (algorithms.py:72) */
+    int32_t* cx_raw;    /* [k/2][2] raw randint(1,size), randint(1,size-1)  */
+    double* blend_u;    /* [k/2][dim] random() per gene (crossover.py:256)  */
+    uint8_t* mut_flag;  /* [k] random() < mutpb            (algorithms.py:78) */
+    uint64_t* mut_mask; /* [k][ceil(dim/64)] per-gene random() < indpb      */
+    double* gauss;      /* [k][dim] random.gauss(mu,sigma) where masked     */
+    int32_t* varor_op;  /* [k] 0 = crossover, 1 = mutation, 2 = reproduction */
+    int32_t* varor_idx; /* [k][2] random.sample / random.choice indices      */
+} dm_decisions;
+
+typedef struct dm_ctx dm_ctx;
+
+/* ---- context ------------------------------------------------------------- */
+const char* dm_last_error(void);
+const char* dm_version(void);
+int dm_ctx_create(int device, void* hip_stream, dm_ctx** out);
+int dm_ctx_destroy(dm_ctx* ctx);
+int dm_ctx_set_stream(dm_ctx* ctx, void* hip_stream);
+int dm_ctx_sync(dm_ctx* ctx);  /* hipStreamSynchronize on the ctx stream */
+
+/* ---- RNG (test + init) ---------------------------------------------------- */
+/* Raw Philox4x32-10 blocks: out[i*4..i*4+3] = philox(ctr_i, key) with
+ * ctr_i = {ctr0[0]+i, ctr0[1], ctr0[2], ctr0[3]}. */
+int dm_philox_blocks(dm_ctx* ctx, const uint32_t ctr0[4], const uint32_t key[2],
+                     int64_t nblocks, uint32_t* out);
+
+/* Population initialisation (tools.initRepeat/initIterate stand-in,
+ * deap/tools/init.py:3-51): bits i.i.d. Bernoulli(1/2), floats U[low, high).
+ * Marks every fitness invalid. */
+int dm_init_uniform(dm_ctx* ctx, dm_pop* pop, double low, double high, dm_rng rng);
+
+/* ---- evaluation ------------------------------------------------------------ */
+/* toolbox.map(toolbox.evaluate, invalid_ind) + fitness.values = fit
+ * (algorithms.py:149-152 / :171-174).  only_invalid != 0 evaluates rows
+ * with valid == 0 only; *nevals (device int64, may be NULL) is incremented
+ * by the number of rows evaluated. */
+int dm_evaluate(dm_ctx* ctx, dm_pop* pop, const dm_eval* ev, int only_invalid,
+                int64_t* nevals);
+
+/* ---- selection ------------------------------------------------------------- */
+/* selTournament (selection.py:51-69): out_idx[k] = winner of tournsize
+ * aspirants (selRandom, :12-24); ties keep the first-drawn aspirant,
+ * comparison is DEAP's lexicographic Fitness.__gt__ on wvalues. */
+int dm_sel_tournament(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t tournsize,
+                      dm_rng rng, int32_t mode, const dm_decisions* dec,
+                      int32_t* out_idx);
+/* selRandom (selection.py:12-24). */
+int dm_sel_random(dm_ctx* ctx, int64_t n, int64_t k, dm_rng rng, int32_t mode,
+                  const dm_decisions* dec, int32_t* out_idx);
+/* selBest (selection.py:27-36): indices of the k best, stable (ties by
+ * ascending index), via a device sort of the lexicographic wvalues. */
+int dm_sel_best(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx);
+/* selWorst (selection.py:39-48), same machinery ascending. */
+int dm_sel_worst(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx);
+
+/* toolbox.clone over a selection (base.py:49, algorithms.py:68):
+ * dst row r <- src row idx[r] (genome, wvalues, valid). */
+int dm_gather(dm_ctx* ctx, const dm_pop* src, const int32_t* idx, dm_pop* dst);
+
+/* ---- variation / fused generation ----------------------------------------- */
+/* One eaSimple generation body (algorithms.py:163-181), fused:
+ *   select (per `sel`) -> clone -> varAnd (algorithms.py:33-82) -> evaluate
+ *   invalid children (per `ev`, fn NONE = leave them invalid).
+ * children->n offspring are produced (children may not alias parents).
+ * sel_index is used for DM_SEL_INDEX.  *nevals += #invalid children. */
+int dm_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children,
+                  int32_t sel, int32_t tournsize, const int32_t* sel_index,
+                  const dm_variation* var, const dm_eval* ev, dm_rng rng,
+                  int32_t mode, const dm_decisions* dec, int64_t* nevals);
+
+/* varOr (algorithms.py:192-245): children->n = lambda offspring from
+ * parents, optionally evaluated.  Requires cxpb + mutpb <= 1. */
+int dm_var_or(dm_ctx* ctx, const dm_pop* parents, dm_pop* children,
+              const dm_variation* var, const dm_eval* ev, dm_rng rng,
+              int32_t mode, const dm_decisions* dec, int64_t* nevals);
+
+/* ---- multi-objective selection (deap/tools/emo.py) ----------------------- */
+/* sortNondominated (emo.py:53-117).  Outputs, over the n individuals of pop:
+ *   order[0..nsorted)   individual indices in DEAP's front order;
+ *   front_start[0..nfronts]  offsets into order (front f = order[fs[f]..fs[f+1]));
+ *   rank[n]             front index, or -1 if not sorted (truncated).
+ * Sorting stops once >= min(n, k) individuals are placed (or after the first
+ * front if first_front_only).  Host-synchronising (front count is data
+ * dependent).  *nsorted / *nfronts are host pointers. */
+int dm_sort_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
+                         int32_t first_front_only, int32_t* order,
+                         int32_t* front_start, int32_t* rank,
+                         int64_t* nsorted, int32_t* nfronts);
+/* assignCrowdingDist (emo.py:119-143) on every front of a sorted order:
+ * crowd[order[j]] = crowding distance within its front (weights unapply
+ * values = wvalues / weights as in base.py:184-185). weights: host [nobj]. */
+int dm_crowding_dist(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                     const int32_t* order, const int32_t* front_start,
+                     int32_t nfronts, double* crowd);
+/* selNSGA2 (emo.py:15-50), nd='standard': out_idx[k] chosen indices in
+ * DEAP's order; crowd[n] receives fitness.crowding_dist of sorted rows.
+ * Host-synchronising. */
+int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                 int64_t k, int32_t* out_idx, double* crowd);
+
+/* ---- island migration (deap/tools/migration.py:4-51) --------------------- */
+/* Pack rows idx[0..k) of pop into a contiguous emigrant block:
+ * [k][stride] genomes, then [k][nobj] wvalues, then [k] valid (padded to 8 B),
+ * then [k] int32 source row indices.  dm_pack_bytes gives its size. */
+int dm_pack_rows(dm_ctx* ctx, const dm_pop* pop, const int32_t* idx, int64_t k,
+                 void* block);
+int64_t dm_pack_bytes(const dm_pop* pop, int64_t k);
+/* migRing placement for one receiving deme (migration.py:48-51): for j in
+ * 0..k-1 in order, slot = first row of the *current* deme whose genome equals
+ * immigrant j (list.index value equality), then that row <- emigrant j.
+ * immigrants: rows of `pop` as selected before any placement (idx[k]);
+ * emigrants: a packed block from dm_pack_rows.  out_slots[k] (device) gets the
+ * slots written.  An immigrant absent from the deme is DM_ERR_INVALID (the
+ * reference's list.index ValueError).  Host-synchronising. */
+int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
+                 const void* emigrant_block, int64_t k, int32_t* out_slots);
+
+/* ---- statistics (tools.Statistics / Logbook helpers) --------------------- */
+/* Per objective j: out[j*6 + {0..5}] = {min, max, sum, sumsq, argmin, argmax}
+ * of fitness.values (= wvalues / weights) over valid rows (device doubles).
+ * weights: host [nobj]. */
+int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                     double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEAPMI_H */

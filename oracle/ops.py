@@ -1,0 +1,435 @@
+"""Decision-replay restatement of DEAP's hot path — TEST INFRASTRUCTURE ONLY
+(see oracle/__init__.py; never imported by deap_amd).
+
+Populations are plain numpy arrays: ``genes [n, dim]`` (uint8 0/1 for binary
+genomes, float64 / float32 otherwise), ``wvalues [n, m]`` float64 (weighted
+fitness, ``deap/base.py:187-198``) and ``valid [n]`` bool.  Randomness enters
+only through explicit decision arrays (vocabulary of ``deap_amd/decisions.py``)
+so the same decisions replayed into DEAP (``tests/golden/make_golden.py``) and
+into the GPU must give identical outputs.
+
+Per-gene arithmetic follows the reference expressions operation by operation
+with Python floats (``math``), i.e. glibc libm — the same values DEAP computes.
+"""
+import math
+from collections import defaultdict
+
+import numpy as np
+
+
+# ---------------------------------------------------------------------------
+# Fitness comparisons (deap/base.py:209-250)
+# ---------------------------------------------------------------------------
+def fit_gt(a, b):
+    """Fitness.__gt__ = not (a.wvalues <= b.wvalues)           (base.py:234-244)"""
+    return not (tuple(a) <= tuple(b))
+
+
+def dominates(a, b):
+    """Fitness.dominates on wvalues                            (base.py:209-224)"""
+    not_equal = False
+    for x, y in zip(a, b):
+        if x > y:
+            not_equal = True
+        elif x < y:
+            return False
+    return not_equal
+
+
+# ---------------------------------------------------------------------------
+# Objective functions (deap/benchmarks/__init__.py) on one genome (list)
+# ---------------------------------------------------------------------------
+def onemax(ind):
+    """README.md:85-86"""
+    return (sum(ind),)
+
+
+def rastrigin(ind):
+    """benchmarks/__init__.py:239-240"""
+    return (10 * len(ind) + sum(g * g - 10 * math.cos(2 * math.pi * g) for g in ind),)
+
+
+def rosenbrock(ind):
+    """benchmarks/__init__.py:117-118"""
+    return (sum(100 * (x * x - y) ** 2 + (1. - x) ** 2 for x, y in zip(ind[:-1], ind[1:])),)
+
+
+def sphere(ind):
+    """benchmarks/__init__.py:77"""
+    return (sum(g * g for g in ind),)
+
+
+def zdt1(ind):
+    """benchmarks/__init__.py:400-403"""
+    g = 1.0 + 9.0 * sum(ind[1:]) / (len(ind) - 1)
+    f1 = ind[0]
+    return f1, g * (1 - math.sqrt(f1 / g))
+
+
+def zdt2(ind):
+    """benchmarks/__init__.py:416-419"""
+    g = 1.0 + 9.0 * sum(ind[1:]) / (len(ind) - 1)
+    f1 = ind[0]
+    return f1, g * (1 - (f1 / g) ** 2)
+
+
+def zdt3(ind):
+    """benchmarks/__init__.py:432-435"""
+    g = 1.0 + 9.0 * sum(ind[1:]) / (len(ind) - 1)
+    f1 = ind[0]
+    return f1, g * (1 - math.sqrt(f1 / g) - f1 / g * math.sin(10 * math.pi * f1))
+
+
+def zdt4(ind):
+    """benchmarks/__init__.py:447-450"""
+    g = 1 + 10 * (len(ind) - 1) + sum(xi ** 2 - 10 * math.cos(4 * math.pi * xi) for xi in ind[1:])
+    f1 = ind[0]
+    return f1, g * (1 - math.sqrt(f1 / g))
+
+
+def zdt6(ind):
+    """benchmarks/__init__.py:462-465"""
+    g = 1 + 9 * (sum(ind[1:]) / (len(ind) - 1)) ** 0.25
+    f1 = 1 - math.exp(-4 * ind[0]) * math.sin(6 * math.pi * ind[0]) ** 6
+    return f1, g * (1 - (f1 / g) ** 2)
+
+
+def _prod(xs, start):
+    acc = start
+    for x in xs:
+        acc = acc * x
+    return acc
+
+
+def dtlz1(ind, obj):
+    """benchmarks/__init__.py:489-493"""
+    xm = ind[obj - 1:]
+    g = 100 * (len(xm) + sum((xi - 0.5) ** 2 - math.cos(20 * math.pi * (xi - 0.5)) for xi in xm))
+    f = [0.5 * _prod(ind[:obj - 1], 1) * (1 + g)]
+    f.extend(0.5 * _prod(ind[:m], 1) * (1 - ind[m]) * (1 + g) for m in reversed(range(obj - 1)))
+    return tuple(f)
+
+
+def _dtlz2_like(ind, obj, g, alpha=None):
+    xc = ind[:obj - 1]
+    tr = (lambda x: x) if alpha is None else (lambda x: x ** alpha)
+    f = [(1.0 + g) * _prod((math.cos(0.5 * tr(xi) * math.pi) for xi in xc), 1.0)]
+    f.extend((1.0 + g) * _prod((math.cos(0.5 * tr(xi) * math.pi) for xi in xc[:m]), 1)
+             * math.sin(0.5 * tr(xc[m]) * math.pi) for m in range(obj - 2, -1, -1))
+    return tuple(f)
+
+
+def dtlz2(ind, obj):
+    """benchmarks/__init__.py:516-521"""
+    return _dtlz2_like(ind, obj, sum((xi - 0.5) ** 2 for xi in ind[obj - 1:]))
+
+
+def dtlz3(ind, obj):
+    """benchmarks/__init__.py:544-548"""
+    xm = ind[obj - 1:]
+    g = 100 * (len(xm) + sum((xi - 0.5) ** 2 - math.cos(20 * math.pi * (xi - 0.5)) for xi in xm))
+    return _dtlz2_like(ind, obj, g)
+
+
+def dtlz4(ind, obj, alpha):
+    """benchmarks/__init__.py:574-577"""
+    return _dtlz2_like(ind, obj, sum((xi - 0.5) ** 2 for xi in ind[obj - 1:]), alpha)
+
+
+OBJECTIVES = {"onemax": onemax, "rastrigin": rastrigin, "rosenbrock": rosenbrock,
+              "sphere": sphere, "zdt1": zdt1, "zdt2": zdt2, "zdt3": zdt3, "zdt4": zdt4,
+              "zdt6": zdt6, "dtlz1": dtlz1, "dtlz2": dtlz2, "dtlz3": dtlz3, "dtlz4": dtlz4}
+
+
+def _row(genes, i):
+    r = genes[i]
+    if r.dtype == np.uint8:
+        return [int(x) for x in r]
+    return [float(x) for x in r]  # float32 widened exactly, as array('f') items
+
+
+def evaluate(genes, name, weights, rows=None, **kw):
+    """fitness.values = evaluate(ind) for each row -> wvalues (values*weights)."""
+    fn = OBJECTIVES[name]
+    n = genes.shape[0]
+    rows = range(n) if rows is None else rows
+    out = np.zeros((n, len(weights)), np.float64)
+    for i in rows:
+        vals = fn(_row(genes, i), **kw)
+        out[i] = [v * w for v, w in zip(vals, weights)]
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Selection (deap/tools/selection.py)
+# ---------------------------------------------------------------------------
+def sel_tournament(wvalues, aspirants):
+    """selTournament with pre-drawn selRandom indices aspirants[k][t]
+    (selection.py:51-69): max(aspirants, key=fitness) keeps the first-drawn
+    aspirant among equals."""
+    out = np.empty(len(aspirants), np.int64)
+    for c, asp in enumerate(aspirants):
+        best = int(asp[0])
+        for a in asp[1:]:
+            if fit_gt(wvalues[int(a)], wvalues[best]):
+                best = int(a)
+        out[c] = best
+    return out
+
+
+def sel_best(wvalues, k):
+    """sorted(individuals, key=fitness, reverse=True)[:k]        (selection.py:27-36)"""
+    order = sorted(range(len(wvalues)), key=lambda i: tuple(wvalues[i]), reverse=True)
+    return np.array(order[:k], np.int64)
+
+
+def sel_worst(wvalues, k):
+    """sorted(individuals, key=fitness)[:k]                        (selection.py:39-48)"""
+    order = sorted(range(len(wvalues)), key=lambda i: tuple(wvalues[i]))
+    return np.array(order[:k], np.int64)
+
+
+# ---------------------------------------------------------------------------
+# Variation (deap/algorithms.py:33-82, crossover.py, mutation.py)
+# ---------------------------------------------------------------------------
+def cx_two_point(a, b, r1, r2):
+    """cxTwoPoint with raw draws r1=randint(1,size), r2=randint(1,size-1)
+    (crossover.py:49-60)."""
+    c1, c2 = int(r1), int(r2)
+    if c2 >= c1:
+        c2 += 1
+    else:
+        c1, c2 = c2, c1
+    a[c1:c2], b[c1:c2] = b[c1:c2].copy(), a[c1:c2].copy()
+
+
+def cx_blend(a, b, u, alpha, store):
+    """cxBlend with per-gene random() u (crossover.py:255-258)."""
+    for i in range(min(len(a), len(b))):
+        x1, x2 = float(a[i]), float(b[i])
+        gamma = (1. + 2. * alpha) * float(u[i]) - alpha
+        a[i] = store((1. - gamma) * x1 + gamma * x2)
+        b[i] = store(gamma * x1 + (1. - gamma) * x2)
+
+
+def mut_flip_bit(x, mask):
+    """mutFlipBit with per-gene mask (mutation.py:139-141)."""
+    for i in np.nonzero(mask)[0]:
+        x[i] = 0 if x[i] else 1
+
+
+def mut_gaussian(x, mask, gauss, store):
+    """mutGaussian with per-gene mask and the random.gauss values (mutation.py:44-46)."""
+    for i in np.nonzero(mask)[0]:
+        x[i] = store(float(x[i]) + float(gauss[i]))
+
+
+def _store_for(genes):
+    if genes.dtype == np.float32:
+        return lambda v: np.float32(v)  # array('f'): round to nearest on store
+    if genes.dtype == np.uint8:
+        return int
+    return float
+
+
+def unpack_mask(words, dim):
+    words = np.ascontiguousarray(np.asarray(words, dtype=np.uint64))
+    by = words.view(np.uint8).reshape(words.shape[0], -1)
+    return np.unpackbits(by, axis=1, bitorder="little")[:, :dim].astype(bool)
+
+
+def var_and(genes, wvalues, valid, cxpb, mutpb, cx, mut, dec, alpha=0.5):
+    """varAnd (algorithms.py:33-82) replaying decisions:
+    dec: cx_flag[k//2], cx_raw[k//2][2] | blend_u[k//2][dim], mut_flag[k],
+    mut_mask[k][dim] (bool), gauss[k][dim].  Returns (genes, wvalues, valid)
+    of the offspring (cloned)."""
+    g = genes.copy()
+    wv = wvalues.copy()
+    ok = valid.copy().astype(bool)
+    store = _store_for(g)
+    n = g.shape[0]
+    for i in range(1, n, 2):
+        p = (i - 1) // 2
+        if cx is not None and dec["cx_flag"][p]:
+            if cx == "twopoint":
+                cx_two_point(g[i - 1], g[i], *dec["cx_raw"][p])
+            else:
+                cx_blend(g[i - 1], g[i], dec["blend_u"][p], alpha, store)
+            ok[i - 1] = ok[i] = False
+    for i in range(n):
+        if mut is not None and dec["mut_flag"][i]:
+            if mut == "flipbit":
+                mut_flip_bit(g[i], dec["mut_mask"][i])
+            else:
+                mut_gaussian(g[i], dec["mut_mask"][i], dec["gauss"][i], store)
+            ok[i] = False
+    return g, wv, ok
+
+
+def ea_generation(genes, wvalues, valid, cxpb, mutpb, cx, mut, dec, objective, weights,
+                  alpha=0.5, obj_kw=None):
+    """One eaSimple generation body (algorithms.py:163-181): selTournament
+    (aspirants from dec) -> clone -> varAnd -> evaluate invalid.
+    Returns (genes, wvalues, valid, nevals)."""
+    idx = sel_tournament(wvalues, dec["aspirants"])
+    g, wv, ok = var_and(genes[idx], wvalues[idx], valid[idx], cxpb, mutpb, cx, mut, dec, alpha)
+    inv = np.nonzero(~ok)[0]
+    if objective is not None:
+        ev = evaluate(g, objective, weights, rows=inv, **(obj_kw or {}))
+        wv[inv] = ev[inv]
+        ok[inv] = True
+    return g, wv, ok, len(inv)
+
+
+def var_or(genes, wvalues, valid, lambda_, cxpb, mutpb, cx, mut, dec, alpha=0.5):
+    """varOr (algorithms.py:229-245): dec varor_op[k] (0 cx / 1 mut / 2 repro),
+    varor_idx[k][2], plus cx_raw / blend_u / mut_mask / gauss indexed by child."""
+    store = _store_for(genes)
+    dim = genes.shape[1]
+    g = np.zeros((lambda_, dim), genes.dtype)
+    wv = np.zeros((lambda_, wvalues.shape[1]), np.float64)
+    ok = np.zeros(lambda_, bool)
+    for c in range(lambda_):
+        op = int(dec["varor_op"][c])
+        a, b = (int(x) for x in dec["varor_idx"][c])
+        if op == 0:
+            x1, x2 = genes[a].copy(), genes[b].copy()
+            if cx == "twopoint":
+                cx_two_point(x1, x2, *dec["cx_raw"][c])
+            else:
+                cx_blend(x1, x2, dec["blend_u"][c], alpha, store)
+            g[c] = x1
+        elif op == 1:
+            x = genes[a].copy()
+            if mut == "flipbit":
+                mut_flip_bit(x, dec["mut_mask"][c])
+            else:
+                mut_gaussian(x, dec["mut_mask"][c], dec["gauss"][c], store)
+            g[c] = x
+        else:
+            g[c] = genes[a]
+            wv[c] = wvalues[a]
+            ok[c] = valid[a]
+    return g, wv, ok
+
+
+# ---------------------------------------------------------------------------
+# NSGA-II (deap/tools/emo.py:15-143)
+# ---------------------------------------------------------------------------
+def sort_nondominated(wvalues, k, first_front_only=False):
+    """emo.py:53-117 restated over row indices: returns list of fronts (lists
+    of indices) in the reference's order."""
+    if k == 0:
+        return []
+    map_fit_ind = defaultdict(list)
+    keys = []
+    for i, w in enumerate(wvalues):
+        key = tuple(float(x) + 0.0 for x in w)  # -0.0 and 0.0 are one dict key
+        if key not in map_fit_ind:
+            keys.append(key)
+        map_fit_ind[key].append(i)
+    fits = keys  # first-appearance order, as dict.keys() of the reference
+    current_front, next_front = [], []
+    dominating_fits = defaultdict(int)
+    dominated_fits = defaultdict(list)
+    for i, fit_i in enumerate(fits):
+        for fit_j in fits[i + 1:]:
+            if dominates(fit_i, fit_j):
+                dominating_fits[fit_j] += 1
+                dominated_fits[fit_i].append(fit_j)
+            elif dominates(fit_j, fit_i):
+                dominating_fits[fit_i] += 1
+                dominated_fits[fit_j].append(fit_i)
+        if dominating_fits[fit_i] == 0:
+            current_front.append(fit_i)
+    fronts = [[]]
+    for fit in current_front:
+        fronts[-1].extend(map_fit_ind[fit])
+    pareto_sorted = len(fronts[-1])
+    if not first_front_only:
+        N = min(len(wvalues), k)
+        while pareto_sorted < N:
+            fronts.append([])
+            for fit_p in current_front:
+                for fit_d in dominated_fits[fit_p]:
+                    dominating_fits[fit_d] -= 1
+                    if dominating_fits[fit_d] == 0:
+                        next_front.append(fit_d)
+                        pareto_sorted += len(map_fit_ind[fit_d])
+                        fronts[-1].extend(map_fit_ind[fit_d])
+            current_front = next_front
+            next_front = []
+    return fronts
+
+
+def assign_crowding_dist(values):
+    """emo.py:119-143 on one front; values = fitness.values rows (unweighted)
+    in front order.  Returns the distances in the same order."""
+    n = len(values)
+    if n == 0:
+        return []
+    distances = [0.0] * n
+    crowd = [(tuple(float(x) for x in values[i]), i) for i in range(n)]
+    nobj = len(values[0])
+    for i in range(nobj):
+        crowd.sort(key=lambda element: element[0][i])
+        distances[crowd[0][1]] = float("inf")
+        distances[crowd[-1][1]] = float("inf")
+        if crowd[-1][0][i] == crowd[0][0][i]:
+            continue
+        norm = nobj * float(crowd[-1][0][i] - crowd[0][0][i])
+        for prev, cur, nxt in zip(crowd[:-2], crowd[1:-1], crowd[2:]):
+            distances[cur[1]] += (nxt[0][i] - prev[0][i]) / norm
+    return distances
+
+
+def sel_nsga2(wvalues, weights, k):
+    """emo.py:15-50 with nd='standard'.  Returns (chosen indices, crowding
+    distance per index for the sorted individuals)."""
+    fronts = sort_nondominated(wvalues, k)
+    crowd = {}
+    for front in fronts:
+        vals = [[float(w) / float(x) for w, x in zip(wvalues[i], weights)] for i in front]
+        for i, d in zip(front, assign_crowding_dist(vals)):
+            crowd[i] = d
+    chosen = [i for f in fronts[:-1] for i in f]
+    kk = k - len(chosen)
+    if kk > 0:
+        last = sorted(fronts[-1], key=lambda i: crowd[i], reverse=True)
+        chosen.extend(last[:kk])
+    return chosen, crowd
+
+
+# ---------------------------------------------------------------------------
+# migRing (deap/tools/migration.py:4-51) on demes of (genes, wvalues, valid)
+# ---------------------------------------------------------------------------
+def mig_ring(demes, emigrant_idx, immigrant_idx=None, migarray=None):
+    """demes: list of dicts {genes, wvalues, valid} (modified in place).
+    emigrant_idx[d]: selection(pop_d, k) row indices; immigrant_idx[d]:
+    replacement(pop_d, k) or None (immigrants = emigrants).  Placement uses
+    value equality on genomes against the *current* destination deme."""
+    n = len(demes)
+    if migarray is None:
+        migarray = list(range(1, n)) + [0]
+    # snapshot the selected individuals (references in the reference: values
+    # never change after selection, so copies are equivalent)
+    em = [[(demes[d]["genes"][i].copy(), demes[d]["wvalues"][i].copy(), bool(demes[d]["valid"][i]))
+           for i in emigrant_idx[d]] for d in range(n)]
+    if immigrant_idx is None:
+        im = em
+    else:
+        im = [[(demes[d]["genes"][i].copy(),) for i in immigrant_idx[d]] for d in range(n)]
+    for from_deme, to_deme in enumerate(migarray):
+        dst = demes[to_deme]
+        for i, immigrant in enumerate(im[to_deme]):
+            target = immigrant[0]
+            eq = np.all(dst["genes"] == target[None, :], axis=1)
+            hits = np.nonzero(eq)[0]
+            if len(hits) == 0:
+                raise ValueError("immigrant is not in list")
+            indx = int(hits[0])
+            g, w, v = em[from_deme][i]
+            dst["genes"][indx] = g
+            dst["wvalues"][indx] = w
+            dst["valid"][indx] = v
+    return demes

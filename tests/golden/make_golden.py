@@ -1,0 +1,559 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors that pin the oracle — run in the BUILD
+container only (needs /root/reference; the fixtures it writes travel, the
+reference does not).
+
+The reference (DEAP 1.3.1, Python-2 source) is made importable exactly as its
+own setup.py prescribes (``use_2to3=True``, setup.py:90): a scratch copy under
+/tmp is converted with lib2to3.  Nothing from it is copied into the repo.
+
+Parity is defined on random *decisions*: DEAP draws through the module-level
+functions ``random.random / randint / choice / gauss / sample``; they are
+replaced by iterators over pre-drawn decision arrays in DEAP's consumption
+order, so DEAP consumes exactly the decisions the GPU and the oracle get.
+The C1 trajectory (README OneMax, examples/ga/onemax_short.py, seed 64) is
+recorded the other way round: DEAP runs with the real Mersenne Twister and a
+recording wrapper captures every decision it draws.
+
+Usage:  python tests/golden/make_golden.py            # writes tests/golden/*.npz
+"""
+import array
+import importlib
+import os
+import random
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference/deap"
+SCRATCH = "/tmp/deap_oracle"
+NOT_TAKEN = 1.0 - 2.0 ** -53  # random() value that fails every `< p` test with p < 1
+TAKEN = 0.0
+
+
+def load_reference():
+    if not os.path.isdir(os.path.join(SCRATCH, "deap")):
+        shutil.rmtree(SCRATCH, ignore_errors=True)
+        os.makedirs(SCRATCH)
+        shutil.copytree(REF, os.path.join(SCRATCH, "deap"))
+        for root, dirs, files in os.walk(SCRATCH):
+            for f in files + dirs:
+                os.chmod(os.path.join(root, f), 0o755)
+        subprocess.check_call([sys.executable, "-W", "ignore", "-m", "lib2to3", "-w", "-n",
+                               "deap"], cwd=SCRATCH, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.DEVNULL)
+    sys.path.insert(0, SCRATCH)
+    mods = {}
+    for name in ("deap", "deap.base", "deap.creator", "deap.tools", "deap.algorithms",
+                 "deap.benchmarks", "deap.tools.emo"):
+        mods[name] = importlib.import_module(name)
+    return mods
+
+
+class Replay:
+    """Module-level random stubs served from per-function queues."""
+
+    def __init__(self, floats=(), ints=(), choices=(), gausses=(), samples=()):
+        self.q = {"random": list(floats), "randint": list(ints), "choice": list(choices),
+                  "gauss": list(gausses), "sample": list(samples)}
+        self.saved = {}
+
+    def __enter__(self):
+        for name in ("random", "randint", "choice", "gauss", "sample"):
+            self.saved[name] = getattr(random, name)
+        q = self.q
+        random.random = lambda: q["random"].pop(0)
+        random.randint = lambda a, b: q["randint"].pop(0)
+        random.choice = lambda seq: seq[q["choice"].pop(0)]
+        random.gauss = lambda mu, sigma: q["gauss"].pop(0)
+        random.sample = lambda seq, k: [seq[i] for i in q["sample"].pop(0)]
+        return self
+
+    def __exit__(self, *exc):
+        for name, fn in self.saved.items():
+            setattr(random, name, fn)
+        for name, left in self.q.items():
+            assert not left, "unconsumed %s decisions: %d" % (name, len(left))
+
+
+def flag(b):
+    return TAKEN if b else NOT_TAKEN
+
+
+def make_types(D, typecode, weights):
+    creator = D["deap.creator"]
+    base = D["deap.base"]
+    for name in ("FitG", "IndG"):
+        if hasattr(creator, name):
+            delattr(creator, name)
+    creator.create("FitG", base.Fitness, weights=weights)
+    if typecode == "list":
+        creator.create("IndG", list, fitness=creator.FitG)
+    else:
+        creator.create("IndG", array.array, typecode=typecode, fitness=creator.FitG)
+    return creator.IndG
+
+
+def to_inds(Ind, genes, wvalues=None, valid=None):
+    out = []
+    for i, row in enumerate(genes):
+        ind = Ind([int(x) for x in row] if genes.dtype == np.uint8 else [float(x) for x in row])
+        if wvalues is not None and (valid is None or valid[i]):
+            ind.fitness.values = tuple(float(w) / float(ww) for w, ww in
+                                       zip(wvalues[i], ind.fitness.weights))
+        out.append(ind)
+    return out
+
+
+def from_inds(inds, dtype, m):
+    genes = np.array([list(ind) for ind in inds], dtype=dtype)
+    wv = np.array([ind.fitness.wvalues if ind.fitness.valid else (0.0,) * m for ind in inds],
+                  np.float64)
+    valid = np.array([ind.fitness.valid for ind in inds], bool)
+    return genes, wv, valid
+
+
+# ---------------------------------------------------------------------------
+def gen_eval(D, rng):
+    bm = D["deap.benchmarks"]
+    out = {}
+    cases = [("rastrigin", 1000, (-5.12, 5.12), {}), ("rastrigin", 37, (-50, 50), {}),
+             ("rosenbrock", 1000, (-2.048, 2.048), {}), ("rosenbrock", 13, (-3, 3), {}),
+             ("sphere", 64, (-1, 1), {}),
+             ("zdt1", 30, (0, 1), {}), ("zdt2", 30, (0, 1), {}), ("zdt3", 30, (0, 1), {}),
+             ("zdt4", 10, (0, 1), {}), ("zdt6", 10, (0, 1), {}),
+             ("dtlz1", 7, (0, 1), {"obj": 3}), ("dtlz2", 12, (0, 1), {"obj": 3}),
+             ("dtlz3", 12, (0, 1), {"obj": 3}), ("dtlz4", 12, (0, 1), {"obj": 3, "alpha": 100}),
+             ("dtlz2", 14, (0, 1), {"obj": 5})]
+    for j, (name, dim, (lo, hi), kw) in enumerate(cases):
+        n = 24
+        x = rng.uniform(lo, hi, size=(n, dim))
+        if name.startswith("zdt4"):
+            x[:, 1:] = rng.uniform(-5, 5, size=(n, dim - 1))
+        fn = getattr(bm, name)
+        vals = np.array([fn(list(map(float, row)), **kw) for row in x], np.float64)
+        out["eval%d_x" % j] = x
+        out["eval%d_f" % j] = vals
+        out["eval%d_meta" % j] = np.array([name, str(kw)])
+    # OneMax (README) on 0/1 genomes
+    bits = rng.integers(0, 2, size=(32, 100)).astype(np.uint8)
+    out["onemax_x"] = bits
+    out["onemax_f"] = bits.sum(axis=1).astype(np.float64)
+    # float32 genomes: DEAP evaluates the stored fp32 values widened to fp64
+    x32 = rng.uniform(-5.12, 5.12, size=(16, 100)).astype(np.float32)
+    Ind = make_types(D, "f", (-1.0,))
+    out["rastrigin_f32_x"] = x32
+    out["rastrigin_f32_f"] = np.array([bm.rastrigin(Ind(list(map(float, r))))[0] for r in x32])
+    return out
+
+
+def gen_varand(D, rng):
+    algorithms = D["deap.algorithms"]
+    tools = D["deap.tools"]
+    base = D["deap.base"]
+    out = {}
+    cases = [("bits", "list", 100, 40, "twopoint", "flipbit"),
+             ("bits", "b", 4096, 10, "twopoint", "flipbit"),
+             ("f64", "d", 1000, 12, "blend", "gaussian"),
+             ("f64", "d", 30, 33, "twopoint", "gaussian"),
+             ("f32", "f", 50, 20, "blend", "gaussian")]
+    for j, (gt, tc, dim, n, cx, mut) in enumerate(cases):
+        Ind = make_types(D, tc, (1.0,))
+        if gt == "bits":
+            genes = rng.integers(0, 2, size=(n, dim)).astype(np.uint8)
+        else:
+            genes = rng.uniform(-5, 5, size=(n, dim)).astype(np.float32 if gt == "f32"
+                                                              else np.float64)
+        wv = rng.integers(0, 50, size=(n, 1)).astype(np.float64)
+        valid = np.ones(n, bool)
+        cxpb, mutpb, indpb, alpha = 0.5, 0.3, 0.05, 0.5
+        npairs = n // 2
+        cx_flag = rng.random(npairs) < cxpb
+        cx_raw = np.stack([rng.integers(1, dim + 1, npairs), rng.integers(1, dim, npairs)], 1)
+        blend_u = rng.random((npairs, dim))
+        mut_flag = rng.random(n) < mutpb
+        mask = rng.random((n, dim)) < indpb
+        gauss = rng.normal(0.0, 1.0, size=(n, dim))
+        floats, ints, gausses = [], [], []
+        for p in range(npairs):
+            floats.append(flag(cx_flag[p]))
+            if cx_flag[p]:
+                if cx == "twopoint":
+                    ints.extend(int(v) for v in cx_raw[p])
+                else:
+                    floats.extend(float(v) for v in blend_u[p])
+        for i in range(n):
+            floats.append(flag(mut_flag[i]))
+            if mut_flag[i]:
+                for g in range(dim):
+                    floats.append(flag(mask[i, g]))
+                    if mut == "gaussian" and mask[i, g]:
+                        gausses.append(float(gauss[i, g]))
+        tb = base.Toolbox()
+        if cx == "twopoint":
+            tb.register("mate", tools.cxTwoPoint)
+        else:
+            tb.register("mate", tools.cxBlend, alpha=alpha)
+        if mut == "flipbit":
+            tb.register("mutate", tools.mutFlipBit, indpb=indpb)
+        else:
+            tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=indpb)
+        pop = to_inds(Ind, genes, wv, valid)
+        with Replay(floats=floats, ints=ints, gausses=gausses):
+            off = algorithms.varAnd(pop, tb, cxpb, mutpb)
+        og, owv, ovalid = from_inds(off, genes.dtype, 1)
+        key = "va%d_" % j
+        out.update({key + "genes": genes, key + "wv": wv, key + "valid": valid,
+                    key + "cx_flag": cx_flag, key + "cx_raw": cx_raw, key + "blend_u": blend_u,
+                    key + "mut_flag": mut_flag, key + "mask": mask, key + "gauss": gauss,
+                    key + "out_genes": og, key + "out_wv": owv, key + "out_valid": ovalid,
+                    key + "meta": np.array([gt, tc, cx, mut, str(cxpb), str(mutpb),
+                                            str(indpb), str(alpha)])})
+    return out
+
+
+def gen_selection(D, rng):
+    tools = D["deap.tools"]
+    out = {}
+    for j, (n, m, t) in enumerate([(64, 1, 3), (40, 2, 4), (33, 3, 2)]):
+        weights = tuple([1.0, -1.0, 1.0][:m])
+        Ind = make_types(D, "d", weights)
+        wv = rng.integers(0, 6, size=(n, m)).astype(np.float64)  # heavy ties
+        genes = rng.uniform(0, 1, size=(n, 3))
+        pop = to_inds(Ind, genes, wv)
+        k = n
+        asp = rng.integers(0, n, size=(k, t))
+        with Replay(choices=[int(a) for a in asp.ravel()]):
+            chosen = tools.selTournament(pop, k, tournsize=t)
+        idx = [next(i for i, p in enumerate(pop) if p is c) for c in chosen]
+        best = tools.selBest(pop, 10)
+        worst = tools.selWorst(pop, 10)
+        key = "sel%d_" % j
+        out.update({key + "wv": wv, key + "asp": asp, key + "out": np.array(idx),
+                    key + "best": np.array([next(i for i, p in enumerate(pop) if p is c)
+                                            for c in best]),
+                    key + "worst": np.array([next(i for i, p in enumerate(pop) if p is c)
+                                             for c in worst]),
+                    key + "weights": np.array(weights)})
+    return out
+
+
+def gen_ea_generation(D, rng):
+    """One eaSimple generation body (select -> varAnd -> evaluate invalid)
+    with replayed decisions, for the fused kernel."""
+    algorithms = D["deap.algorithms"]
+    tools = D["deap.tools"]
+    base = D["deap.base"]
+    bm = D["deap.benchmarks"]
+    out = {}
+    cases = [("f64", "d", 1000, 16, "blend", "gaussian", "rastrigin", (-1.0,)),
+             ("f64", "d", 100, 21, "blend", "gaussian", "rosenbrock", (-1.0,)),
+             ("bits", "b", 4096, 16, "twopoint", "flipbit", "onemax", (1.0,)),
+             ("bits", "list", 100, 30, "twopoint", "flipbit", "onemax", (1.0,))]
+    for j, (gt, tc, dim, n, cx, mut, objective, weights) in enumerate(cases):
+        Ind = make_types(D, tc, weights)
+        if gt == "bits":
+            genes = rng.integers(0, 2, size=(n, dim)).astype(np.uint8)
+        else:
+            genes = rng.uniform(-5.12, 5.12, size=(n, dim))
+        if objective == "onemax":
+            evalf = lambda ind: (sum(ind),)  # noqa: E731 - README.md:85-86
+        else:
+            evalf = getattr(bm, objective)
+        pop = to_inds(Ind, genes)
+        for ind in pop:
+            ind.fitness.values = evalf(ind)
+        genes0, wv0, valid0 = from_inds(pop, genes.dtype, 1)
+        t, cxpb, mutpb, indpb, alpha = 3, 0.5, 0.2, 0.05, 0.5
+        asp = rng.integers(0, n, size=(n, t))
+        npairs = n // 2
+        cx_flag = rng.random(npairs) < cxpb
+        cx_raw = np.stack([rng.integers(1, dim + 1, npairs), rng.integers(1, dim, npairs)], 1)
+        blend_u = rng.random((npairs, dim))
+        mut_flag = rng.random(n) < mutpb
+        mask = rng.random((n, dim)) < indpb
+        gauss = rng.normal(0.0, 1.0, size=(n, dim))
+        floats, ints, gausses = [], [], []
+        for p in range(npairs):
+            floats.append(flag(cx_flag[p]))
+            if cx_flag[p]:
+                if cx == "twopoint":
+                    ints.extend(int(v) for v in cx_raw[p])
+                else:
+                    floats.extend(float(v) for v in blend_u[p])
+        for i in range(n):
+            floats.append(flag(mut_flag[i]))
+            if mut_flag[i]:
+                for g in range(dim):
+                    floats.append(flag(mask[i, g]))
+                    if mut == "gaussian" and mask[i, g]:
+                        gausses.append(float(gauss[i, g]))
+        tb = base.Toolbox()
+        tb.register("evaluate", evalf)
+        tb.register("select", tools.selTournament, tournsize=t)
+        if cx == "twopoint":
+            tb.register("mate", tools.cxTwoPoint)
+        else:
+            tb.register("mate", tools.cxBlend, alpha=alpha)
+        if mut == "flipbit":
+            tb.register("mutate", tools.mutFlipBit, indpb=indpb)
+        else:
+            tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=indpb)
+        with Replay(floats=floats, ints=ints, gausses=gausses,
+                    choices=[int(a) for a in asp.ravel()]):
+            pop2, log = algorithms.eaSimple(pop, tb, cxpb, mutpb, 1, verbose=False)
+        og, owv, ovalid = from_inds(pop2, genes.dtype, 1)
+        key = "ea%d_" % j
+        out.update({key + "genes": genes0, key + "wv": wv0, key + "valid": valid0,
+                    key + "asp": asp, key + "cx_flag": cx_flag, key + "cx_raw": cx_raw,
+                    key + "blend_u": blend_u, key + "mut_flag": mut_flag, key + "mask": mask,
+                    key + "gauss": gauss, key + "out_genes": og, key + "out_wv": owv,
+                    key + "out_valid": ovalid,
+                    key + "nevals": np.array(log.select("nevals")),
+                    key + "meta": np.array([gt, tc, cx, mut, objective, str(t), str(cxpb),
+                                            str(mutpb), str(indpb), str(alpha), str(weights[0])])})
+    return out
+
+
+def gen_varor(D, rng):
+    algorithms = D["deap.algorithms"]
+    tools = D["deap.tools"]
+    base = D["deap.base"]
+    out = {}
+    cases = [("f64", "d", 12, 20, 30, "blend", "gaussian"),
+             ("bits", "list", 70, 16, 25, "twopoint", "flipbit")]
+    for j, (gt, tc, dim, n, lam, cx, mut) in enumerate(cases):
+        Ind = make_types(D, tc, (-1.0, -1.0))
+        genes = (rng.integers(0, 2, size=(n, dim)).astype(np.uint8) if gt == "bits"
+                 else rng.uniform(0, 1, size=(n, dim)))
+        wv = rng.uniform(-5, 0, size=(n, 2))
+        valid = np.ones(n, bool)
+        pop = to_inds(Ind, genes, wv, valid)
+        cxpb, mutpb, indpb, alpha = 0.5, 0.3, 0.1, 0.5
+        op_u = rng.random(lam)
+        op = np.where(op_u < cxpb, 0, np.where(op_u < cxpb + mutpb, 1, 2))
+        idx = np.zeros((lam, 2), np.int64)
+        cx_raw = np.stack([rng.integers(1, dim + 1, lam), rng.integers(1, dim, lam)], 1)
+        blend_u = rng.random((lam, dim))
+        mask = rng.random((lam, dim)) < indpb
+        gauss = rng.normal(0, 1, size=(lam, dim))
+        floats, ints, choices, gausses, samples = [], [], [], [], []
+        for c in range(lam):
+            floats.append(float(op_u[c]))
+            if op[c] == 0:
+                a, b = rng.choice(n, 2, replace=False)
+                idx[c] = (a, b)
+                samples.append([int(a), int(b)])
+                if cx == "twopoint":
+                    ints.extend(int(v) for v in cx_raw[c])
+                else:
+                    floats.extend(float(v) for v in blend_u[c])
+            else:
+                a = int(rng.integers(0, n))
+                idx[c] = (a, 0)
+                choices.append(a)
+                if op[c] == 1:
+                    for g in range(dim):
+                        floats.append(flag(mask[c, g]))
+                        if mut == "gaussian" and mask[c, g]:
+                            gausses.append(float(gauss[c, g]))
+        tb = base.Toolbox()
+        if cx == "twopoint":
+            tb.register("mate", tools.cxTwoPoint)
+        else:
+            tb.register("mate", tools.cxBlend, alpha=alpha)
+        if mut == "flipbit":
+            tb.register("mutate", tools.mutFlipBit, indpb=indpb)
+        else:
+            tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=indpb)
+        with Replay(floats=floats, ints=ints, choices=choices, gausses=gausses, samples=samples):
+            off = algorithms.varOr(pop, tb, lam, cxpb, mutpb)
+        og, owv, ovalid = from_inds(off, genes.dtype, 2)
+        key = "vo%d_" % j
+        out.update({key + "genes": genes, key + "wv": wv, key + "valid": valid,
+                    key + "op": op, key + "op_u": op_u, key + "idx": idx, key + "cx_raw": cx_raw,
+                    key + "blend_u": blend_u, key + "mask": mask, key + "gauss": gauss,
+                    key + "out_genes": og, key + "out_wv": owv, key + "out_valid": ovalid,
+                    key + "meta": np.array([gt, tc, cx, mut, str(lam), str(cxpb), str(mutpb),
+                                            str(indpb), str(alpha)])})
+    return out
+
+
+def gen_nsga2(D, rng):
+    tools = D["deap.tools"]
+    emo = D["deap.tools.emo"]
+    out = {}
+    cases = [(200, 2, "ties", 100), (300, 3, "ties", 150), (257, 3, "cont", 128),
+             (120, 2, "dups", 60), (64, 4, "ties", 64), (150, 3, "cont", 500)]
+    for j, (n, m, kind, k) in enumerate(cases):
+        weights = tuple([-1.0, -1.0, 1.0, -1.0][:m])
+        Ind = make_types(D, "d", weights)
+        if kind == "ties":
+            vals = rng.integers(0, 7, size=(n, m)).astype(np.float64)
+        elif kind == "dups":
+            base_pts = rng.uniform(0, 1, size=(n // 4, m))
+            vals = base_pts[rng.integers(0, n // 4, n)]
+        else:
+            vals = rng.uniform(0, 1, size=(n, m))
+        wv = vals * np.array(weights)
+        genes = rng.uniform(0, 1, size=(n, 2))
+        pop = to_inds(Ind, genes, wv)
+        ident = {id(p): i for i, p in enumerate(pop)}
+        fronts = tools.sortNondominated(pop, k)
+        flat = [ident[id(p)] for f in fronts for p in f]
+        fstart = np.cumsum([0] + [len(f) for f in fronts])
+        # crowding on each front (emo.assignCrowdingDist is not exported)
+        for f in fronts:
+            emo.assignCrowdingDist(f)
+        crowd = np.array([pop[i].fitness.crowding_dist for i in flat])
+        pop2 = to_inds(Ind, genes, wv)
+        ident2 = {id(p): i for i, p in enumerate(pop2)}
+        chosen = tools.selNSGA2(pop2, k)
+        key = "nd%d_" % j
+        out.update({key + "wv": wv, key + "weights": np.array(weights), key + "k": np.array(k),
+                    key + "order": np.array(flat), key + "fstart": fstart,
+                    key + "crowd": crowd,
+                    key + "chosen": np.array([ident2[id(p)] for p in chosen])})
+        ff = tools.sortNondominated(to_inds(Ind, genes, wv), k, first_front_only=True)
+        out[key + "first"] = np.array([len(ff[0])])
+    return out
+
+
+def gen_migration(D, rng):
+    tools = D["deap.tools"]
+    out = {}
+    for j, (ndemes, n, dim, k, repl) in enumerate([(3, 40, 6, 5, None), (4, 30, 5, 6, "sample"),
+                                                   (2, 25, 4, 8, None)]):
+        Ind = make_types(D, "d", (1.0,))
+        # few distinct genomes -> duplicates inside and across demes
+        palette = rng.integers(0, 3, size=(6, dim)).astype(np.float64)
+        demes, raw = [], []
+        for d in range(ndemes):
+            g = palette[rng.integers(0, len(palette), n)]
+            wv = g.sum(axis=1, keepdims=True)
+            raw.append((g.copy(), wv.copy()))
+            demes.append(to_inds(Ind, g, wv))
+        sel_idx = []
+        samples = []
+        for d in range(ndemes):
+            best = tools.selBest(demes[d], k)
+            sel_idx.append([next(i for i, p in enumerate(demes[d]) if p is b) for b in best])
+            if repl == "sample":
+                samples.append([int(x) for x in rng.choice(n, k, replace=False)])
+        with Replay(samples=samples):
+            tools.migRing(demes, k, tools.selBest,
+                          replacement=(random.sample if repl == "sample" else None))
+        key = "mig%d_" % j
+        for d in range(ndemes):
+            out[key + "in_genes%d" % d] = raw[d][0]
+            out[key + "in_wv%d" % d] = raw[d][1]
+            out[key + "sel%d" % d] = np.array(sel_idx[d])
+            out[key + "out_genes%d" % d] = np.array([list(p) for p in demes[d]])
+            out[key + "out_wv%d" % d] = np.array([p.fitness.wvalues for p in demes[d]])
+            if repl == "sample":
+                out[key + "repl%d" % d] = np.array(samples[d])
+        out[key + "meta"] = np.array([str(ndemes), str(k), str(repl)])
+    return out
+
+
+def gen_c1_trajectory(D):
+    """examples/ga/onemax_short.py (seed 64, pop 300, 100 bits, eaSimple
+    cxpb 0.5 mutpb 0.2, 40 gens) with every decision recorded."""
+    creator = D["deap.creator"]
+    base = D["deap.base"]
+    tools = D["deap.tools"]
+    algorithms = D["deap.algorithms"]
+    Ind = make_types(D, "b", (1.0,))
+    tb = base.Toolbox()
+    tb.register("attr_bool", random.randint, 0, 1)
+    tb.register("individual", tools.initRepeat, Ind, tb.attr_bool, 100)
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    tb.register("evaluate", lambda ind: (sum(ind),))
+    tb.register("mate", tools.cxTwoPoint)
+    tb.register("mutate", tools.mutFlipBit, indpb=0.05)
+    tb.register("select", tools.selTournament, tournsize=3)
+    random.seed(64)
+    pop = tb.population(n=300)
+    init = np.array([list(p) for p in pop], np.uint8)
+    log_calls = []
+    real = {name: getattr(random, name) for name in ("random", "randint", "choice")}
+
+    def rec_random():
+        v = real["random"]()
+        log_calls.append(("random", v))
+        return v
+
+    def rec_randint(a, b):
+        v = real["randint"](a, b)
+        log_calls.append(("randint", v))
+        return v
+
+    def rec_choice(seq):
+        i = random._inst._randbelow(len(seq))  # CPython 3.10 choice()
+        log_calls.append(("choice", i))
+        return seq[i]
+
+    random.random, random.randint, random.choice = rec_random, rec_randint, rec_choice
+    try:
+        pop, log = algorithms.eaSimple(pop, tb, cxpb=0.5, mutpb=0.2, ngen=40, verbose=False)
+    finally:
+        for name, fn in real.items():
+            setattr(random, name, fn)
+    # split the recorded stream into per-generation decision arrays
+    n, dim, t, ngen = 300, 100, 3, 40
+    it = iter(log_calls)
+    out = {"c1_init": init, "c1_final": np.array([list(p) for p in pop], np.uint8),
+           "c1_final_wv": np.array([p.fitness.wvalues for p in pop]),
+           "c1_nevals": np.array(log.select("nevals"))}
+    asp_all, cxf_all, raw_all, mutf_all, mask_all = [], [], [], [], []
+    for g in range(ngen):
+        asp = np.array([next(it)[1] for _ in range(n * t)]).reshape(n, t)
+        cxf = np.zeros(n // 2, bool)
+        raw = np.zeros((n // 2, 2), np.int64)
+        for p in range(n // 2):
+            kind, v = next(it)
+            assert kind == "random"
+            cxf[p] = v < 0.5
+            if cxf[p]:
+                raw[p] = (next(it)[1], next(it)[1])
+        mutf = np.zeros(n, bool)
+        mask = np.zeros((n, dim), bool)
+        for i in range(n):
+            kind, v = next(it)
+            mutf[i] = v < 0.2
+            if mutf[i]:
+                mask[i] = [next(it)[1] < 0.05 for _ in range(dim)]
+        asp_all.append(asp)
+        cxf_all.append(cxf)
+        raw_all.append(raw)
+        mutf_all.append(mutf)
+        mask_all.append(mask)
+    assert next(it, None) is None
+    out.update({"c1_asp": np.array(asp_all), "c1_cx_flag": np.array(cxf_all),
+                "c1_cx_raw": np.array(raw_all), "c1_mut_flag": np.array(mutf_all),
+                "c1_mask": np.packbits(np.array(mask_all), axis=-1)})
+    return out
+
+
+def main():
+    D = load_reference()
+    rng = np.random.default_rng(20260415)
+    os.makedirs(HERE, exist_ok=True)
+    np.savez_compressed(os.path.join(HERE, "eval.npz"), **gen_eval(D, rng))
+    np.savez_compressed(os.path.join(HERE, "varand.npz"), **gen_varand(D, rng))
+    np.savez_compressed(os.path.join(HERE, "selection.npz"), **gen_selection(D, rng))
+    np.savez_compressed(os.path.join(HERE, "generation.npz"), **gen_ea_generation(D, rng))
+    np.savez_compressed(os.path.join(HERE, "varor.npz"), **gen_varor(D, rng))
+    np.savez_compressed(os.path.join(HERE, "nsga2.npz"), **gen_nsga2(D, rng))
+    np.savez_compressed(os.path.join(HERE, "migration.npz"), **gen_migration(D, rng))
+    np.savez_compressed(os.path.join(HERE, "c1_trajectory.npz"), **gen_c1_trajectory(D))
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

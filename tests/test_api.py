@@ -1,0 +1,122 @@
+"""Host-side API mirror (Toolbox / Fitness / creator / Logbook / Statistics /
+HallOfFame on host lists) and operator resolution, on CPU."""
+import array
+import functools
+import operator
+import random
+
+import numpy as np
+import pytest
+
+from deap_amd import base, creator
+
+
+def test_toolbox_register_partial_and_decorate():
+    tb = base.Toolbox()
+    assert tb.clone([1, [2]]) == [1, [2]]
+    tb.register("f", lambda a, b, c=3: (a, b, c), 2, c=4)
+    assert tb.f(3) == (2, 3, 4)
+    assert tb.f.__name__ == "f"
+    tb.decorate("f", lambda fn: (lambda *a, **k: ("deco",) + fn(*a, **k)))
+    assert tb.f(3) == ("deco", 2, 3, 4)
+    tb.unregister("f")
+    assert not hasattr(tb, "f")
+
+
+def test_fitness_semantics():
+    creator.create("FMaxMin", base.Fitness, weights=(1.0, -1.0))
+    f1, f2 = creator.FMaxMin(), creator.FMaxMin()
+    assert not f1.valid
+    f1.values = (2.0, 3.0)
+    assert f1.wvalues == (2.0, -3.0) and f1.values == (2.0, 3.0)
+    f2.values = (2.0, 4.0)
+    assert f1 > f2 and f1.dominates(f2) and not f2.dominates(f1)
+    f2.values = (2.0, 3.0)
+    assert f1 == f2 and not f1.dominates(f2) and not (f1 > f2)
+    del f1.values
+    assert not f1.valid
+    with pytest.raises(TypeError):
+        base.Fitness()
+    with pytest.raises(AssertionError):
+        f2.values = (1.0,)
+
+
+def test_creator_array_individual():
+    creator.create("FMax1", base.Fitness, weights=(1.0,))
+    creator.create("IndB", array.array, typecode="b", fitness=creator.FMax1)
+    ind = creator.IndB([1, 0, 1])
+    ind.fitness.values = (2,)
+    import copy
+    c = copy.deepcopy(ind)
+    assert list(c) == [1, 0, 1] and c.fitness.values == (2.0,) and c.fitness is not ind.fitness
+    from deap_amd.device import gtype_of
+    from deap_amd import _lib
+    assert gtype_of(creator.IndB) == _lib.DM_BITS
+    creator.create("IndF", array.array, typecode="f", fitness=creator.FMax1)
+    assert gtype_of(creator.IndF) == _lib.DM_F32
+    creator.create("IndL", list, fitness=creator.FMax1)
+    assert gtype_of(creator.IndL) == _lib.DM_F64
+
+
+def test_operator_resolution():
+    from deap_amd import tools, benchmarks
+    from deap_amd.ops import resolve
+    tb = base.Toolbox()
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("evaluate", benchmarks.dtlz2, obj=3)
+    op, a, kw = resolve(tb.mate)
+    assert op is tools.cxBlend and kw == {"alpha": 0.5}
+    op, a, kw = resolve(tb.evaluate)
+    ev = op.eval_struct((-1.0, -1.0, -1.0), a, kw)
+    assert ev.obj == 3 and ev.weights[2] == -1.0
+    tb.register("bad", lambda x: x)
+    with pytest.raises(TypeError):
+        resolve(tb.bad)
+
+
+def test_drivers_reject_host_lists():
+    from deap_amd import algorithms, tools
+    tb = base.Toolbox()
+    with pytest.raises(TypeError):
+        algorithms.eaSimple([[0, 1]], tb, 0.5, 0.2, 1)
+    with pytest.raises(TypeError):
+        tools.selTournament([[0, 1]], 1, 3)
+
+
+def test_logbook_and_statistics_on_host_lists():
+    from deap_amd import tools
+    creator.create("FMaxS", base.Fitness, weights=(1.0,))
+    pop = []
+    for v in (1.0, 3.0, 2.0):
+        f = creator.FMaxS()
+        f.values = (v,)
+        pop.append(type("I", (), {"fitness": f})())
+    stats = tools.Statistics(lambda ind: ind.fitness.values)
+    stats.register("avg", np.mean)
+    stats.register("max", np.max)
+    rec = stats.compile(pop)
+    assert rec == {"avg": 2.0, "max": 3.0}
+    log = tools.Logbook()
+    log.header = ["gen", "nevals", "avg", "max"]
+    log.record(gen=0, nevals=3, **rec)
+    log.record(gen=1, nevals=2, **rec)
+    assert log.select("gen") == [0, 1]
+    assert log.select("gen", "nevals") == ([0, 1], [3, 2])
+    text = log.stream
+    assert "gen" in text.splitlines()[0] and len(text.splitlines()) == 3
+    assert log.stream == ""
+
+
+def test_hall_of_fame_on_host_lists():
+    from deap_amd import tools
+    creator.create("FMaxH", base.Fitness, weights=(1.0,))
+    creator.create("IndH", list, fitness=creator.FMaxH)
+    pop = []
+    for genes, v in (([1], 1.0), ([2], 5.0), ([2], 5.0), ([3], 4.0), ([4], 5.0)):
+        ind = creator.IndH(genes)
+        ind.fitness.values = (v,)
+        pop.append(ind)
+    hof = tools.HallOfFame(2)
+    hof.update(pop)
+    # value pinned against the reference HallOfFame (bisect_right insertion)
+    assert [list(i) for i in hof] == [[4], [2]]

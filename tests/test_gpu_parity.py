@@ -1,0 +1,376 @@
+"""GPU parity: every hot-path kernel against the golden vectors of the
+reference and against the CPU oracle, through the C ABI (libdeapmi.so)."""
+import ast
+import ctypes
+import functools
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import ops, philox
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_close(a, b, tol):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
+
+
+def _dp():
+    from deap_amd.device import DevicePopulation
+    return DevicePopulation
+
+
+def _toolbox(cx, mut, indpb=0.05, alpha=0.5, evaluate=None, select=None, tournsize=3, **ev_kw):
+    from deap_amd import base, tools, benchmarks
+    tb = base.Toolbox()
+    if cx == "twopoint":
+        tb.register("mate", tools.cxTwoPoint)
+    else:
+        tb.register("mate", tools.cxBlend, alpha=alpha)
+    if mut == "flipbit":
+        tb.register("mutate", tools.mutFlipBit, indpb=indpb)
+    else:
+        tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=indpb)
+    if evaluate:
+        tb.register("evaluate", getattr(benchmarks, evaluate), **ev_kw)
+    tb.register("select", tools.selTournament, tournsize=tournsize)
+    return tb
+
+
+# ---------------------------------------------------------------------------
+def test_philox_blocks_match_oracle(gpu):
+    import torch
+    from deap_amd import _lib
+    from deap_amd.device import Context
+    ctx = Context.get()
+    n = 4096
+    out = torch.empty((n, 4), dtype=torch.int32, device=gpu)
+    c0 = (ctypes.c_uint32 * 4)(7, 3, 11, (5 << 16) | 2)
+    key = (ctypes.c_uint32 * 2)(0xDEADBEEF, 0x12345678)
+    _lib.call("dm_philox_blocks", ctx.bind(), c0, key, n, ctypes.c_void_p(out.data_ptr()))
+    got = out.cpu().numpy().view(np.uint32)
+    ctr = np.stack([7 + np.arange(n), np.full(n, 3), np.full(n, 11), np.full(n, (5 << 16) | 2)], 1)
+    want = philox.philox4x32_10(ctr.astype(np.uint64), (0xDEADBEEF, 0x12345678))
+    assert np.array_equal(got, want)
+
+
+def test_eval_matches_reference(gpu):
+    from deap_amd import benchmarks
+    d = golden("eval.npz")
+    j = 0
+    while "eval%d_x" % j in d:
+        name, kw = d["eval%d_meta" % j]
+        kw = ast.literal_eval(kw)
+        f = d["eval%d_f" % j]
+        pop = _dp().from_numpy(d["eval%d_x" % j], weights=(1.0,) * f.shape[1], gtype="f64")
+        got = getattr(benchmarks, name)(pop, **kw).cpu().numpy()
+        assert _rel_close(got, f, 1e-12), (name, np.max(np.abs(got - f)))
+        assert pop.valid[: len(pop)].bool().all()
+        j += 1
+    pop = _dp().from_numpy(d["onemax_x"], weights=(1.0,), gtype="bits")
+    assert np.array_equal(benchmarks.onemax(pop).cpu().numpy()[:, 0], d["onemax_f"])
+    pop = _dp().from_numpy(d["rastrigin_f32_x"], weights=(-1.0,), gtype="f32")
+    got = benchmarks.rastrigin(pop).cpu().numpy()[:, 0]
+    assert _rel_close(got, d["rastrigin_f32_f"], 1e-12)
+
+
+def test_eval_only_invalid_and_nevals(gpu):
+    import torch
+    from deap_amd import benchmarks
+    x = np.random.default_rng(3).uniform(-5, 5, size=(1000, 64))
+    pop = _dp().from_numpy(x, weights=(-1.0,), gtype="f64")
+    pop.valid[::2] = 1
+    pop.wvalues[::2] = 123.0
+    nev = torch.zeros(1, dtype=torch.int64, device=gpu)
+    benchmarks.sphere(pop, only_invalid=True, nevals=nev)
+    assert int(nev.item()) == 500
+    wv = pop.wvalues.cpu().numpy()[:, 0]
+    assert np.all(wv[::2] == 123.0)
+    assert _rel_close(wv[1::2], -(x[1::2] ** 2).sum(1), 1e-12)
+
+
+def _decisions_from(d, k, gpu, aspirants=None):
+    from deap_amd.decisions import Decisions
+    return Decisions.from_numpy(gpu, aspirants=aspirants, cx_flag=d[k + "cx_flag"],
+                                cx_raw=d[k + "cx_raw"], blend_u=d[k + "blend_u"],
+                                mut_flag=d[k + "mut_flag"], mut_mask=d[k + "mask"],
+                                gauss=d[k + "gauss"])
+
+
+def test_var_and_matches_reference(gpu):
+    from deap_amd import algorithms
+    d = golden("varand.npz")
+    j = 0
+    while "va%d_genes" % j in d:
+        k = "va%d_" % j
+        gt, tc, cx, mut, cxpb, mutpb, indpb, alpha = d[k + "meta"]
+        pop = _dp().from_numpy(d[k + "genes"], weights=(1.0,), gtype=gt, wvalues=d[k + "wv"],
+                               valid=d[k + "valid"])
+        tb = _toolbox(cx, mut, float(indpb), float(alpha))
+        dec = _decisions_from(d, k, gpu)
+        off = algorithms.varAnd(pop, tb, float(cxpb), float(mutpb), decisions=dec, mode="inject")
+        g, wv, ok = off.to_numpy()
+        assert np.array_equal(g, d[k + "out_genes"]), (j, gt, cx, mut)
+        assert np.array_equal(ok, d[k + "out_valid"])
+        assert np.array_equal(wv[ok], d[k + "out_wv"][ok])
+        j += 1
+
+
+def test_ea_generation_matches_reference(gpu):
+    from deap_amd import algorithms
+    d = golden("generation.npz")
+    j = 0
+    while "ea%d_genes" % j in d:
+        k = "ea%d_" % j
+        gt, tc, cx, mut, objective, t, cxpb, mutpb, indpb, alpha, w0 = d[k + "meta"]
+        pop = _dp().from_numpy(d[k + "genes"], weights=(float(w0),), gtype=gt,
+                               wvalues=d[k + "wv"], valid=d[k + "valid"])
+        tb = _toolbox(cx, mut, float(indpb), float(alpha), evaluate=objective,
+                      tournsize=int(t))
+        dec = _decisions_from(d, k, gpu, aspirants=d[k + "asp"])
+        pop, log = algorithms.eaSimple(pop, tb, float(cxpb), float(mutpb), 1, verbose=False,
+                                       decisions=[dec], mode="inject")
+        g, wv, ok = pop.to_numpy()
+        assert np.array_equal(g, d[k + "out_genes"]), j
+        assert ok.all()
+        tol = 0 if objective == "onemax" else 1e-12
+        assert _rel_close(wv, d[k + "out_wv"], tol), (j, np.max(np.abs(wv - d[k + "out_wv"])))
+        assert log.select("nevals") == d[k + "nevals"].tolist()
+        j += 1
+
+
+def test_selection_matches_reference(gpu):
+    from deap_amd import tools
+    from deap_amd.decisions import Decisions
+    d = golden("selection.npz")
+    for j in range(3):
+        k = "sel%d_" % j
+        wv = d[k + "wv"]
+        n, m = wv.shape
+        pop = _dp().from_numpy(np.zeros((n, 3)), weights=tuple(d[k + "weights"]), gtype="f64",
+                               wvalues=wv, valid=np.ones(n))
+        asp = d[k + "asp"]
+        dec = Decisions.from_numpy(gpu, aspirants=asp)
+        got = tools.selTournament(pop, n, asp.shape[1], mode="inject", decisions=dec)
+        assert got.cpu().numpy().tolist() == d[k + "out"].tolist()
+        assert tools.selBest(pop, 10).cpu().numpy().tolist() == d[k + "best"].tolist()
+        assert tools.selWorst(pop, 10).cpu().numpy().tolist() == d[k + "worst"].tolist()
+
+
+def test_var_or_matches_reference(gpu):
+    from deap_amd import algorithms
+    from deap_amd.decisions import Decisions
+    d = golden("varor.npz")
+    for j in range(2):
+        k = "vo%d_" % j
+        gt, tc, cx, mut, lam, cxpb, mutpb, indpb, alpha = d[k + "meta"]
+        pop = _dp().from_numpy(d[k + "genes"], weights=(-1.0, -1.0), gtype=gt,
+                               wvalues=d[k + "wv"], valid=d[k + "valid"])
+        tb = _toolbox(cx, mut, float(indpb), float(alpha))
+        dec = Decisions.from_numpy(gpu, varor_op=d[k + "op"], varor_idx=d[k + "idx"],
+                                   cx_raw=d[k + "cx_raw"], blend_u=d[k + "blend_u"],
+                                   mut_mask=d[k + "mask"], gauss=d[k + "gauss"])
+        off = algorithms.varOr(pop, tb, int(lam), float(cxpb), float(mutpb), decisions=dec,
+                               mode="inject")
+        g, wv, ok = off.to_numpy()
+        assert np.array_equal(g, d[k + "out_genes"]), j
+        assert np.array_equal(ok, d[k + "out_valid"])
+        assert np.array_equal(wv[ok], d[k + "out_wv"][ok])
+
+
+def test_nsga2_matches_reference(gpu):
+    from deap_amd import tools
+    from deap_amd.tools import emo
+    d = golden("nsga2.npz")
+    for j in range(6):
+        k = "nd%d_" % j
+        wv, weights, kk = d[k + "wv"], tuple(d[k + "weights"]), int(d[k + "k"])
+        n = len(wv)
+        pop = _dp().from_numpy(np.zeros((n, 2)), weights=weights, gtype="f64", wvalues=wv,
+                               valid=np.ones(n))
+        fronts = tools.sortNondominated(pop, kk)
+        flat = np.concatenate([f.cpu().numpy() for f in fronts]).tolist()
+        assert flat == d[k + "order"].tolist(), j
+        assert np.cumsum([0] + [len(f) for f in fronts]).tolist() == d[k + "fstart"].tolist()
+        crowd = emo.assignCrowdingDist(pop, fronts)
+        got = crowd.cpu().numpy()[np.array(flat)]
+        assert np.array_equal(got, d[k + "crowd"]), j
+        chosen = tools.selNSGA2(pop, kk)
+        assert chosen.cpu().numpy().tolist() == d[k + "chosen"].tolist(), j
+        ff = tools.sortNondominated(pop, kk, first_front_only=True)
+        assert len(ff) == 1 and len(ff[0]) == d[k + "first"][0]
+
+
+def test_mig_ring_matches_reference(gpu):
+    import torch
+    from deap_amd import tools
+    from deap_amd.tools import migration
+    d = golden("migration.npz")
+    for j in range(3):
+        k = "mig%d_" % j
+        nd, kk, repl = d[k + "meta"]
+        nd, kk = int(nd), int(kk)
+        demes = [_dp().from_numpy(d[k + "in_genes%d" % i], weights=(1.0,), gtype="f64",
+                                  wvalues=d[k + "in_wv%d" % i],
+                                  valid=np.ones(len(d[k + "in_wv%d" % i])))
+                 for i in range(nd)]
+        if repl == "None":
+            tools.migRing(demes, kk, tools.selBest)
+        else:
+            # replacement=random.sample with the reference's drawn indices
+            em = [migration.pack(demes[i], torch.tensor(d[k + "sel%d" % i], dtype=torch.int32,
+                                                         device=gpu)) for i in range(nd)]
+            im = [migration.pack(demes[i], torch.tensor(d[k + "repl%d" % i], dtype=torch.int32,
+                                                         device=gpu)) for i in range(nd)]
+            for frm, to in enumerate(list(range(1, nd)) + [0]):
+                migration.place(demes[to], im[to], em[frm], kk)
+        for i in range(nd):
+            g, wv, _ = demes[i].to_numpy()
+            assert np.array_equal(g, d[k + "out_genes%d" % i]), (j, i)
+            assert np.array_equal(wv, d[k + "out_wv%d" % i]), (j, i)
+
+
+def test_c1_trajectory_bit_exact(gpu):
+    """README OneMax (examples/ga/onemax_short.py, seed 64): the reference's
+    own 40 generations of decisions replayed on the GPU give its final
+    population and logbook."""
+    from deap_amd import algorithms
+    from deap_amd.decisions import Decisions
+    d = golden("c1_trajectory.npz")
+    pop = _dp().from_numpy(d["c1_init"], weights=(1.0,), gtype="bits")
+    decs = [Decisions.from_numpy(gpu, aspirants=d["c1_asp"][g], cx_flag=d["c1_cx_flag"][g],
+                                 cx_raw=d["c1_cx_raw"][g], mut_flag=d["c1_mut_flag"][g],
+                                 mut_mask=np.unpackbits(d["c1_mask"][g], axis=-1)[:, :100])
+            for g in range(40)]
+    tb = _toolbox("twopoint", "flipbit", 0.05, evaluate="onemax")
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 40, verbose=False, decisions=decs,
+                                   mode="inject")
+    g, wv, ok = pop.to_numpy()
+    assert np.array_equal(g, d["c1_final"])
+    assert np.array_equal(wv, d["c1_final_wv"])
+    assert log.select("nevals") == d["c1_nevals"].tolist()
+
+
+# ---------------------------------------------------------------------------
+# Native (counter-based RNG) mode: the decisions the device drew are dumped
+# and replayed into the oracle.
+# ---------------------------------------------------------------------------
+def _replay_native(gpu, gt, dim, n, cx, mut, objective, weights, seed):
+    from deap_amd import algorithms, tools
+    from deap_amd.ops import RandomStream
+    stream = RandomStream(seed)
+    low, high = (-5.12, 5.12) if gt != "bits" else (0, 1)
+    pop = tools.initPopulation(n=n, dim=dim, low=low, high=high, gtype=gt, weights=weights,
+                               stream=stream)
+    tb = _toolbox(cx, mut, 0.05, 0.5, evaluate=objective)
+    from deap_amd import benchmarks
+    getattr(benchmarks, objective)(pop)
+    g0, wv0, ok0 = pop.to_numpy()
+    decs = []
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 1, verbose=False, decisions=decs,
+                                   mode="dump", stream=stream)
+    g1, wv1, ok1 = pop.to_numpy()
+    dn = decs[0].numpy()
+    dec = {"aspirants": dn["aspirants"], "cx_flag": dn["cx_flag"].astype(bool),
+           "cx_raw": dn.get("cx_raw"), "blend_u": dn.get("blend_u"),
+           "mut_flag": dn["mut_flag"].astype(bool),
+           "mut_mask": ops.unpack_mask(dn["mut_mask"], dim), "gauss": dn.get("gauss")}
+    og, owv, ook, nev = ops.ea_generation(g0, wv0, ok0, 0.5, 0.2, cx, mut, dec, objective,
+                                          weights, 0.5)
+    return g1, wv1, og, owv, nev, log, dn, stream
+
+
+@pytest.mark.parametrize("gt,dim,n,cx,mut,objective,weights", [
+    ("f64", 1000, 512, "blend", "gaussian", "rastrigin", (-1.0,)),
+    ("f64", 1000, 256, "blend", "gaussian", "rosenbrock", (-1.0,)),
+    ("f32", 200, 300, "blend", "gaussian", "rastrigin", (-1.0,)),
+    ("f64", 77, 301, "twopoint", "gaussian", "sphere", (-1.0,)),
+    ("bits", 4096, 512, "twopoint", "flipbit", "onemax", (1.0,)),
+    ("bits", 100, 301, "twopoint", "flipbit", "onemax", (1.0,)),
+])
+def test_native_generation_replays_in_oracle(gpu, gt, dim, n, cx, mut, objective, weights):
+    g1, wv1, og, owv, nev, log, dn, _ = _replay_native(gpu, gt, dim, n, cx, mut, objective,
+                                                       weights, 1234)
+    assert np.array_equal(g1, og)
+    tol = 0 if objective == "onemax" else 1e-12
+    assert _rel_close(wv1, owv, tol)
+    assert log.select("nevals")[1] == nev
+
+
+def test_native_decisions_follow_the_documented_stream(gpu):
+    """Integer decisions of native mode recomputed from the Philox spec."""
+    from deap_amd import algorithms, tools, benchmarks
+    from deap_amd.ops import RandomStream
+    n, dim, seed = 1000, 40, 99
+    stream = RandomStream(seed, island=3)
+    pop = tools.initPopulation(n=n, dim=dim, low=-1, high=1, gtype="f64", weights=(-1.0,),
+                               stream=stream)
+    benchmarks.sphere(pop)
+    decs = []
+    gen_counter = stream.counter
+    algorithms.eaSimple(pop, _toolbox("twopoint", "gaussian", evaluate="sphere"), 0.5, 0.2, 1,
+                        verbose=False, decisions=decs, mode="dump", stream=stream)
+    dn = decs[0].numpy()
+    r = philox.Rng(seed, island=3, gen=gen_counter)
+    c = np.arange(n)
+    w = r(philox.ST_SEL, c, 0)
+    w1 = r(philox.ST_SEL, c, 1)
+    asp = np.stack([philox.bounded64(w[:, 0], w[:, 1], n), philox.bounded64(w[:, 2], w[:, 3], n),
+                    philox.bounded64(w1[:, 0], w1[:, 1], n)], 1)
+    assert np.array_equal(dn["aspirants"], asp)
+    p = np.arange(n // 2)
+    wc = r(philox.ST_CX, p, 0)
+    flags = wc[:, 0].astype(np.uint64) < philox.prob_threshold(0.5)
+    assert np.array_equal(dn["cx_flag"].astype(bool), flags)
+    wc2 = r(philox.ST_CX, p, 1)
+    r1 = 1 + philox.bounded64(wc[:, 2], wc[:, 3], dim)
+    r2 = 1 + philox.bounded64(wc2[:, 0], wc2[:, 1], dim - 1)
+    assert np.array_equal(dn["cx_raw"][flags], np.stack([r1, r2], 1)[flags])
+    wm = r(philox.ST_MUT, c, 0)
+    mflags = wm[:, 0].astype(np.uint64) < philox.prob_threshold(0.2)
+    assert np.array_equal(dn["mut_flag"].astype(bool), mflags)
+    # per-gene masks of float genomes
+    genes = np.arange(0, dim, 4)
+    mask = np.zeros((n, dim), bool)
+    for gi in genes:
+        ww = r(philox.ST_MASK, c, gi // 4)
+        for j in range(4):
+            if gi + j < dim:
+                mask[:, gi + j] = ww[:, j].astype(np.uint64) < philox.prob_threshold(0.05)
+    got = ops.unpack_mask(dn["mut_mask"], dim)
+    assert np.array_equal(got[mflags], mask[mflags])
+
+
+def test_sort_nondominated_large_random(gpu):
+    """Random 3-objective fronts at n=3000 vs the oracle (exact order)."""
+    from deap_amd import tools
+    rng = np.random.default_rng(5)
+    for kind in ("cont", "ties"):
+        n = 3000
+        wv = (rng.uniform(0, 1, size=(n, 3)) if kind == "cont"
+              else rng.integers(0, 12, size=(n, 3)).astype(np.float64))
+        pop = _dp().from_numpy(np.zeros((n, 2)), weights=(1.0, 1.0, 1.0), gtype="f64",
+                               wvalues=wv, valid=np.ones(n))
+        fronts = tools.sortNondominated(pop, n // 2)
+        want = ops.sort_nondominated(wv, n // 2)
+        assert [f.cpu().numpy().tolist() for f in fronts] == want
+        chosen = tools.selNSGA2(pop, n // 2).cpu().numpy().tolist()
+        want_c, _ = ops.sel_nsga2(wv, (1.0, 1.0, 1.0), n // 2)
+        assert chosen == want_c
+
+
+def test_sel_best_large_ties(gpu):
+    from deap_amd import tools
+    rng = np.random.default_rng(6)
+    n = 100000
+    wv = rng.integers(0, 50, size=(n, 2)).astype(np.float64)
+    wv[rng.integers(0, n, 100), 0] = -0.0
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0, -1.0), gtype="f64", wvalues=wv,
+                           valid=np.ones(n))
+    got = tools.selBest(pop, 500).cpu().numpy().tolist()
+    assert got == ops.sel_best(wv, 500).tolist()
+    got = tools.selWorst(pop, 500).cpu().numpy().tolist()
+    assert got == ops.sel_worst(wv, 500).tolist()
