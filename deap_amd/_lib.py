@@ -15,7 +15,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdeapmi.so")
+LIB_PATH = os.environ.get("DEAPMI_LIB") or os.path.join(_HERE, "libdeapmi.so")
 
 DM_OK, DM_ERR_INVALID, DM_ERR_INDEX, DM_ERR_HIP, DM_ERR_NOMEM, DM_ERR_UNSUPPORTED = range(6)
 DM_BITS, DM_F32, DM_F64 = 0, 1, 2

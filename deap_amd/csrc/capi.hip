@@ -247,7 +247,7 @@ template <typename T, int G>
 static void launch_eval_float(const dm_pop* p, const dm_eval* ev, int oi, int64_t* ne,
                               dim3 grid, hipStream_t s) {
     const int ec = eval_class(ev->fn);
-    if (ec == EC_SUM)
+    if (ec_single(ec))
         eval_float_kernel<T, G, EC_SUM><<<grid, 256, 0, s>>>((const char*)p->genes, p->stride,
                                                             p->wvalues, p->valid, p->n, p->dim,
                                                             p->nobj, *ev, oi, ne);

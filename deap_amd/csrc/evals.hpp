@@ -17,14 +17,23 @@ namespace dm {
 constexpr double PI = 3.141592653589793;  // math.pi
 
 // Classification of objectives by the evaluation template they need.
-enum EvalClass { EC_NONE = 0, EC_SUM = 1, EC_MO = 2 };
+enum EvalClass {
+    EC_NONE = 0,
+    EC_SUM = 1,    // single-objective sums, objective chosen at run time
+    EC_MO = 2,     // ZDT / DTLZ
+    EC_RAST = 3,   // rastrigin, specialised (benchmark hot path)
+    EC_ROSEN = 4   // rosenbrock, specialised
+};
+__host__ __device__ constexpr bool ec_single(int ec) {
+    return ec == EC_SUM || ec == EC_RAST || ec == EC_ROSEN;
+}
 
 __host__ __device__ inline int eval_class(int fn) {
     switch (fn) {
         case DM_EVAL_NONE: return EC_NONE;
+        case DM_EVAL_RASTRIGIN: return EC_RAST;
+        case DM_EVAL_ROSENBROCK: return EC_ROSEN;
         case DM_EVAL_ONEMAX:
-        case DM_EVAL_RASTRIGIN:
-        case DM_EVAL_ROSENBROCK:
         case DM_EVAL_SPHERE: return EC_SUM;
         default: return EC_MO;
     }
@@ -56,11 +65,55 @@ __host__ __device__ inline int mo_tail_start(const dm_eval& ev) {
     }
 }
 
+// cos(a) for an already-rounded fp64 argument a (the reference evaluates
+// cos(2*pi*gene) on the rounded product).  Cody-Waite reduction by pi/2 with
+// three FMA terms (exact enough for |a| < 2^20*pi/2) and fdlibm's
+// __kernel_sin/__kernel_cos minimax polynomials on |r| <= pi/4: <= 1 ulp,
+// i.e. agrees with glibc's correctly rounded cos to within 1 ulp.  Larger
+// arguments take ocml's Payne-Hanek path (never on the benchmark inputs).
+// Explicit fma() is used only where the algorithm requires it; the build's
+// -ffp-contract=off still forbids implicit contraction everywhere else.
+__device__ __noinline__ double cos_slow(double a) { return cos(a); }
+
+__device__ __forceinline__ double cos_fast(double a) {
+    if (!(fabs(a) < 1.6e6)) return cos_slow(a);
+    constexpr double TWO_OVER_PI = 0.63661977236758138243;
+    constexpr double PIO2_HI = 1.5707963267948966e+00;     // 0x3FF921FB54442D18
+    constexpr double PIO2_MID = 6.123233995736766e-17;     // 0x3C91A62633145C07
+    constexpr double PIO2_LO = -1.4973849048591698e-33;    // 0xB91F1976B7ED8FBC
+    const double q = rint(a * TWO_OVER_PI);
+    double r = fma(-q, PIO2_HI, a);
+    r = fma(-q, PIO2_MID, r);
+    r = fma(-q, PIO2_LO, r);
+    const int quad = (int)(int64_t)q & 3;
+    const double z = r * r;
+    // __kernel_cos (y = 0)
+    const double cr = z * (4.16666666666666019037e-02 +
+                      z * (-1.38888888888741095749e-03 +
+                      z * (2.48015872894767294178e-05 +
+                      z * (-2.75573143513906633035e-07 +
+                      z * (2.08757232129817482790e-09 +
+                      z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * cr);
+    // __kernel_sin (y = 0)
+    const double v = z * r;
+    const double sr = 8.33333333332248946124e-03 +
+                      z * (-1.98412698298579493134e-04 +
+                      z * (2.75573137070700676789e-06 +
+                      z * (-2.50507602534068634195e-08 +
+                      z * 1.58969099521155010221e-10)));
+    const double sn = r + v * (-1.66666666666666324348e-01 + z * sr);
+    const double mag = (quad & 1) ? sn : c;
+    return (quad == 1 || quad == 2) ? -mag : mag;
+}
+
 // Per-gene term of a single-objective sum (EC_SUM) for gene x.
 __device__ __forceinline__ double sum_term(int fn, double x) {
     switch (fn) {
         case DM_EVAL_RASTRIGIN:  // gene*gene - 10*cos(2*pi*gene)          :239-240
-            return x * x - 10.0 * cos((2.0 * PI) * x);
+            return x * x - 10.0 * cos_fast((2.0 * PI) * x);
         case DM_EVAL_SPHERE:  // gene*gene                                   :77
             return x * x;
         default:  // ONEMAX on real-valued genes: sum(individual)
@@ -195,8 +248,10 @@ __device__ __forceinline__ void eval_chunk(const dm_eval& ev, int dim, int gbase
     const int lane = threadIdx.x & 63;
     const int gl0 = lane & ~(G - 1);  // first lane of this group
     const int sub = lane & (G - 1);
-    if constexpr (EC == EC_SUM) {
-        if (ev.fn == DM_EVAL_ROSENBROCK) {
+    if constexpr (ec_single(EC)) {
+        const int fn = EC == EC_RAST ? (int)DM_EVAL_RASTRIGIN
+                       : EC == EC_ROSEN ? (int)DM_EVAL_ROSENBROCK : ev.fn;
+        if (fn == DM_EVAL_ROSENBROCK) {
             const double nb = __shfl(y[0], gl0 + ((sub + 1) & (G - 1)), 64);
             const double last = __shfl(y[3], gl0 + G - 1, 64);
             if (active) {
@@ -217,7 +272,7 @@ __device__ __forceinline__ void eval_chunk(const dm_eval& ev, int dim, int gbase
 #pragma unroll 1
                 for (int j = 0; j < nj; ++j) {
                     const double x = j == 0 ? y[0] : j == 1 ? y[1] : j == 2 ? y[2] : y[3];
-                    acc += sum_term(ev.fn, x);
+                    acc += sum_term(fn, x);
                 }
                 st.s += acc;
             }
@@ -255,8 +310,8 @@ template <int G, int EC>
 __device__ __forceinline__ void eval_finish(const dm_eval& ev, int dim, EvalState& st,
                                             double* f) {
     const double S = group_sum<G>(st.s);
-    if constexpr (EC == EC_SUM) {
-        if (ev.fn == DM_EVAL_RASTRIGIN)
+    if constexpr (ec_single(EC)) {
+        if (EC == EC_RAST || (EC == EC_SUM && ev.fn == DM_EVAL_RASTRIGIN))
             f[0] = (double)(10 * (int64_t)dim) + S;  // 10*len(individual) + sum(...)
         else
             f[0] = S;

@@ -1,7 +1,7 @@
 // generation.hip — host side of the fused generation (see generation.hpp for
 // the kernels; per-genome-type instantiations live in generation_{f64,f32,bits}.hip
 // so they compile in parallel).
-#include "generation.hpp"
+#include "generation_rows.hpp"
 
 namespace dm {
 
@@ -100,6 +100,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                           ? (float)(1.0 / std::log2(1.0 - var->indpb))
                           : 0.0f;
     a.eval_fn = ev->fn;
+    a.w0 = ev->weights[0];
     a.ev = *ev;
     a.rng = Rng(rng);
     a.mode = mode;
@@ -108,6 +109,22 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
 
     const int ec = eval_class(ev->fn);
     const int64_t npairs = (children->n + 1) / 2;
+    // hot path: native RNG, float rows of 65..1024 genes, fused tournament / random
+    // selection -> whole-row kernel with lane-parallel decisions
+    if (mode == DM_RNG_NATIVE && parents->gtype != DM_BITS && parents->dim > 64 &&
+        parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
+        tournsize <= 30 && ec != EC_MO && !std::getenv("DM_DISABLE_ROWS")) {
+        const int nch = parents->dim <= 512 ? 2 : 4;
+        int64_t blocks = (npairs + 3) / 4;
+        blocks = std::min<int64_t>(blocks, (int64_t)ctx->num_cus * 8);
+        const dim3 grid((unsigned)std::max<int64_t>(blocks, 1));
+        if (parents->gtype == DM_F64)
+            launch_gen_rows_f64(a, ec, nch, grid, ctx->stream);
+        else
+            launch_gen_rows_f32(a, ec, nch, grid, ctx->stream);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
     const int G = parents->gtype == DM_BITS ? pick_group_bits(a.words64)
                                             : pick_group_float(parents->dim);
     const int64_t groups_per_block = 256 / G;
@@ -117,9 +134,11 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     if (parents->gtype == DM_BITS)
         launch_gen_bits(a, ec, G, grid, ctx->stream);
     else if (parents->gtype == DM_F64)
-        launch_gen_f64(a, ec, G, grid, ctx->stream);
+        (mode == DM_RNG_NATIVE ? launch_gen_f64_native : launch_gen_f64_replay)(a, ec, G, grid,
+                                                                                 ctx->stream);
     else
-        launch_gen_f32(a, ec, G, grid, ctx->stream);
+        (mode == DM_RNG_NATIVE ? launch_gen_f32_native : launch_gen_f32_replay)(a, ec, G, grid,
+                                                                                 ctx->stream);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

@@ -36,6 +36,7 @@ struct GenArgs {
     const double* sigma_vec;
     float flip_inv_log2;  // 1 / log2(1 - indpb) for geometric skips
     int32_t eval_fn;
+    double w0;  // ev.weights[0]
     dm_eval ev;
     Rng rng;
     int32_t mode;
@@ -47,6 +48,7 @@ struct GenArgs {
 // Selection of the parent of child c (all lanes of the group compute the same
 // value; only the group leader writes dumped decisions).
 // ---------------------------------------------------------------------------
+template <bool RP>
 __device__ __forceinline__ int64_t parent_of(const GenArgs& a, int64_t c, bool leader) {
     if (a.sel == DM_SEL_IDENTITY) return c;
     if (a.sel == DM_SEL_INDEX) return a.sel_index[c];
@@ -55,12 +57,12 @@ __device__ __forceinline__ int64_t parent_of(const GenArgs& a, int64_t c, bool l
     int64_t best = 0;
     for (int j = 0; j < t; ++j) {
         int64_t cand;
-        if (a.mode == DM_RNG_INJECT) {
+        if ((RP && a.mode == DM_RNG_INJECT)) {
             cand = a.dec.aspirants[c * t + j];
         } else {
             const u32x4 w = a.rng(ST_SEL, (uint32_t)c, (uint32_t)(j >> 1));
             cand = (j & 1) ? bounded64(w.z, w.w, (uint32_t)a.np) : bounded64(w.x, w.y, (uint32_t)a.np);
-            if (a.mode == DM_RNG_DUMP && leader) a.dec.aspirants[c * t + j] = (int32_t)cand;
+            if ((RP && a.mode == DM_RNG_DUMP) && leader) a.dec.aspirants[c * t + j] = (int32_t)cand;
         }
         if (a.sel == DM_SEL_RANDOM) return cand;  // selRandom: k draws of one aspirant
         if (j == 0) {
@@ -78,13 +80,14 @@ struct PairDecisions {
     bool mut0, mut1;
 };
 
+template <bool RP>
 __device__ __forceinline__ PairDecisions pair_decisions(const GenArgs& a, int64_t p, bool has1,
                                                         bool leader) {
     PairDecisions d{};
     const int64_t c0 = 2 * p, c1i = 2 * p + 1;
     int32_t r1 = 0, r2 = 0;
     if (has1 && a.cx != DM_CX_NONE) {
-        if (a.mode == DM_RNG_INJECT) {
+        if ((RP && a.mode == DM_RNG_INJECT)) {
             d.cx = a.dec.cx_flag[p] != 0;
             if (a.cx == DM_CX_TWOPOINT && d.cx) {
                 r1 = a.dec.cx_raw[2 * p];
@@ -99,7 +102,7 @@ __device__ __forceinline__ PairDecisions pair_decisions(const GenArgs& a, int64_
                 r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
                 r2 = 1 + (int32_t)bounded64(w2.x, w2.y, (uint32_t)(a.dim - 1));
             }
-            if (a.mode == DM_RNG_DUMP && leader) {
+            if ((RP && a.mode == DM_RNG_DUMP) && leader) {
                 a.dec.cx_flag[p] = d.cx;
                 if (a.dec.cx_raw) {
                     a.dec.cx_raw[2 * p] = r1;
@@ -121,13 +124,13 @@ __device__ __forceinline__ PairDecisions pair_decisions(const GenArgs& a, int64_
         }
     }
     if (a.mut != DM_MUT_NONE) {
-        if (a.mode == DM_RNG_INJECT) {
+        if ((RP && a.mode == DM_RNG_INJECT)) {
             d.mut0 = a.dec.mut_flag[c0] != 0;
             d.mut1 = has1 && a.dec.mut_flag[c1i] != 0;
         } else {
             d.mut0 = (uint64_t)a.rng(ST_MUT, (uint32_t)c0, 0).x < a.thr_mut;
             d.mut1 = has1 && (uint64_t)a.rng(ST_MUT, (uint32_t)c1i, 0).x < a.thr_mut;
-            if (a.mode == DM_RNG_DUMP && leader) {
+            if ((RP && a.mode == DM_RNG_DUMP) && leader) {
                 a.dec.mut_flag[c0] = d.mut0;
                 if (has1) a.dec.mut_flag[c1i] = d.mut1;
             }
@@ -176,16 +179,28 @@ struct Vec4<float> {
 // Per-gene Gaussian mutation of one child's chunk (mutation.py:44-46).
 // Returns the 4-bit mask of mutated genes; the normal draws happen in
 // gauss_apply so only one inlined copy of log/cos/sqrt exists.
+// Standard normal draw for (child, gene): Box-Muller on two 53-bit uniforms.
+// Out of line: the normal transform is rare (indpb of the genes of mutated
+// children) and keeping its log/cos/sqrt out of the streaming loop saves ~50
+// VGPRs there.
+__device__ __noinline__ double std_normal(Rng rng, int64_t c, int gi) {
+    const u32x4 z = rng(ST_GAUSS, (uint32_t)c, (uint32_t)gi);
+    const double u1 = u01_53(z.x, z.y);
+    const double u2 = u01_53(z.z, z.w);
+    return cos_fast((2.0 * PI) * u1) * sqrt(-2.0 * log(1.0 - u2));
+}
+
+template <bool RP>
 __device__ __forceinline__ uint32_t gauss_mask(const GenArgs& a, int64_t c, int g) {
     uint32_t bits = 0;
-    if (a.mode == DM_RNG_INJECT) {
+    if ((RP && a.mode == DM_RNG_INJECT)) {
         const uint64_t word = a.dec.mut_mask[c * a.words64 + (g >> 6)];
         bits = (uint32_t)(word >> (g & 63)) & 0xFu;
     } else {
         const u32x4 w = a.rng(ST_MASK, (uint32_t)c, (uint32_t)(g >> 2));
         bits = ((uint64_t)w.x < a.thr_ind ? 1u : 0u) | ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
                ((uint64_t)w.z < a.thr_ind ? 4u : 0u) | ((uint64_t)w.w < a.thr_ind ? 8u : 0u);
-        if (a.mode == DM_RNG_DUMP && bits) {
+        if ((RP && a.mode == DM_RNG_DUMP) && bits) {
             atomicOr((unsigned long long*)&a.dec.mut_mask[c * a.words64 + (g >> 6)],
                      (unsigned long long)bits << (g & 63));
         }
@@ -194,19 +209,18 @@ __device__ __forceinline__ uint32_t gauss_mask(const GenArgs& a, int64_t c, int 
     if (valid < 4) bits &= (1u << max(valid, 0)) - 1u;
     return bits;
 }
+template <bool RP>
 __device__ __forceinline__ double gauss_value(const GenArgs& a, int64_t c, int gi) {
-    if (a.mode == DM_RNG_INJECT) return a.dec.gauss[c * a.dim + gi];
-    const u32x4 z = a.rng(ST_GAUSS, (uint32_t)c, (uint32_t)gi);
-    const double u1 = u01_53(z.x, z.y);
-    const double u2 = u01_53(z.z, z.w);
-    const double nrm = cos((2.0 * PI) * u1) * sqrt(-2.0 * log(1.0 - u2));
+    if ((RP && a.mode == DM_RNG_INJECT)) return a.dec.gauss[c * a.dim + gi];
+    const double nrm = std_normal(a.rng, c, gi);
     const double m = a.mu_vec ? a.mu_vec[gi] : a.mu;
     const double s = a.sigma_vec ? a.sigma_vec[gi] : a.sigma;
     const double gv = m + nrm * s;  // random.gauss(mu, sigma) = mu + z*sigma
-    if (a.mode == DM_RNG_DUMP) a.dec.gauss[c * a.dim + gi] = gv;
+    if ((RP && a.mode == DM_RNG_DUMP)) a.dec.gauss[c * a.dim + gi] = gv;
     return gv;
 }
 // Apply the Gaussian steps of both children: bits 0-3 child 0, 4-7 child 1.
+template <bool RP>
 __device__ __forceinline__ void gauss_apply(const GenArgs& a, int64_t c0, int g, uint32_t bits,
                                             double (&y0)[4], double (&y1)[4]) {
 #pragma unroll 1
@@ -214,7 +228,7 @@ __device__ __forceinline__ void gauss_apply(const GenArgs& a, int64_t c0, int g,
         const int b = __builtin_ctz(bits);
         bits &= bits - 1;
         const int j = b & 3;
-        const double gv = gauss_value(a, c0 + (b >> 2), g + j);
+        const double gv = gauss_value<RP>(a, c0 + (b >> 2), g + j);
         if (b < 4) {
             y0[0] = j == 0 ? y0[0] + gv : y0[0];
             y0[1] = j == 1 ? y0[1] + gv : y0[1];
@@ -229,8 +243,14 @@ __device__ __forceinline__ void gauss_apply(const GenArgs& a, int64_t c0, int g,
     }
 }
 
-template <typename T, int G, int CX, int MUT, int EC>
-__global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
+#ifndef DM_GEN_MINWAVES
+#define DM_GEN_MINWAVES 4
+#endif
+#ifndef DM_GEN_PREFETCH
+#define DM_GEN_PREFETCH 1
+#endif
+template <typename T, int G, int CX, int MUT, int EC, bool RP>
+__global__ __launch_bounds__(256, DM_GEN_MINWAVES) void gen_float_kernel(GenArgs a) {
     const int lane = threadIdx.x & 63;
     const int sub = lane & (G - 1);
     const bool leader = sub == 0;
@@ -241,9 +261,9 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
          p += gstride) {
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const bool has1 = c1 < a.nc;
-        const int64_t s0 = parent_of(a, c0, leader);
-        const int64_t s1 = has1 ? parent_of(a, c1, leader) : s0;
-        const PairDecisions d = pair_decisions(a, p, has1, leader);
+        const int64_t s0 = parent_of<RP>(a, c0, leader);
+        const int64_t s1 = has1 ? parent_of<RP>(a, c1, leader) : s0;
+        const PairDecisions d = pair_decisions<RP>(a, p, has1, leader);
         const bool inv0 = d.cx || d.mut0 || !a.pvalid[s0];
         const bool inv1 = has1 && (d.cx || d.mut1 || !a.pvalid[s1]);
         const bool do_eval = EC != EC_NONE;
@@ -257,18 +277,36 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
         eval_init(e1);
         const double gamma_scale = 1.0 + 2.0 * a.alpha;  // (1. + 2. * alpha)
 
+        // software pipeline: the next chunk's parent loads are in flight while
+        // the current chunk is varied, evaluated and stored
+        double n0[4] = {0, 0, 0, 0}, n1[4] = {0, 0, 0, 0};
+        if (DM_GEN_PREFETCH && 4 * sub < a.dim) {
+            Vec4<T>::load(r0, 4 * sub, n0);
+            if (has1) Vec4<T>::load(r1, 4 * sub, n1);
+        }
         for (int cbase = 0; cbase < a.dim; cbase += 4 * G) {
             const int g = cbase + 4 * sub;
-            double y0[4] = {0, 0, 0, 0}, y1[4] = {0, 0, 0, 0};
+            double y0[4], y1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                y0[j] = n0[j];
+                y1[j] = n1[j];
+            }
             const bool in = g < a.dim;
-            if (in) {
+            if (DM_GEN_PREFETCH) {
+                const int gn = g + 4 * G;
+                if (gn < a.dim) {
+                    Vec4<T>::load(r0, gn, n0);
+                    if (has1) Vec4<T>::load(r1, gn, n1);
+                }
+            } else if (in) {
                 Vec4<T>::load(r0, g, y0);
                 if (has1) Vec4<T>::load(r1, g, y1);
             }
             if (CX == DM_CX_BLEND && d.cx && in) {
                 // gamma = (1. + 2.*alpha)*random() - alpha ; y1/y2 blend  (crossover.py:255-258)
                 double u[4];
-                if (a.mode == DM_RNG_INJECT) {
+                if ((RP && a.mode == DM_RNG_INJECT)) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         u[j] = (g + j < a.dim) ? a.dec.blend_u[p * a.dim + g + j] : 0.0;
@@ -278,7 +316,7 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
                     u[1] = u01_32(w.y);
                     u[2] = u01_32(w.z);
                     u[3] = u01_32(w.w);
-                    if (a.mode == DM_RNG_DUMP) {
+                    if ((RP && a.mode == DM_RNG_DUMP)) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
                             if (g + j < a.dim) a.dec.blend_u[p * a.dim + g + j] = u[j];
@@ -304,11 +342,19 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
                     }
                 }
             }
+            if constexpr (sizeof(T) == 4) {
+                // array('f') stores the crossover result (rounded) before mutation reads it
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    y0[j] = (double)(float)y0[j];
+                    y1[j] = (double)(float)y1[j];
+                }
+            }
             if (MUT == DM_MUT_GAUSSIAN && in) {
                 uint32_t bits = 0;
-                if (d.mut0) bits |= gauss_mask(a, c0, g);
-                if (d.mut1) bits |= gauss_mask(a, c1, g) << 4;
-                gauss_apply(a, c0, g, bits, y0, y1);
+                if (d.mut0) bits |= gauss_mask<RP>(a, c0, g);
+                if (d.mut1) bits |= gauss_mask<RP>(a, c1, g) << 4;
+                gauss_apply<RP>(a, c0, g, bits, y0, y1);
             }
             if (in) {
                 Vec4<T>::store(w0, g, y0);
@@ -333,12 +379,18 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
             eval_finish<G, EC>(a.ev, a.dim, e1, f1);
         }
         if (leader) {
-            const int m = a.nobj;
-            for (int o = 0; o < m; ++o) {
-                a.cwv[c0 * m + o] = (do_eval && inv0) ? f0[o] * a.ev.weights[o] : a.pwv[s0 * m + o];
-                if (has1)
-                    a.cwv[c1 * m + o] =
-                        (do_eval && inv1) ? f1[o] * a.ev.weights[o] : a.pwv[s1 * m + o];
+            if constexpr (ec_single(EC)) {  // one objective
+                a.cwv[c0] = inv0 ? f0[0] * a.w0 : a.pwv[s0];
+                if (has1) a.cwv[c1] = inv1 ? f1[0] * a.w0 : a.pwv[s1];
+            } else {
+                const int m = a.nobj;
+                for (int o = 0; o < m; ++o) {
+                    a.cwv[c0 * m + o] =
+                        (do_eval && inv0) ? f0[o] * a.ev.weights[o] : a.pwv[s0 * m + o];
+                    if (has1)
+                        a.cwv[c1 * m + o] =
+                            (do_eval && inv1) ? f1[o] * a.ev.weights[o] : a.pwv[s1 * m + o];
+                }
             }
             a.cvalid[c0] = do_eval ? 1 : (inv0 ? 0 : 1);
             if (has1) a.cvalid[c1] = do_eval ? 1 : (inv1 ? 0 : 1);
@@ -358,6 +410,8 @@ __global__ __launch_bounds__(256) void gen_float_kernel(GenArgs a) {
 // Packed-bit genomes: chunk = one u64 word per lane (64 genes).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, hi) of a word
+    lo = max(lo, 0);
+    hi = min(hi, 64);
     if (hi <= lo) return 0;
     const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
     const uint64_t dn = lo <= 0 ? 0ull : ((1ull << lo) - 1);
@@ -365,8 +419,9 @@ __device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, h
 }
 
 // mutFlipBit on one word (mutation.py:139-141): Bernoulli(indpb) per gene.
+template <bool RP>
 __device__ __forceinline__ uint64_t flip_mask_word(const GenArgs& a, int64_t c, int wi) {
-    if (a.mode == DM_RNG_INJECT) return a.dec.mut_mask[c * a.words64 + wi];
+    if ((RP && a.mode == DM_RNG_INJECT)) return a.dec.mut_mask[c * a.words64 + wi];
     const int nbits = min(64, a.dim - wi * 64);
     uint64_t mask = 0;
     if (a.thr_ind >= (1ull << 32)) {
@@ -391,11 +446,11 @@ __device__ __forceinline__ uint64_t flip_mask_word(const GenArgs& a, int64_t c, 
             if (done || call >= 255) break;
         }
     }
-    if (a.mode == DM_RNG_DUMP) a.dec.mut_mask[c * a.words64 + wi] = mask;
+    if ((RP && a.mode == DM_RNG_DUMP)) a.dec.mut_mask[c * a.words64 + wi] = mask;
     return mask;
 }
 
-template <int G, int CX, int MUT, int EC>
+template <int G, int CX, int MUT, int EC, bool RP>
 __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
     const int lane = threadIdx.x & 63;
     const int sub = lane & (G - 1);
@@ -407,9 +462,9 @@ __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
          p += gstride) {
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const bool has1 = c1 < a.nc;
-        const int64_t s0 = parent_of(a, c0, leader);
-        const int64_t s1 = has1 ? parent_of(a, c1, leader) : s0;
-        const PairDecisions d = pair_decisions(a, p, has1, leader);
+        const int64_t s0 = parent_of<RP>(a, c0, leader);
+        const int64_t s1 = has1 ? parent_of<RP>(a, c1, leader) : s0;
+        const PairDecisions d = pair_decisions<RP>(a, p, has1, leader);
         const bool inv0 = d.cx || d.mut0 || !a.pvalid[s0];
         const bool inv1 = has1 && (d.cx || d.mut1 || !a.pvalid[s1]);
         const uint64_t* r0 = reinterpret_cast<const uint64_t*>(a.pgenes + s0 * a.pstride);
@@ -429,8 +484,8 @@ __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
                     x1 ^= t;
                 }
                 if (MUT == DM_MUT_FLIPBIT) {
-                    if (d.mut0) x0 ^= flip_mask_word(a, c0, wi);
-                    if (d.mut1) x1 ^= flip_mask_word(a, c1, wi);
+                    if (d.mut0) x0 ^= flip_mask_word<RP>(a, c0, wi);
+                    if (d.mut1) x1 ^= flip_mask_word<RP>(a, c1, wi);
                 }
                 w0[wi] = x0;
                 if (has1) w1[wi] = x1;
@@ -465,8 +520,10 @@ __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
     }
 }
 
-void launch_gen_f64(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
-void launch_gen_f32(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_f64_native(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_f64_replay(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_f32_native(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
+void launch_gen_f32_replay(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
 void launch_gen_bits(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s);
 
 }  // namespace dm

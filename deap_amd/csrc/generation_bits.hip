@@ -3,12 +3,19 @@
 
 namespace dm {
 
+template <int G, int CX, int MUT, bool RP>
+static void launch_m(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {
+    if (ec != EC_NONE)
+        gen_bits_kernel<G, CX, MUT, EC_SUM, RP><<<grid, 256, 0, s>>>(a);
+    else
+        gen_bits_kernel<G, CX, MUT, EC_NONE, RP><<<grid, 256, 0, s>>>(a);
+}
 template <int G, int CX, int MUT>
 static void launch_g(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {
-    if (ec != EC_NONE)
-        gen_bits_kernel<G, CX, MUT, EC_SUM><<<grid, 256, 0, s>>>(a);
+    if (a.mode == DM_RNG_NATIVE)
+        launch_m<G, CX, MUT, false>(a, ec, grid, s);
     else
-        gen_bits_kernel<G, CX, MUT, EC_NONE><<<grid, 256, 0, s>>>(a);
+        launch_m<G, CX, MUT, true>(a, ec, grid, s);
 }
 template <int G>
 static void launch_ops(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {

@@ -1,16 +1,21 @@
-// generation_f32.hip — float-genome instantiations of the fused generation kernel.
+// generation_f32_replay.hip — float-genome instantiations of the fused
+// generation kernel, replay mode (split per file so hipcc runs in parallel).
 #include "generation.hpp"
 
 namespace dm {
 
 template <int G, int CX, int MUT>
 static void launch_g(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {
-    if (ec == EC_SUM)
-        gen_float_kernel<float, G, CX, MUT, EC_SUM><<<grid, 256, 0, s>>>(a);
+    if (G == 64 && ec == EC_RAST)
+        gen_float_kernel<float, G, CX, MUT, EC_RAST, true><<<grid, 256, 0, s>>>(a);
+    else if (G == 64 && ec == EC_ROSEN)
+        gen_float_kernel<float, G, CX, MUT, EC_ROSEN, true><<<grid, 256, 0, s>>>(a);
+    else if (ec_single(ec))
+        gen_float_kernel<float, G, CX, MUT, EC_SUM, true><<<grid, 256, 0, s>>>(a);
     else if (ec == EC_MO)
-        gen_float_kernel<float, G, CX, MUT, EC_MO><<<grid, 256, 0, s>>>(a);
+        gen_float_kernel<float, G, CX, MUT, EC_MO, true><<<grid, 256, 0, s>>>(a);
     else
-        gen_float_kernel<float, G, CX, MUT, EC_NONE><<<grid, 256, 0, s>>>(a);
+        gen_float_kernel<float, G, CX, MUT, EC_NONE, true><<<grid, 256, 0, s>>>(a);
 }
 template <int G>
 static void launch_ops(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {
@@ -29,7 +34,7 @@ static void launch_ops(const GenArgs& a, int ec, dim3 grid, hipStream_t s) {
                : launch_g<G, DM_CX_NONE, DM_MUT_NONE>(a, ec, grid, s);
     }
 }
-void launch_gen_f32(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s) {
+void launch_gen_f32_replay(const GenArgs& a, int ec, int G, dim3 grid, hipStream_t s) {
     switch (G) {
         case 4: launch_ops<4>(a, ec, grid, s); break;
         case 16: launch_ops<16>(a, ec, grid, s); break;

@@ -314,7 +314,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     // ---- workspace: everything O(n) in slot 0 (U <= n), D in slot 1 ----
     const int64_t max_chunks = 64;
     const size_t nb8 = align_up((size_t)n * 8, 256), nb4 = align_up((size_t)(n + 2) * 4, 256);
-    const size_t need = 2 * nb8 + 16 * nb4 + align_up((size_t)n * m * 8, 256) +
+    const size_t need = 2 * nb8 + 20 * nb4 + align_up((size_t)n * m * 8, 256) +
                         2 * align_up((size_t)max_chunks * n * 4, 256) +
                         radix_sort_temp_bytes(n) + scan_temp_bytes(n) + 8192;
     char* base = (char*)scratch(ctx, need);

@@ -125,9 +125,13 @@ __global__ __launch_bounds__(256) void varor_float_kernel(GenArgs a, double cxpb
                         if (g + j >= d.c1 && g + j < d.c2) y[j] = x2[j];
                 }
             }
+            if constexpr (sizeof(T) == 4) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (double)(float)y[j];
+            }
             if (d.op == 1 && in && a.mut == DM_MUT_GAUSSIAN) {
                 double dummy[4] = {0, 0, 0, 0};
-                gauss_apply(a, c, g, gauss_mask(a, c, g), y, dummy);
+                gauss_apply<true>(a, c, g, gauss_mask<true>(a, c, g), y, dummy);
             }
             if (in) Vec4<T>::store(wc, g, y);
             if constexpr (sizeof(T) == 4) {
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(256) void varor_bits_kernel(GenArgs a, double cxpb,
                 const uint64_t m = range_mask(d.c1 - wi * 64, d.c2 - wi * 64);
                 x = (x & ~m) | (rb[wi] & m);
             }
-            if (d.op == 1 && a.mut == DM_MUT_FLIPBIT) x ^= flip_mask_word(a, c, wi);
+            if (d.op == 1 && a.mut == DM_MUT_FLIPBIT) x ^= flip_mask_word<true>(a, c, wi);
             wc[wi] = x;
             pc += __popcll(x);
         }
@@ -204,7 +208,7 @@ int validate_variation(const dm_variation* v, const dm_pop* p);
 template <typename T, int G>
 static void launch_varor_float(const GenArgs& a, int ec, dim3 grid, hipStream_t s, double cxpb,
                                double cxmutpb) {
-    if (ec == EC_SUM)
+    if (ec_single(ec))
         varor_float_kernel<T, G, EC_SUM><<<grid, 256, 0, s>>>(a, cxpb, cxmutpb);
     else if (ec == EC_MO)
         varor_float_kernel<T, G, EC_MO><<<grid, 256, 0, s>>>(a, cxpb, cxmutpb);
@@ -282,6 +286,7 @@ extern "C" int dm_var_or(dm_ctx* ctx, const dm_pop* parents, dm_pop* children,
                           ? (float)(1.0 / std::log2(1.0 - var->indpb))
                           : 0.0f;
     a.eval_fn = ev->fn;
+    a.w0 = ev->weights[0];
     a.ev = *ev;
     a.rng = Rng(rng);
     a.mode = mode;

@@ -374,3 +374,37 @@ def test_sel_best_large_ties(gpu):
     assert got == ops.sel_best(wv, 500).tolist()
     got = tools.selWorst(pop, 500).cpu().numpy().tolist()
     assert got == ops.sel_worst(wv, 500).tolist()
+
+
+@pytest.mark.parametrize("gt,dim,n,cx,mut,objective,sel", [
+    ("f64", 1000, 1000, "blend", "gaussian", "rastrigin", "tournament"),
+    ("f64", 1000, 257, "blend", "gaussian", "rosenbrock", "tournament"),
+    ("f64", 300, 400, "twopoint", "gaussian", "sphere", "tournament"),
+    ("f32", 200, 300, "blend", "gaussian", "rastrigin", "tournament"),
+    ("f64", 513, 64, "blend", "gaussian", "rastrigin", "random"),
+])
+def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
+    """The whole-row hot kernel (native mode, lane-parallel decisions) draws
+    the same decisions as the replay kernel's dump mode and produces the same
+    generation bit for bit (the dump mode is itself replayed in the oracle)."""
+    from deap_amd import algorithms, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    outs = []
+    for mode in ("native", "dump"):
+        stream = RandomStream(77)
+        pop = tools.initPopulation(n=n, dim=dim, low=-3, high=3, gtype=gt, weights=(-1.0,),
+                                   stream=stream)
+        getattr(benchmarks, objective)(pop)
+        tb = _toolbox(cx, mut, 0.05, 0.5, evaluate=objective)
+        if sel == "random":
+            tb.register("select", tools.selRandom)
+        decs = [] if mode == "dump" else None
+        pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 2, verbose=False, decisions=decs,
+                                       mode=mode, stream=stream)
+        outs.append((pop.to_numpy(), log.select("nevals")))
+    (g1, wv1, ok1), nev1 = outs[0]
+    (g2, wv2, ok2), nev2 = outs[1]
+    assert np.array_equal(g1, g2)
+    assert np.array_equal(ok1, ok2)
+    assert np.array_equal(wv1, wv2)
+    assert nev1 == nev2
