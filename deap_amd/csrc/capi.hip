@@ -8,6 +8,21 @@
 
 namespace dm {
 
+// Layer edges of the 256-layer normal ziggurat: equal-area (V) layers under
+// f(x) = exp(-x^2/2), R = 3.6541528853610088 (Marsaglia & Tsang 2000).
+int zig_make_tables(double* t) {
+    const double R = 3.6541528853610088, V = 0.00492867323399;
+    double* x = t;
+    double* f = t + (ZIG_N + 1);
+    x[0] = V / std::exp(-0.5 * R * R);
+    x[1] = R;
+    for (int i = 2; i < ZIG_N; ++i)
+        x[i] = std::sqrt(-2.0 * std::log(V / x[i - 1] + std::exp(-0.5 * x[i - 1] * x[i - 1])));
+    x[ZIG_N] = 0.0;
+    for (int i = 0; i <= ZIG_N; ++i) f[i] = std::exp(-0.5 * x[i] * x[i]);
+    return DM_OK;
+}
+
 static thread_local char g_err[1024] = "";
 
 void set_error(const char* fmt, ...) {
@@ -406,6 +421,14 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
         c->num_cus = cus;
+    double tab[2 * (ZIG_N + 1)];
+    zig_make_tables(tab);
+    if (hipMalloc(&c->zig, sizeof(tab)) != hipSuccess ||
+        hipMemcpy(c->zig, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("ziggurat table upload failed");
+        delete c;
+        return DM_ERR_HIP;
+    }
     *out = c;
     return DM_OK;
 }
@@ -416,6 +439,7 @@ int dm_ctx_destroy(dm_ctx* ctx) {
     for (int i = 0; i < dm_ctx::kSlots; ++i)
         if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->zig) (void)hipFree(ctx->zig);
     delete ctx;
     return DM_OK;
 }

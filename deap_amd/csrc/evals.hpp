@@ -75,8 +75,8 @@ __host__ __device__ inline int mo_tail_start(const dm_eval& ev) {
 // -ffp-contract=off still forbids implicit contraction everywhere else.
 __device__ __noinline__ double cos_slow(double a) { return cos(a); }
 
-__device__ __forceinline__ double cos_fast(double a) {
-    if (!(fabs(a) < 1.6e6)) return cos_slow(a);
+// Reduction + polynomials only (caller guarantees |a| < 1.6e6).
+__device__ __forceinline__ double cos_core(double a) {
     constexpr double TWO_OVER_PI = 0.63661977236758138243;
     constexpr double PIO2_HI = 1.5707963267948966e+00;     // 0x3FF921FB54442D18
     constexpr double PIO2_MID = 6.123233995736766e-17;     // 0x3C91A62633145C07
@@ -87,26 +87,36 @@ __device__ __forceinline__ double cos_fast(double a) {
     r = fma(-q, PIO2_LO, r);
     const int quad = (int)(int64_t)q & 3;
     const double z = r * r;
-    // __kernel_cos (y = 0)
-    const double cr = z * (4.16666666666666019037e-02 +
-                      z * (-1.38888888888741095749e-03 +
-                      z * (2.48015872894767294178e-05 +
-                      z * (-2.75573143513906633035e-07 +
-                      z * (2.08757232129817482790e-09 +
-                      z * -1.13596475577881948265e-11)))));
+    // __kernel_cos (y = 0), Horner with explicit FMAs
+    double cr = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    cr = fma(z, cr, -2.75573143513906633035e-07);
+    cr = fma(z, cr, 2.48015872894767294178e-05);
+    cr = fma(z, cr, -1.38888888888741095749e-03);
+    cr = fma(z, cr, 4.16666666666666019037e-02);
+    cr = z * cr;
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
-    const double c = w + (((1.0 - w) - hz) + z * cr);
+    const double c = w + fma(z, cr, (1.0 - w) - hz);
     // __kernel_sin (y = 0)
+    double sr = fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    sr = fma(z, sr, 2.75573137070700676789e-06);
+    sr = fma(z, sr, -1.98412698298579493134e-04);
+    sr = fma(z, sr, 8.33333333332248946124e-03);
     const double v = z * r;
-    const double sr = 8.33333333332248946124e-03 +
-                      z * (-1.98412698298579493134e-04 +
-                      z * (2.75573137070700676789e-06 +
-                      z * (-2.50507602534068634195e-08 +
-                      z * 1.58969099521155010221e-10)));
-    const double sn = r + v * (-1.66666666666666324348e-01 + z * sr);
+    const double sn = fma(v, fma(z, sr, -1.66666666666666324348e-01), r);
     const double mag = (quad & 1) ? sn : c;
     return (quad == 1 || quad == 2) ? -mag : mag;
+}
+__device__ __forceinline__ double cos_fast(double a) {
+    if (__builtin_expect(!(fabs(a) < 1.6e6), 0)) return cos_slow(a);
+    return cos_core(a);
+}
+// Rastrigin term gene*gene - 10*cos(2*pi*gene)                            :239-240
+__device__ __forceinline__ double rast_term(double x) {
+    const double a = (2.0 * PI) * x;
+    double c = cos_core(a);
+    if (__builtin_expect(!(fabs(a) < 1.6e6), 0)) c = cos_slow(a);
+    return x * x - 10.0 * c;
 }
 
 // Per-gene term of a single-objective sum (EC_SUM) for gene x.
@@ -264,6 +274,20 @@ __device__ __forceinline__ void eval_chunk(const dm_eval& ev, int dim, int gbase
                 st.s += acc;
             }
             st.carry = last;
+        } else if (EC == EC_RAST) {
+            if (active) {
+                if (gbase + 3 < dim) {  // full slot: four independent cosines (ILP)
+                    const double t0 = rast_term(y[0]), t1 = rast_term(y[1]);
+                    const double t2 = rast_term(y[2]), t3 = rast_term(y[3]);
+                    st.s += (t0 + t1) + (t2 + t3);
+                } else {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (gbase + j < dim) acc += rast_term(y[j]);
+                    st.s += acc;
+                }
+            }
         } else {
             if (active) {
                 // one (not four) inlined copy of the transcendental: keeps VGPRs low

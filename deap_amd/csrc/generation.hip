@@ -103,6 +103,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     a.w0 = ev->weights[0];
     a.ev = *ev;
     a.rng = Rng(rng);
+    a.zig = ctx->zig;
     a.mode = mode;
     a.dec = d;
     a.nevals = nevals;

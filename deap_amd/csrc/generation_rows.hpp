@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256, DM_ROWS_MINWAVES) void gen_rows_kernel(GenArgs
                 gauss_apply<false>(a, c0, g, bits, x0, x1);
             }
             if (in) {
-                Vec4<T>::store(w0, g, x0);
-                if (has1) Vec4<T>::store(w1, g, x1);
+                Vec4<T>::store_nt(w0, g, x0);
+                if (has1) Vec4<T>::store_nt(w1, g, x1);
             }
             if constexpr (sizeof(T) == 4) {
 #pragma unroll

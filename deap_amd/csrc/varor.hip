@@ -289,6 +289,7 @@ extern "C" int dm_var_or(dm_ctx* ctx, const dm_pop* parents, dm_pop* children,
     a.w0 = ev->weights[0];
     a.ev = *ev;
     a.rng = Rng(rng);
+    a.zig = ctx->zig;
     a.mode = mode;
     a.dec = d;
     a.nevals = nevals;
