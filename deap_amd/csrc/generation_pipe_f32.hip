@@ -1,0 +1,15 @@
+// generation_pipe_f32.hip — float instantiations of the rolling-pipeline hot
+// kernel (generation_pipe.hpp).
+#include "generation_pipe.hpp"
+
+namespace dm {
+
+void launch_gen_pipe_f32(const PipeArgs& a, int ec, int cx, int mut, int nch, dim3 grid,
+                         hipStream_t s) {
+    if (nch <= 2)
+        launch_pipe_ops<float, 2>(a, ec, cx, mut, grid, s);
+    else
+        launch_pipe_ops<float, 4>(a, ec, cx, mut, grid, s);
+}
+
+}  // namespace dm

@@ -1,0 +1,91 @@
+// generation_pipe_f64.hip — double instantiations of the rolling-pipeline hot
+// kernel and the per-pair decision kernel (generation_pipe.hpp).
+#include "generation_pipe.hpp"
+
+namespace dm {
+
+// One thread per pair: the decisions the replay kernels consume, drawn from
+// the same Philox counters — selTournament / selRandom of
+// both children (selection.py:55-70, 36-48), the varAnd crossover flag and
+// cxTwoPoint cuts (algorithms.py:72-76, crossover.py:62-70), the two mutation
+// flags (algorithms.py:78-81) and which children need evaluation
+// (algorithms.py:75-81 `del fitness.values`, algorithms.py:155-158).
+__global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t npairs = (a.nc + 1) / 2;
+    if (p >= npairs) return;
+    const int64_t c0 = 2 * p, c1 = 2 * p + 1;
+    const bool has1 = c1 < a.nc;
+    const int m = a.nobj;
+    const uint32_t np = (uint32_t)a.np;
+    int32_t s[2];
+    for (int h = 0; h < (has1 ? 2 : 1); ++h) {
+        const uint32_t c = (uint32_t)(h ? c1 : c0);
+        if (a.sel == DM_SEL_RANDOM) {
+            const u32x4 w = a.rng(ST_SEL, c, 0);
+            s[h] = (int32_t)bounded64(w.x, w.y, np);
+            continue;
+        }
+        // first-drawn aspirant wins ties: replace only on fit_gt (selection.py:68)
+        int32_t best = 0;
+        u32x4 w{};
+        for (int j = 0; j < a.tournsize; ++j) {
+            if (!(j & 1)) w = a.rng(ST_SEL, c, (uint32_t)(j >> 1));
+            const int32_t k = (int32_t)((j & 1) ? bounded64(w.z, w.w, np) : bounded64(w.x, w.y, np));
+            if (j == 0 || fit_gt(a.pwv + (int64_t)k * m, a.pwv + (int64_t)best * m, m)) best = k;
+        }
+        s[h] = best;
+    }
+    if (!has1) s[1] = s[0];
+    uint32_t fl = has1 ? PF_HAS1 : 0u;
+    uint32_t cuts = 0;
+    if (a.cx != DM_CX_NONE && has1) {
+        const u32x4 w = a.rng(ST_CX, (uint32_t)p, 0);
+        if ((uint64_t)w.x < a.thr_cx) {
+            fl |= PF_CX;
+            if (a.cx == DM_CX_TWOPOINT) {
+                const u32x4 w2 = a.rng(ST_CX, (uint32_t)p, 1);
+                int32_t r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
+                int32_t r2 = 1 + (int32_t)bounded64(w2.x, w2.y, (uint32_t)(a.dim - 1));
+                if (r2 >= r1) {
+                    r2 += 1;
+                } else {
+                    const int32_t t = r1;
+                    r1 = r2;
+                    r2 = t;
+                }
+                cuts = (uint32_t)r1 | ((uint32_t)r2 << 16);
+            }
+        }
+    }
+    if (a.mut != DM_MUT_NONE) {
+        if ((uint64_t)a.rng(ST_MUT, (uint32_t)c0, 0).x < a.thr_mut) fl |= PF_MUT0;
+        if (has1 && (uint64_t)a.rng(ST_MUT, (uint32_t)c1, 0).x < a.thr_mut) fl |= PF_MUT1;
+    }
+    const bool cx = fl & PF_CX;
+    if (cx || (fl & PF_MUT0) || !a.pvalid[s[0]]) fl |= PF_INV0;
+    if (has1 && (cx || (fl & PF_MUT1) || !a.pvalid[s[1]])) fl |= PF_INV1;
+    PairPlan pl;
+    pl.s0 = s[0];
+    pl.s1 = s[1];
+    pl.cuts = cuts;
+    pl.flags = fl;
+    pl.f0 = a.pwv[(int64_t)s[0] * m];
+    pl.f1 = a.pwv[(int64_t)s[1] * m];
+    plans[p] = pl;
+}
+
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, hipStream_t s) {
+    const int64_t npairs = (a.nc + 1) / 2;
+    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans);
+}
+
+void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, dim3 grid,
+                         hipStream_t s) {
+    if (nch <= 2)
+        launch_pipe_ops<double, 2>(a, ec, cx, mut, grid, s);
+    else
+        launch_pipe_ops<double, 4>(a, ec, cx, mut, grid, s);
+}
+
+}  // namespace dm

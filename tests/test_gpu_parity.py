@@ -382,12 +382,22 @@ def test_sel_best_large_ties(gpu):
     ("f64", 300, 400, "twopoint", "gaussian", "sphere", "tournament"),
     ("f32", 200, 300, "blend", "gaussian", "rastrigin", "tournament"),
     ("f64", 513, 64, "blend", "gaussian", "rastrigin", "random"),
+    # more pairs than resident waves: every wave's row ring wraps several times
+    ("f64", 130, 9001, "twopoint", "gaussian", "rastrigin", "tournament"),
+    ("f32", 1000, 6001, "blend", "gaussian", "rastrigin", "tournament"),
+    ("f64", 700, 5000, "blend", "gaussian", "rosenbrock", "random"),
+    ("f64", 1000, 4099, "blend", "gaussian", "rastrigin", "tournament7"),
 ])
-def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
+@pytest.mark.parametrize("hot", ["pipe", "rows"])
+def test_native_hot_kernel_equals_replay_kernel(gpu, monkeypatch, hot, gt, dim, n, cx, mut,
+                                                objective, sel):
     """The whole-row hot kernel (native mode, lane-parallel decisions) draws
     the same decisions as the replay kernel's dump mode and produces the same
-    generation bit for bit (the dump mode is itself replayed in the oracle)."""
+    generation bit for bit (the dump mode is itself replayed in the oracle).
+    Both hot variants run: the rolling pipeline (default) and the one-pair rows
+    kernel (DM_HOT_KERNEL=rows)."""
     from deap_amd import algorithms, benchmarks, tools
+    monkeypatch.setenv("DM_HOT_KERNEL", hot)
     from deap_amd.ops import RandomStream
     outs = []
     for mode in ("native", "dump"):
@@ -395,7 +405,8 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
         pop = tools.initPopulation(n=n, dim=dim, low=-3, high=3, gtype=gt, weights=(-1.0,),
                                    stream=stream)
         getattr(benchmarks, objective)(pop)
-        tb = _toolbox(cx, mut, 0.05, 0.5, evaluate=objective)
+        tb = _toolbox(cx, mut, 0.05, 0.5, evaluate=objective,
+                      tournsize=7 if sel == "tournament7" else 3)
         if sel == "random":
             tb.register("select", tools.selRandom)
         decs = [] if mode == "dump" else None
