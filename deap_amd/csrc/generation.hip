@@ -1,7 +1,6 @@
 // generation.hip — host side of the fused generation (see generation.hpp for
 // the kernels; per-genome-type instantiations live in generation_{f64,f32,bits}.hip
 // so they compile in parallel).
-#include "generation_rows.hpp"
 #include "generation_pipe.hpp"
 
 namespace dm {
@@ -112,59 +111,43 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     const int ec = eval_class(ev->fn);
     const int64_t npairs = (children->n + 1) / 2;
     // hot path: native RNG, float rows of 65..1024 genes, fused tournament / random
-    // selection -> whole-row kernel with lane-parallel decisions
+    // selection -> per-pair decision kernel + rolling-pipeline kernel on a
+    // persistent grid (generation_pipe.hpp)
     if (mode == DM_RNG_NATIVE && parents->gtype != DM_BITS && parents->dim > 64 &&
         parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
-        tournsize <= 30 && ec != EC_MO && !std::getenv("DM_DISABLE_ROWS")) {
+        ec != EC_MO && !std::getenv("DM_DISABLE_PIPE")) {
         const int nch = parents->dim <= 512 ? 2 : 4;
-        const char* hk = std::getenv("DM_HOT_KERNEL");
-        if (!(hk && hk[0] == 'r')) {
-            // decisions kernel + rolling-pipeline kernel on a persistent grid
-            PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
-            if (!plans) return DM_ERR_NOMEM;
-            launch_pair_plans(a, plans, ctx->stream);
-            DM_LAUNCH_CHECK();
-            PipeArgs q{};
-            q.pgenes = a.pgenes;
-            q.cgenes = a.cgenes;
-            q.cwv = a.cwv;
-            q.cvalid = a.cvalid;
-            q.plans = plans;
-            q.pwv = a.pwv;
-            q.mu_vec = a.mu_vec;
-            q.sigma_vec = a.sigma_vec;
-            q.zig = a.zig;
-            q.nevals = a.nevals;
-            q.nc = a.nc;
-            q.pstride = a.pstride;
-            q.cstride = a.cstride;
-            q.dim = a.dim;
-            q.nobj = a.nobj;
-            q.rng = a.rng;
-            q.thr_ind = a.thr_ind;
-            q.alpha = a.alpha;
-            q.mu = a.mu;
-            q.sigma = a.sigma;
-            q.w0 = a.w0;
-            q.ev = a.ev;
-            const char* bpc = std::getenv("DM_PIPE_BPC");
-            int64_t blocks = (npairs + 3) / 4;
-            blocks = std::min<int64_t>(blocks, (int64_t)ctx->num_cus * (bpc ? atoi(bpc) : 2));
-            const dim3 grid((unsigned)std::max<int64_t>(blocks, 1));
-            if (parents->gtype == DM_F64)
-                launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, grid, ctx->stream);
-            else
-                launch_gen_pipe_f32(q, ec, a.cx, a.mut, nch, grid, ctx->stream);
-            DM_LAUNCH_CHECK();
-            return DM_OK;
-        }
-        int64_t blocks = (npairs + 3) / 4;
-        blocks = std::min<int64_t>(blocks, (int64_t)ctx->num_cus * 8);
-        const dim3 grid((unsigned)std::max<int64_t>(blocks, 1));
+        PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
+        if (!plans) return DM_ERR_NOMEM;
+        launch_pair_plans(a, plans, ctx->stream);
+        DM_LAUNCH_CHECK();
+        PipeArgs q{};
+        q.pgenes = a.pgenes;
+        q.cgenes = a.cgenes;
+        q.cwv = a.cwv;
+        q.cvalid = a.cvalid;
+        q.plans = plans;
+        q.pwv = a.pwv;
+        q.mu_vec = a.mu_vec;
+        q.sigma_vec = a.sigma_vec;
+        q.zig = a.zig;
+        q.nevals = a.nevals;
+        q.nc = a.nc;
+        q.pstride = a.pstride;
+        q.cstride = a.cstride;
+        q.dim = a.dim;
+        q.nobj = a.nobj;
+        q.rng = a.rng;
+        q.thr_ind = a.thr_ind;
+        q.alpha = a.alpha;
+        q.mu = a.mu;
+        q.sigma = a.sigma;
+        q.w0 = a.w0;
+        q.ev = a.ev;
         if (parents->gtype == DM_F64)
-            launch_gen_rows_f64(a, ec, nch, grid, ctx->stream);
+            launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
         else
-            launch_gen_rows_f32(a, ec, nch, grid, ctx->stream);
+            launch_gen_pipe_f32(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }

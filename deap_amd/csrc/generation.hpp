@@ -203,6 +203,24 @@ struct Vec4<float> {
     }
 };
 
+// Per-gene Philox slots (streams ST_BLEND, ST_MASK): the four words of call
+// (stage, item, sub = 64c + L) feed the four genes lane L holds in chunk c of
+// the hot kernel's lane layout (generation_pipe.hpp ChunkLayout): fp64 genes
+// {256c + 2L, +1, 256c + 128 + 2L, +1}, fp32 genes 256c + 4L .. +3.  Here the
+// words of four consecutive genes g .. g+3 (g % 4 == 0) are gathered from
+// that layout: one call for fp32 rows, two for fp64 rows.
+template <typename T>
+__device__ __forceinline__ u32x4 gene4_words(const Rng& rng, uint32_t stage, uint32_t item, int g) {
+    if constexpr (sizeof(T) == 4) {
+        return rng(stage, item, (uint32_t)(g >> 2));
+    } else {
+        const int r = g & 255;
+        const uint32_t sub = (uint32_t)(((g >> 8) << 6) + ((r & 127) >> 1));
+        const u32x4 a = rng(stage, item, sub), b = rng(stage, item, sub + 1);
+        return (r & 128) ? u32x4{a.z, a.w, b.z, b.w} : u32x4{a.x, a.y, b.x, b.y};
+    }
+}
+
 // Per-gene Gaussian mutation of one child's chunk (mutation.py:44-46).
 // Returns the 4-bit mask of mutated genes; the normal draws happen in
 // gauss_apply so only one inlined copy of log/cos/sqrt exists.
@@ -214,14 +232,14 @@ __device__ __noinline__ double std_normal(const double* zig, Rng rng, int64_t c,
     return zig_normal(zig, rng, ST_GAUSS, (uint32_t)c, (uint32_t)gi);
 }
 
-template <bool RP>
+template <typename T, bool RP>
 __device__ __forceinline__ uint32_t gauss_mask(const GenArgs& a, int64_t c, int g) {
     uint32_t bits = 0;
     if ((RP && a.mode == DM_RNG_INJECT)) {
         const uint64_t word = a.dec.mut_mask[c * a.words64 + (g >> 6)];
         bits = (uint32_t)(word >> (g & 63)) & 0xFu;
     } else {
-        const u32x4 w = a.rng(ST_MASK, (uint32_t)c, (uint32_t)(g >> 2));
+        const u32x4 w = gene4_words<T>(a.rng, ST_MASK, (uint32_t)c, g);
         bits = ((uint64_t)w.x < a.thr_ind ? 1u : 0u) | ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
                ((uint64_t)w.z < a.thr_ind ? 4u : 0u) | ((uint64_t)w.w < a.thr_ind ? 8u : 0u);
         if ((RP && a.mode == DM_RNG_DUMP) && bits) {
@@ -335,7 +353,7 @@ __global__ __launch_bounds__(256, DM_GEN_MINWAVES) void gen_float_kernel(GenArgs
                     for (int j = 0; j < 4; ++j)
                         u[j] = (g + j < a.dim) ? a.dec.blend_u[p * a.dim + g + j] : 0.0;
                 } else {
-                    const u32x4 w = a.rng(ST_BLEND, (uint32_t)p, (uint32_t)(g >> 2));
+                    const u32x4 w = gene4_words<T>(a.rng, ST_BLEND, (uint32_t)p, g);
                     u[0] = u01_32(w.x);
                     u[1] = u01_32(w.y);
                     u[2] = u01_32(w.z);
@@ -376,8 +394,8 @@ __global__ __launch_bounds__(256, DM_GEN_MINWAVES) void gen_float_kernel(GenArgs
             }
             if (MUT == DM_MUT_GAUSSIAN && in) {
                 uint32_t bits = 0;
-                if (d.mut0) bits |= gauss_mask<RP>(a, c0, g);
-                if (d.mut1) bits |= gauss_mask<RP>(a, c1, g) << 4;
+                if (d.mut0) bits |= gauss_mask<T, RP>(a, c0, g);
+                if (d.mut1) bits |= gauss_mask<T, RP>(a, c1, g) << 4;
                 gauss_apply<RP>(a, c0, g, bits, y0, y1);
             }
             if (in) {

@@ -9,15 +9,27 @@
 //     weighted fitness (what a clone inherits).  16 MB of plans per 2^20
 //     children: 0.1% of the generation's traffic.
 //  2. gen_pipe_kernel — one wave per pair, persistent grid, rolling pipeline:
-//     the wave holds all NCH x 4 genes per lane of both parent rows in
-//     registers; as soon as chunk c of pair p has been varied, stored and
-//     evaluated, chunk c of the parents of pair p + W is loaded into the same
-//     registers, so 2 x NCH x 2 KB per wave stay in flight while it computes.
+//     a row is streamed in chunks of 256 genes; the wave keeps D chunks of
+//     both parent rows in flight in registers, and as soon as chunk c of pair
+//     p has been varied, stored and evaluated, chunk c + D (or a chunk of the
+//     parents of pair p + W) is loaded into the freed registers.
 //     Nothing inside the compute phase may issue a vector load or a call
 //     (vmcnt is in-order on CDNA, a callee starts with a full wait): plans
-//     come through SCALAR loads (lgkmcnt) two pairs ahead, the ziggurat tables
-//     live in LDS, and the rare ziggurat rejection (~0.6% of draws) is inlined.
-// Results are bit-identical to the replay kernel:
+//     come through SCALAR loads (lgkmcnt) two pairs ahead, the ziggurat and
+//     cosine tables live in LDS, and the rare ziggurat rejection (~0.6% of
+//     draws) is inlined.
+//
+// Lane layout of a chunk (ChunkLayout<T>): every load / store instruction of
+// the wave covers ONE contiguous KiB (16 B per lane).  fp64: two pieces per
+// row, lane L holds genes {256c + 2L, +1} and {256c + 128 + 2L, +1}; fp32:
+// one piece, lane L holds genes 256c + 4L .. +3.  (The earlier 32-B-per-lane
+// layout made every instruction span 2 KiB with holes and capped the row
+// copy at 4.4 TB/s against 5.6 TB/s for whole-KiB instructions — measured
+// with tools_gpu/bwtest2.hip.)  The per-gene Philox slots follow the same
+// layout (gene4_words in generation.hpp), so one Philox call feeds a lane's four
+// genes in every kernel.
+//
+// Genomes are bit-identical to the replay kernel's:
 // tests/test_gpu_parity.py::test_native_hot_kernel_equals_replay_kernel.
 #pragma once
 #include "generation.hpp"
@@ -25,6 +37,10 @@
 namespace dm {
 
 typedef __attribute__((address_space(4))) const uint32_t c4_u32;
+
+#ifndef DM_RAST_ILP
+#define DM_RAST_ILP 2  // Rastrigin terms evaluated side by side (VGPR pressure)
+#endif
 
 struct PairPlan {
     int32_t s0, s1;    // parent rows
@@ -51,14 +67,27 @@ __device__ __forceinline__ PairPlan load_plan(const PairPlan* plans, int64_t p) 
     return r;
 }
 
+// The ziggurat's wedge / tail sampler (~0.6% of draws).  Out of line by
+// default: inlined, its exp / log1p temporaries pushed the hot kernel past
+// 128 VGPRs; the call's vmcnt(0) drain is paid only on those rare draws.
+#ifndef DM_ZIG_SLOW_NOINLINE
+#define DM_ZIG_SLOW_NOINLINE 1
+#endif
+#if DM_ZIG_SLOW_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+double zig_normal_slow(const double* zig, Rng rng, uint32_t c, uint32_t gi) {
+    return zig_normal(zig, rng, ST_GAUSS, c, gi);
+}
+
 // Ziggurat draw with the tables in LDS: the rectangle test accepts ~99.4% of
 // draws; otherwise the full sampler (common.hpp zig_normal) recomputes the
 // same draw from attempt 0 — identical value either way.
-// Inlined on purpose: a call would start with a full s_waitcnt and drain the
-// row prefetches (measured 4.20 vs 3.84 ms per C3 generation).
-__device__ __forceinline__ double zig_normal_slow(const double* zig, Rng rng, uint32_t c, uint32_t gi) {
-    return zig_normal(zig, rng, ST_GAUSS, c, gi);
-}
+// The fast path is inlined: a call would start with a full s_waitcnt and
+// drain the row prefetches on every draw (measured 4.20 vs 3.84 ms per C3
+// generation).
 __device__ __forceinline__ double zig_normal_lds(const double* szig, const double* gzig,
                                                  const Rng& rng, uint32_t c, uint32_t gi) {
     const u32x4 w = rng(ST_GAUSS, c, gi);
@@ -68,6 +97,150 @@ __device__ __forceinline__ double zig_normal_lds(const double* szig, const doubl
     const double x = u * szig[layer];
     if (x < szig[layer + 1]) return neg ? -x : x;
     return zig_normal_slow(gzig, rng, c, gi);
+}
+
+// cos(2*pi*x) for the Rastrigin term `gene*gene - 10*cos(2*pi*gene)`
+// (deap/benchmarks/__init__.py:239-240).  Reduction in turns: k = rint(64x),
+// f = x - k/64 (exact, |f| <= 1/128), and
+//   cos(2pi(k/64 + f)) = C_k cos(2pi f) - S_k sin(2pi f)
+// with (C_k, S_k) = (cos, sin)(2pi k/64) from a 1-KiB LDS table and Taylor
+// polynomials in f (truncation < 1e-15).  Against glibc's cos of the rounded
+// product 2*pi*gene the difference is the reference's own rounding of that
+// product (<= 4e-15 absolute per term), far inside the 1e-12 relative
+// fitness tolerance.  ~17 fp64 operations vs ~28 for a pi/2 reduction that
+// evaluates both the sine and cosine kernels.
+__device__ __forceinline__ double cos2pi_lds(const double2* tab, double x) {
+    const double k = rint(x * 64.0);
+    const double f = fma(-k, 0.015625, x);
+    const double2 cs = tab[(int)k & 63];
+    const double z = f * f;
+    const double c = fma(z, fma(z, fma(z, -85.45681720669373, 64.9393940226683),
+                                -19.739208802178716), 1.0);
+    const double s = f * fma(z, fma(z, fma(z, -76.70585975306139, 81.60524927607506),
+                                    -41.34170224039976), 6.283185307179586);
+    return fma(cs.x, c, -(cs.y * s));
+}
+
+// Lane layout of one 256-gene chunk (see the header comment).
+template <typename T>
+struct ChunkLayout;
+template <>
+struct ChunkLayout<double> {
+    __device__ __forceinline__ static int gene(int c, int lane, int k) {
+        return (c << 8) + ((k >> 1) << 7) + 2 * lane + (k & 1);
+    }
+    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
+                                                double (&x)[4]) {
+        const int g0 = gene(c, lane, 0), g2 = gene(c, lane, 2);
+        if (g0 < dim) {
+            const double2 v = *reinterpret_cast<const double2*>(row + (size_t)g0 * 8);
+            x[0] = v.x;
+            x[1] = v.y;
+        }
+        if (g2 < dim) {
+            const double2 v = *reinterpret_cast<const double2*>(row + (size_t)g2 * 8);
+            x[2] = v.x;
+            x[3] = v.y;
+        }
+    }
+    // streaming store: the child row is not re-read in this launch
+    __device__ __forceinline__ static void store_nt(char* row, int c, int lane, int dim,
+                                                    const double (&x)[4]) {
+        const int g0 = gene(c, lane, 0), g2 = gene(c, lane, 2);
+        if (g0 < dim)
+            __builtin_nontemporal_store(dm_d2{x[0], x[1]}, reinterpret_cast<dm_d2*>(row + (size_t)g0 * 8));
+        if (g2 < dim)
+            __builtin_nontemporal_store(dm_d2{x[2], x[3]}, reinterpret_cast<dm_d2*>(row + (size_t)g2 * 8));
+    }
+};
+template <>
+struct ChunkLayout<float> {
+    __device__ __forceinline__ static int gene(int c, int lane, int k) {
+        return (c << 8) + 4 * lane + k;
+    }
+    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
+                                                double (&x)[4]) {
+        const int g = gene(c, lane, 0);
+        if (g < dim) Vec4<float>::load(row, g, x);
+    }
+    __device__ __forceinline__ static void store_nt(char* row, int c, int lane, int dim,
+                                                    const double (&x)[4]) {
+        const int g = gene(c, lane, 0);
+        if (g < dim) Vec4<float>::store_nt(row, g, x);
+    }
+};
+
+// Single-objective evaluation of one chunk in ChunkLayout<T> (Rastrigin,
+// Rosenbrock, or a per-gene sum).  Called by every lane of the wave (the
+// Rosenbrock neighbours come through shuffles); `carry` is the previous
+// chunk's last gene.
+template <typename T, int EC>
+__device__ __forceinline__ void pipe_eval_chunk(const dm_eval& ev, int dim, int c, int lane,
+                                                const double (&x)[4], const double2* cstab,
+                                                bool active, double& acc, double& carry) {
+    typedef ChunkLayout<T> L;
+    if constexpr (EC == EC_ROSEN) {
+        // 100*(x*x - y)**2 + (1. - x)**2 over consecutive genes     (:117-118)
+        const int up = (lane + 1) & 63;
+        const double s0 = __shfl(x[0], up, 64);
+        const double s2 = __shfl(x[2], up, 64);
+        const double last = __shfl(x[3], 63, 64);
+        if (active) {
+            double t = 0.0;
+            if (lane == 0 && c > 0 && (c << 8) < dim) t += rosen_term(carry, x[0]);
+            if constexpr (sizeof(T) == 8) {
+                const int a0 = L::gene(c, lane, 0), b0 = L::gene(c, lane, 2);
+                if (a0 + 1 < dim) t += rosen_term(x[0], x[1]);
+                if (a0 + 2 < dim) t += rosen_term(x[1], lane < 63 ? s0 : s2);
+                if (b0 + 1 < dim) t += rosen_term(x[2], x[3]);
+                if (lane < 63 && b0 + 2 < dim) t += rosen_term(x[3], s2);
+            } else {
+                const int g = L::gene(c, lane, 0);
+                if (g + 1 < dim) t += rosen_term(x[0], x[1]);
+                if (g + 2 < dim) t += rosen_term(x[1], x[2]);
+                if (g + 3 < dim) t += rosen_term(x[2], x[3]);
+                if (lane < 63 && g + 4 < dim) t += rosen_term(x[3], s0);
+            }
+            acc += t;
+        }
+        carry = last;
+    } else if constexpr (EC == EC_RAST) {
+        if (active) {
+            if (L::gene(c, lane, 3) < dim) {  // all four genes in the row
+#if DM_RAST_ILP == 4
+                const double t0 = x[0] * x[0] - 10.0 * cos2pi_lds(cstab, x[0]);
+                const double t1 = x[1] * x[1] - 10.0 * cos2pi_lds(cstab, x[1]);
+                const double t2 = x[2] * x[2] - 10.0 * cos2pi_lds(cstab, x[2]);
+                const double t3 = x[3] * x[3] - 10.0 * cos2pi_lds(cstab, x[3]);
+                acc += (t0 + t1) + (t2 + t3);
+#else
+#pragma unroll 1
+                for (int h = 0; h < 2; ++h) {  // two independent terms at a time
+                    const double a0 = h ? x[2] : x[0], a1 = h ? x[3] : x[1];
+                    const double t0 = a0 * a0 - 10.0 * cos2pi_lds(cstab, a0);
+                    const double t1 = a1 * a1 - 10.0 * cos2pi_lds(cstab, a1);
+                    acc += t0 + t1;
+                }
+#endif
+            } else {
+                double t = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (L::gene(c, lane, k) < dim) t += x[k] * x[k] - 10.0 * cos2pi_lds(cstab, x[k]);
+                acc += t;
+            }
+        }
+    } else if constexpr (EC == EC_SUM) {
+        if (active) {
+            double t = 0.0;
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const double v = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : x[3];
+                if (L::gene(c, lane, k) < dim) t += sum_term(ev.fn, v);
+            }
+            acc += t;
+        }
+    }
 }
 
 struct PipeArgs {
@@ -99,19 +272,26 @@ struct PipeArgs {
 
 template <typename T, int NCH, int CX, int MUT, int EC>
 __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArgs a) {
+    typedef ChunkLayout<T> L;
     constexpr int D = NCH < DM_PIPE_DEPTH ? NCH : DM_PIPE_DEPTH;
     static_assert(NCH % D == 0, "ring depth must divide the chunk count");
     __shared__ double szig[ZIG_N + 1];
-    if (MUT == DM_MUT_GAUSSIAN) {
+    __shared__ double2 cstab[64];
+    if (MUT == DM_MUT_GAUSSIAN)
         for (int i = threadIdx.x; i <= ZIG_N; i += blockDim.x) szig[i] = a.zig[i];
-        __syncthreads();
+    if (EC == EC_RAST && threadIdx.x < 64) {
+        double sn, cn;
+        sincospi((double)threadIdx.x / 32.0, &sn, &cn);  // (sin, cos)(2 pi k / 64)
+        cstab[threadIdx.x] = make_double2(cn, sn);
     }
+    if (MUT == DM_MUT_GAUSSIAN || EC == EC_RAST) __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (p >= npairs) return;
     int64_t evals = 0;
+    const int dim = a.dim;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
     PairPlan pl = load_plan(a.plans, p);
@@ -120,11 +300,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     double y0[D][4], y1[D][4];
 #pragma unroll
     for (int ch = 0; ch < D; ++ch) {
-        const int g = ch * 256 + 4 * lane;
-        if (g < a.dim) {
-            Vec4<T>::load(a.pgenes + (int64_t)pl.s0 * a.pstride, g, y0[ch]);
-            Vec4<T>::load(a.pgenes + (int64_t)pl.s1 * a.pstride, g, y1[ch]);
-        }
+        L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch]);
+        L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch]);
     }
     for (; p < npairs; p += nw) {
         const bool more = p + nw < npairs;
@@ -141,52 +318,44 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
         const char* r1 = a.pgenes + (int64_t)pl.s1 * a.pstride;
         const char* n0 = a.pgenes + (int64_t)nx.s0 * a.pstride;
         const char* n1 = a.pgenes + (int64_t)nx.s1 * a.pstride;
-        EvalState e0, e1;
-        eval_init(e0);
-        eval_init(e1);
+        double acc0 = 0.0, acc1 = 0.0, carry0 = 0.0, carry1 = 0.0;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
-            const int cbase = ch * 256;
-            const int g = cbase + 4 * lane;
-            const bool in = g < a.dim;
             double x0[4], x1[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                x0[k] = in ? y0[ch % D][k] : 0.0;
-                x1[k] = in ? y1[ch % D][k] : 0.0;
+                x0[k] = y0[ch % D][k];
+                x1[k] = y1[ch % D][k];
             }
             // ring: the chunk D ahead into the freed slot (this pair's rows or
             // the next pair's)
             {
                 const int ca = ch + D;
-                const int ga = (ca < NCH ? ca : ca - NCH) * 256 + 4 * lane;
                 if (ca < NCH) {
-                    if (ga < a.dim) {
-                        Vec4<T>::load(r0, ga, y0[ch % D]);
-                        Vec4<T>::load(r1, ga, y1[ch % D]);
-                    }
-                } else if (more && ga < a.dim) {
-                    Vec4<T>::load(n0, ga, y0[ch % D]);
-                    Vec4<T>::load(n1, ga, y1[ch % D]);
+                    L::load(r0, ca, lane, dim, y0[ch % D]);
+                    L::load(r1, ca, lane, dim, y1[ch % D]);
+                } else if (more) {
+                    L::load(n0, ca - NCH, lane, dim, y0[ch % D]);
+                    L::load(n1, ca - NCH, lane, dim, y1[ch % D]);
                 }
             }
-            if (CX == DM_CX_BLEND && cx && in) {
-                const u32x4 u = a.rng(ST_BLEND, (uint32_t)p, (uint32_t)(g >> 2));
+            const uint32_t slot = (uint32_t)((ch << 6) + lane);  // gene_slot of this lane's genes
+            if (CX == DM_CX_BLEND && cx) {
+                const u32x4 u = a.rng(ST_BLEND, (uint32_t)p, slot);
                 const uint32_t us[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (g + k < a.dim) {
-                        // gamma = (1.+2.*alpha)*random()-alpha; blend   (crossover.py:255-258)
-                        const double gm = gamma_scale * u01_32(us[k]) - a.alpha;
-                        const double v1 = x0[k], v2 = x1[k];
-                        x0[k] = (1.0 - gm) * v1 + gm * v2;
-                        x1[k] = gm * v1 + (1.0 - gm) * v2;
-                    }
+                    // gamma = (1.+2.*alpha)*random()-alpha; blend   (crossover.py:255-258)
+                    const double gm = gamma_scale * u01_32(us[k]) - a.alpha;
+                    const double v1 = x0[k], v2 = x1[k];
+                    x0[k] = (1.0 - gm) * v1 + gm * v2;
+                    x1[k] = gm * v1 + (1.0 - gm) * v2;
                 }
-            } else if (CX == DM_CX_TWOPOINT && cx && in) {
+            } else if (CX == DM_CX_TWOPOINT && cx) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (g + k >= cp1 && g + k < cp2) {  // crossover.py:71-72 slice swap
+                    const int gk = L::gene(ch, lane, k);
+                    if (gk >= cp1 && gk < cp2) {  // crossover.py:71-72 slice swap
                         const double tt = x0[k];
                         x0[k] = x1[k];
                         x1[k] = tt;
@@ -200,30 +369,30 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                     x1[k] = (double)(float)x1[k];
                 }
             }
-            if (MUT == DM_MUT_GAUSSIAN && in && (mut0 || mut1)) {
+            if (MUT == DM_MUT_GAUSSIAN && (mut0 || mut1)) {
                 // per-gene Bernoulli(indpb) + gauss(mu, sigma)   (mutation.py:44-46)
+                uint32_t keep = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) keep |= (L::gene(ch, lane, k) < dim ? 1u : 0u) << k;
                 uint32_t bits = 0;
-                const int lim = a.dim - g < 4 ? a.dim - g : 4;
-                const uint32_t keep = (1u << lim) - 1u;
                 if (mut0) {
-                    const u32x4 w = a.rng(ST_MASK, (uint32_t)c0, (uint32_t)(g >> 2));
-                    bits |= (((uint64_t)w.x < a.thr_ind ? 1u : 0u) |
-                             ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
-                             ((uint64_t)w.z < a.thr_ind ? 4u : 0u) |
-                             ((uint64_t)w.w < a.thr_ind ? 8u : 0u)) & keep;
+                    const u32x4 w = a.rng(ST_MASK, (uint32_t)c0, slot);
+                    bits |= ((uint64_t)w.x < a.thr_ind ? 1u : 0u) | ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
+                            ((uint64_t)w.z < a.thr_ind ? 4u : 0u) | ((uint64_t)w.w < a.thr_ind ? 8u : 0u);
                 }
                 if (mut1) {
-                    const u32x4 w = a.rng(ST_MASK, (uint32_t)c1, (uint32_t)(g >> 2));
-                    bits |= ((((uint64_t)w.x < a.thr_ind ? 1u : 0u) |
-                              ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
-                              ((uint64_t)w.z < a.thr_ind ? 4u : 0u) |
-                              ((uint64_t)w.w < a.thr_ind ? 8u : 0u)) & keep) << 4;
+                    const u32x4 w = a.rng(ST_MASK, (uint32_t)c1, slot);
+                    bits |= (((uint64_t)w.x < a.thr_ind ? 1u : 0u) | ((uint64_t)w.y < a.thr_ind ? 2u : 0u) |
+                             ((uint64_t)w.z < a.thr_ind ? 4u : 0u) | ((uint64_t)w.w < a.thr_ind ? 8u : 0u))
+                            << 4;
                 }
+                bits &= keep | (keep << 4);
 #pragma unroll 1
                 while (bits) {
                     const int b = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    const int j = b & 3, gi = g + j;
+                    const int j = b & 3;
+                    const int gi = L::gene(ch, lane, j);
                     const double nrm =
                         zig_normal_lds(szig, a.zig, a.rng, (uint32_t)(c0 + (b >> 2)), (uint32_t)gi);
                     const double m = a.mu_vec ? a.mu_vec[gi] : a.mu;
@@ -242,10 +411,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                     }
                 }
             }
-            if (in) {
-                Vec4<T>::store_nt(w0, g, x0);
-                if (has1) Vec4<T>::store_nt(w1, g, x1);
-            }
+            L::store_nt(w0, ch, lane, dim, x0);
+            if (has1) L::store_nt(w1, ch, lane, dim, x1);
             if constexpr (sizeof(T) == 4) {
                 // evaluate the stored (fp32-rounded) genes, as DEAP reads array('f')
 #pragma unroll
@@ -255,21 +422,24 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                 }
             }
             if (EC != EC_NONE) {
-                eval_chunk<64, EC>(a.ev, a.dim, g, cbase, x0, inv0, e0);
-                eval_chunk<64, EC>(a.ev, a.dim, g, cbase, x1, inv1, e1);
+                pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x0, cstab, inv0, acc0, carry0);
+                pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x1, cstab, inv1, acc1, carry1);
             }
         }
-        double f0[DM_MAX_OBJ], f1[DM_MAX_OBJ];
+        if (lane == 0) evals += (int64_t)inv0 + (int64_t)inv1;
         if (EC != EC_NONE) {
-            eval_finish<64, EC>(a.ev, a.dim, e0, f0);
-            eval_finish<64, EC>(a.ev, a.dim, e1, f1);
-        }
-        if (lane == 0) {
-            const bool de = EC != EC_NONE;
-            if constexpr (ec_single(EC)) {
-                a.cwv[c0] = inv0 ? f0[0] * a.w0 : pl.f0;
-                if (has1) a.cwv[c1] = inv1 ? f1[0] * a.w0 : pl.f1;
-            } else if (a.nobj == 1) {  // no evaluation requested
+            const double S0 = group_sum<64>(acc0), S1 = group_sum<64>(acc1);
+            if (lane == 0) {
+                const double base = EC == EC_RAST || (EC == EC_SUM && a.ev.fn == DM_EVAL_RASTRIGIN)
+                                        ? (double)(10 * (int64_t)dim)  // 10*len(individual) + sum
+                                        : 0.0;
+                a.cwv[c0] = inv0 ? (base + S0) * a.w0 : pl.f0;
+                if (has1) a.cwv[c1] = inv1 ? (base + S1) * a.w0 : pl.f1;
+                a.cvalid[c0] = 1;
+                if (has1) a.cvalid[c1] = 1;
+            }
+        } else if (lane == 0) {  // no evaluation requested: clones keep their fitness
+            if (a.nobj == 1) {
                 a.cwv[c0] = pl.f0;
                 if (has1) a.cwv[c1] = pl.f1;
             } else {
@@ -279,9 +449,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                     if (has1) a.cwv[c1 * m + o] = a.pwv[(int64_t)pl.s1 * m + o];
                 }
             }
-            a.cvalid[c0] = de ? 1 : (inv0 ? 0 : 1);
-            if (has1) a.cvalid[c1] = de ? 1 : (inv1 ? 0 : 1);
-            evals += (int64_t)inv0 + (int64_t)inv1;
+            a.cvalid[c0] = inv0 ? 0 : 1;
+            if (has1) a.cvalid[c1] = inv1 ? 0 : 1;
         }
         pl = nx;
         nx = nn;
@@ -294,40 +463,60 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     }
 }
 
+// Persistent grid: as many 256-thread workgroups as stay resident on every CU
+// (occupancy API, capped at 6: the admission limit for ~106 SGPRs on gfx950,
+// MI355X_MICROARCH.md §Residency), never more than one wave per pair.
+// DM_PIPE_BPC overrides the per-CU count (A/B experiments).
+template <typename K>
+dim3 pipe_grid(K kern, int num_cus, int64_t npairs) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1)
+        occ = 1;
+    occ = std::min(occ, 6);
+    if (const char* bpc = std::getenv("DM_PIPE_BPC")) occ = std::max(1, atoi(bpc));
+    const int64_t blocks = std::min<int64_t>((npairs + 3) / 4, (int64_t)num_cus * occ);
+    return dim3((unsigned)std::max<int64_t>(blocks, 1));
+}
+template <typename T, int NCH, int CX, int MUT, int EC>
+void launch_pipe_k(const PipeArgs& a, int num_cus, hipStream_t s) {
+    auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC>;
+    kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a);
+}
 template <typename T, int NCH, int CX, int MUT>
-void launch_pipe_e(const PipeArgs& a, int ec, dim3 grid, hipStream_t s) {
+void launch_pipe_e(const PipeArgs& a, int ec, int num_cus, hipStream_t s) {
     if (ec == EC_RAST)
-        gen_pipe_kernel<T, NCH, CX, MUT, EC_RAST><<<grid, 256, 0, s>>>(a);
+        launch_pipe_k<T, NCH, CX, MUT, EC_RAST>(a, num_cus, s);
     else if (ec == EC_ROSEN)
-        gen_pipe_kernel<T, NCH, CX, MUT, EC_ROSEN><<<grid, 256, 0, s>>>(a);
+        launch_pipe_k<T, NCH, CX, MUT, EC_ROSEN>(a, num_cus, s);
     else if (ec_single(ec))
-        gen_pipe_kernel<T, NCH, CX, MUT, EC_SUM><<<grid, 256, 0, s>>>(a);
+        launch_pipe_k<T, NCH, CX, MUT, EC_SUM>(a, num_cus, s);
     else
-        gen_pipe_kernel<T, NCH, CX, MUT, EC_NONE><<<grid, 256, 0, s>>>(a);
+        launch_pipe_k<T, NCH, CX, MUT, EC_NONE>(a, num_cus, s);
 }
 template <typename T, int NCH>
-void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, dim3 grid, hipStream_t s) {
+void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hipStream_t s) {
     const bool mg = mut == DM_MUT_GAUSSIAN;
     switch (cx) {
         case DM_CX_BLEND:
-            mg ? launch_pipe_e<T, NCH, DM_CX_BLEND, DM_MUT_GAUSSIAN>(a, ec, grid, s)
-               : launch_pipe_e<T, NCH, DM_CX_BLEND, DM_MUT_NONE>(a, ec, grid, s);
+            mg ? launch_pipe_e<T, NCH, DM_CX_BLEND, DM_MUT_GAUSSIAN>(a, ec, num_cus, s)
+               : launch_pipe_e<T, NCH, DM_CX_BLEND, DM_MUT_NONE>(a, ec, num_cus, s);
             break;
         case DM_CX_TWOPOINT:
-            mg ? launch_pipe_e<T, NCH, DM_CX_TWOPOINT, DM_MUT_GAUSSIAN>(a, ec, grid, s)
-               : launch_pipe_e<T, NCH, DM_CX_TWOPOINT, DM_MUT_NONE>(a, ec, grid, s);
+            mg ? launch_pipe_e<T, NCH, DM_CX_TWOPOINT, DM_MUT_GAUSSIAN>(a, ec, num_cus, s)
+               : launch_pipe_e<T, NCH, DM_CX_TWOPOINT, DM_MUT_NONE>(a, ec, num_cus, s);
             break;
         default:
-            mg ? launch_pipe_e<T, NCH, DM_CX_NONE, DM_MUT_GAUSSIAN>(a, ec, grid, s)
-               : launch_pipe_e<T, NCH, DM_CX_NONE, DM_MUT_NONE>(a, ec, grid, s);
+            mg ? launch_pipe_e<T, NCH, DM_CX_NONE, DM_MUT_GAUSSIAN>(a, ec, num_cus, s)
+               : launch_pipe_e<T, NCH, DM_CX_NONE, DM_MUT_NONE>(a, ec, num_cus, s);
     }
 }
 
 // Decisions of every pair (thread per pair), generation_pipe_f64.hip.
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, hipStream_t s);
-void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, dim3 grid,
+// num_cus: CUs of the device (the persistent grid is sized from it).
+void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s);
-void launch_gen_pipe_f32(const PipeArgs& a, int ec, int cx, int mut, int nch, dim3 grid,
+void launch_gen_pipe_f32(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s);
 
 }  // namespace dm

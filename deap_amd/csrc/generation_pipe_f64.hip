@@ -80,12 +80,12 @@ void launch_pair_plans(const GenArgs& a, PairPlan* plans, hipStream_t s) {
     pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans);
 }
 
-void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, dim3 grid,
+void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s) {
     if (nch <= 2)
-        launch_pipe_ops<double, 2>(a, ec, cx, mut, grid, s);
+        launch_pipe_ops<double, 2>(a, ec, cx, mut, num_cus, s);
     else
-        launch_pipe_ops<double, 4>(a, ec, cx, mut, grid, s);
+        launch_pipe_ops<double, 4>(a, ec, cx, mut, num_cus, s);
 }
 
 }  // namespace dm

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void varor_float_kernel(GenArgs a, double cxpb
                         for (int j = 0; j < 4; ++j)
                             u[j] = (g + j < a.dim) ? a.dec.blend_u[c * a.dim + g + j] : 0.0;
                     } else {
-                        const u32x4 w = a.rng(ST_BLEND, (uint32_t)c, (uint32_t)(g >> 2));
+                        const u32x4 w = gene4_words<T>(a.rng, ST_BLEND, (uint32_t)c, g);
                         u[0] = u01_32(w.x);
                         u[1] = u01_32(w.y);
                         u[2] = u01_32(w.z);
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void varor_float_kernel(GenArgs a, double cxpb
             }
             if (d.op == 1 && in && a.mut == DM_MUT_GAUSSIAN) {
                 double dummy[4] = {0, 0, 0, 0};
-                gauss_apply<true>(a, c, g, gauss_mask<true>(a, c, g), y, dummy);
+                gauss_apply<true>(a, c, g, gauss_mask<T, true>(a, c, g), y, dummy);
             }
             if (in) Vec4<T>::store(wc, g, y);
             if constexpr (sizeof(T) == 4) {

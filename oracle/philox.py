@@ -72,3 +72,16 @@ def u01_32(w):
 def u01_53(lo, hi):
     v = ((np.asarray(hi, np.uint64) << np.uint64(32)) | np.asarray(lo, np.uint64)) >> np.uint64(11)
     return v.astype(np.float64) * 1.1102230246251565e-16
+
+
+def gene_slot(g, itemsize):
+    """Philox slot (sub, word) of gene g in the per-gene streams ST_BLEND /
+    ST_MASK (deap_amd/csrc/generation.hpp gene4_words): the four words of a
+    call feed the four genes one lane holds in a 256-gene chunk of the hot
+    kernel's layout — fp64 rows: genes {256c + 2L, +1, 256c + 128 + 2L, +1};
+    fp32 rows: genes 256c + 4L .. +3 — with call sub = 64c + L."""
+    g = np.asarray(g, np.int64)
+    if itemsize == 4:
+        return g >> 2, g & 3
+    r = g & 255
+    return ((g >> 8) << 6) + ((r & 127) >> 1), ((r >> 7) << 1) | (r & 1)

@@ -333,13 +333,11 @@ def test_native_decisions_follow_the_documented_stream(gpu):
     mflags = wm[:, 0].astype(np.uint64) < philox.prob_threshold(0.2)
     assert np.array_equal(dn["mut_flag"].astype(bool), mflags)
     # per-gene masks of float genomes
-    genes = np.arange(0, dim, 4)
     mask = np.zeros((n, dim), bool)
-    for gi in genes:
-        ww = r(philox.ST_MASK, c, gi // 4)
-        for j in range(4):
-            if gi + j < dim:
-                mask[:, gi + j] = ww[:, j].astype(np.uint64) < philox.prob_threshold(0.05)
+    for gi in range(dim):
+        sub, word = philox.gene_slot(gi, 8)
+        ww = r(philox.ST_MASK, c, int(sub))
+        mask[:, gi] = ww[:, int(word)].astype(np.uint64) < philox.prob_threshold(0.05)
     got = ops.unpack_mask(dn["mut_mask"], dim)
     assert np.array_equal(got[mflags], mask[mflags])
 
@@ -388,16 +386,14 @@ def test_sel_best_large_ties(gpu):
     ("f64", 700, 5000, "blend", "gaussian", "rosenbrock", "random"),
     ("f64", 1000, 4099, "blend", "gaussian", "rastrigin", "tournament7"),
 ])
-@pytest.mark.parametrize("hot", ["pipe", "rows"])
-def test_native_hot_kernel_equals_replay_kernel(gpu, monkeypatch, hot, gt, dim, n, cx, mut,
-                                                objective, sel):
-    """The whole-row hot kernel (native mode, lane-parallel decisions) draws
-    the same decisions as the replay kernel's dump mode and produces the same
-    generation bit for bit (the dump mode is itself replayed in the oracle).
-    Both hot variants run: the rolling pipeline (default) and the one-pair rows
-    kernel (DM_HOT_KERNEL=rows)."""
+def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
+    """The hot path (per-pair plan kernel + rolling-pipeline kernel, native
+    mode) draws the same decisions as the replay kernel's dump mode and
+    produces the same genomes bit for bit (the dump mode is itself replayed in
+    the oracle).  Fitness sums run in a different lane order (different
+    cosine too, for Rastrigin), so wvalues agree to 1e-12 relative — the
+    tolerance the north star sets for fp64 fitness."""
     from deap_amd import algorithms, benchmarks, tools
-    monkeypatch.setenv("DM_HOT_KERNEL", hot)
     from deap_amd.ops import RandomStream
     outs = []
     for mode in ("native", "dump"):
@@ -417,5 +413,5 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, monkeypatch, hot, gt, dim, 
     (g2, wv2, ok2), nev2 = outs[1]
     assert np.array_equal(g1, g2)
     assert np.array_equal(ok1, ok2)
-    assert np.array_equal(wv1, wv2)
+    assert _rel_close(wv1, wv2, 1e-12)
     assert nev1 == nev2
