@@ -266,6 +266,13 @@ struct PipeArgs {
 #define DM_PIPE_MINWAVES 2
 #endif
 
+// Ablation switches for profiling builds only (bit 1: skip evaluation, 2:
+// cxBlend without Philox (u = 0.5), 4: skip mutation).  Results are wrong
+// in such builds; the product build has DM_PIPE_ABLATE = 0.
+#ifndef DM_PIPE_ABLATE
+#define DM_PIPE_ABLATE 0
+#endif
+
 #ifndef DM_PIPE_DEPTH
 #define DM_PIPE_DEPTH 2
 #endif
@@ -341,7 +348,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
             }
             const uint32_t slot = (uint32_t)((ch << 6) + lane);  // gene_slot of this lane's genes
             if (CX == DM_CX_BLEND && cx) {
-                const u32x4 u = a.rng(ST_BLEND, (uint32_t)p, slot);
+                const u32x4 u = (DM_PIPE_ABLATE & 2) ? u32x4{1u << 31, 1u << 31, 1u << 31, 1u << 31}
+                                                     : a.rng(ST_BLEND, (uint32_t)p, slot);
                 const uint32_t us[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -369,7 +377,7 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                     x1[k] = (double)(float)x1[k];
                 }
             }
-            if (MUT == DM_MUT_GAUSSIAN && (mut0 || mut1)) {
+            if (MUT == DM_MUT_GAUSSIAN && !(DM_PIPE_ABLATE & 4) && (mut0 || mut1)) {
                 // per-gene Bernoulli(indpb) + gauss(mu, sigma)   (mutation.py:44-46)
                 uint32_t keep = 0;
 #pragma unroll
@@ -421,7 +429,7 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
                     x1[k] = (double)(float)x1[k];
                 }
             }
-            if (EC != EC_NONE) {
+            if (EC != EC_NONE && !(DM_PIPE_ABLATE & 1)) {
                 pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x0, cstab, inv0, acc0, carry0);
                 pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x1, cstab, inv1, acc1, carry1);
             }

@@ -31,14 +31,25 @@ def _torch():
 
 
 def row_stride(gtype, dim):
-    """Bytes per genome row: padded to 4-gene vectors and 16-byte alignment."""
+    """Bytes per genome row: padded to 4-gene vectors, then to whole 128-B
+    lines (rows of >= 128 B) or to a power of two (shorter rows), so no row
+    shares an HBM line with its neighbour.  Rastrigin-1000D fp64 rows are
+    8064 B: with 8000-B rows every odd row straddles lines and the row copy
+    tops out at 5.15 TB/s instead of 5.6 (tools_gpu/bwtest2.hip).
+    The pad bytes are never read or written by the kernels."""
     if gtype == _lib.DM_BITS:
         b = ((dim + 63) // 64) * 8
     elif gtype == _lib.DM_F32:
         b = ((dim + 3) // 4) * 16
     else:
         b = ((dim + 3) // 4) * 32
-    return (b + 15) // 16 * 16
+    b = (b + 15) // 16 * 16
+    if b >= 128:
+        return (b + 127) // 128 * 128
+    p = 16
+    while p < b:
+        p *= 2
+    return p
 
 
 class Context:
