@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--mig-every", type=int, default=5)
     ap.add_argument("--mig-k", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=8192)
+    ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1234)
     return ap.parse_args()
 
@@ -75,8 +75,9 @@ def load_traffic(config):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(config)
-    except (OSError, ValueError):
+            ent = json.load(f).get(config)
+        return ent["bytes_per_launch"] if ent else None
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
@@ -126,12 +127,8 @@ def main():
         from deap_amd.islands import migRingDistributed
         migRingDistributed([pop], [rank], world, args.mig_k, tools.selBest, stream=stream)
 
-    def one_gen(g, ev_pair=None):
-        if ev_pair is not None:
-            ev_pair[0].record()
+    def one_gen(g):
         step.step(pop, off, stream, ctypes_ptr(nevals, g))
-        if ev_pair is not None:
-            ev_pair[1].record()
         pop.swap_storage(off)
         if world > 1 and (g + 1) % args.mig_every == 0:
             migrate()
@@ -147,11 +144,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # HIP event pairs recorded by the library itself around the generation
+    # kernel (gen_pipe_kernel), on the stream it is launched on
+    from deap_amd import _lib
+    ctx = pop.ctx.bind()
+    _lib.call("dm_ctx_set_timing", ctx, args.steps)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        one_gen(args.warmup + s, events[s])
+        one_gen(args.warmup + s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -161,7 +161,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    times = (ctypes.c_float * args.steps)()
+    cnt = ctypes.c_int32(0)
+    _lib.call("dm_ctx_kernel_times", ctx, times, args.steps, ctypes.byref(cnt))
+    _lib.call("dm_ctx_set_timing", ctx, 0)
+    assert cnt.value == args.steps, "expected one generation kernel per step, got %d" % cnt.value
+    kern_ms = sum(times) / args.steps
     if world > 1:
         t = torch.tensor([kern_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -177,7 +182,8 @@ def main():
     achieved = (n * bpi) / (kern_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(args.config), "kernel": "gen_float_kernel/gen_bits_kernel",
+                "traffic": load_traffic(args.config),
+                "kernel": "gen_bits_kernel" if gtype == "bits" else "gen_pipe_kernel",
                 "kernel_ms": round(kern_ms, 4), "bytes_per_ind_gen": bpi}
     out = {"metric": "individual-generations/sec @pop=2^20 Rastrigin-1000D, 1-8 GPU; % HBM peak",
            "value": round(value, 1), "unit": "individual-generations/sec", "n_gpus": world,

@@ -75,6 +75,8 @@ SIGNATURES = {
     "dm_ctx_destroy": (ctypes.c_int, [_p]),
     "dm_ctx_set_stream": (ctypes.c_int, [_p, _p]),
     "dm_ctx_sync": (ctypes.c_int, [_p]),
+    "dm_ctx_set_timing": (ctypes.c_int, [_p, _i32]),
+    "dm_ctx_kernel_times": (ctypes.c_int, [_p, _p, _i32, _PP(_i32)]),
     "dm_philox_blocks": (ctypes.c_int, [_p, _PP(_u32), _PP(_u32), _i64, _p]),
     "dm_init_uniform": (ctypes.c_int, [_p, _PP(DevicePop), _f64, _f64, Rng]),
     "dm_evaluate": (ctypes.c_int, [_p, _PP(DevicePop), _PP(Eval), ctypes.c_int, _p]),

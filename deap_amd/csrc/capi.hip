@@ -440,7 +440,33 @@ int dm_ctx_destroy(dm_ctx* ctx) {
         if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->zig) (void)hipFree(ctx->zig);
+    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     delete ctx;
+    return DM_OK;
+}
+
+int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches) {
+    DM_CHECK_ARG(ctx != nullptr && max_launches >= 0, "bad argument");
+    if (ctx->stream) DM_HIP(hipStreamSynchronize(ctx->stream));
+    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+    ctx->tev.clear();
+    ctx->tev_used = 0;
+    for (int i = 0; i < 2 * max_launches; ++i) {
+        hipEvent_t e;
+        DM_HIP(hipEventCreate(&e));
+        ctx->tev.push_back(e);
+    }
+    return DM_OK;
+}
+
+int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count) {
+    DM_CHECK_ARG(ctx != nullptr && count != nullptr && (ms != nullptr || cap == 0), "bad argument");
+    const int n = std::min(ctx->tev_used, (int)cap);
+    for (int i = 0; i < n; ++i) {
+        DM_HIP(hipEventSynchronize(ctx->tev[2 * i + 1]));
+        DM_HIP(hipEventElapsedTime(&ms[i], ctx->tev[2 * i], ctx->tev[2 * i + 1]));
+    }
+    *count = ctx->tev_used;
     return DM_OK;
 }
 

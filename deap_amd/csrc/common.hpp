@@ -52,7 +52,27 @@ struct dm_ctx {
     size_t pinned_bytes = 0;
     int num_cus = 256;
     double* zig = nullptr;  // ziggurat tables (device), see zig_normal
+    // Hot-kernel timing (dm_ctx_set_timing): HIP event pairs recorded on the
+    // launch stream around each generation kernel, for bench.py's roofline.
+    std::vector<hipEvent_t> tev;
+    int tev_used = 0;  // pairs recorded so far
 };
+
+namespace dm {
+// Event pair i around the next generation-kernel launch (no-op when timing is
+// off or every pair has been used).
+inline void timing_begin(dm_ctx* ctx) {
+    const int i = ctx->tev_used;
+    if (2 * i + 1 < (int)ctx->tev.size()) (void)hipEventRecord(ctx->tev[2 * i], ctx->stream);
+}
+inline void timing_end(dm_ctx* ctx) {
+    const int i = ctx->tev_used;
+    if (2 * i + 1 < (int)ctx->tev.size()) {
+        (void)hipEventRecord(ctx->tev[2 * i + 1], ctx->stream);
+        ctx->tev_used = i + 1;
+    }
+}
+}  // namespace dm
 
 namespace dm {
 // Grow-only scratch arenas; returns nullptr on failure (error set).  Growing

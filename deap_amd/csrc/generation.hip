@@ -144,10 +144,12 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.sigma = a.sigma;
         q.w0 = a.w0;
         q.ev = a.ev;
+        timing_begin(ctx);
         if (parents->gtype == DM_F64)
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
         else
             launch_gen_pipe_f32(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
+        timing_end(ctx);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
@@ -157,6 +159,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     int64_t blocks = (npairs + groups_per_block - 1) / groups_per_block;
     blocks = std::min<int64_t>(blocks, (int64_t)ctx->num_cus * 16);
     const dim3 grid((unsigned)std::max<int64_t>(blocks, 1));
+    timing_begin(ctx);
     if (parents->gtype == DM_BITS)
         launch_gen_bits(a, ec, G, grid, ctx->stream);
     else if (parents->gtype == DM_F64)
@@ -165,6 +168,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     else
         (mode == DM_RNG_NATIVE ? launch_gen_f32_native : launch_gen_f32_replay)(a, ec, G, grid,
                                                                                  ctx->stream);
+    timing_end(ctx);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

@@ -146,6 +146,13 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out);
 int dm_ctx_destroy(dm_ctx* ctx);
 int dm_ctx_set_stream(dm_ctx* ctx, void* hip_stream);
 int dm_ctx_sync(dm_ctx* ctx);  /* hipStreamSynchronize on the ctx stream */
+/* Measurement hook (no reference counterpart; used by bench.py): record a HIP
+ * event pair on the ctx stream around each of the next `max_launches`
+ * generation-kernel launches of dm_generation (0 = off).  dm_ctx_kernel_times
+ * waits for them and writes up to `cap` durations in ms; *count = pairs
+ * recorded. */
+int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches);
+int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count);
 
 /* ---- RNG (test + init) ---------------------------------------------------- */
 /* Raw Philox4x32-10 blocks: out[i*4..i*4+3] = philox(ctr_i, key) with
