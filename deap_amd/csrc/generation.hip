@@ -153,6 +153,21 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
+    // packed-bit hot path (C2): same plan kernel + a pipelined one-wave-per-pair
+    // kernel (generation_pipe_bits.hip)
+    if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 64 &&
+        parents->nobj == 1 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
+        !std::getenv("DM_DISABLE_PIPE")) {
+        PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
+        if (!plans) return DM_ERR_NOMEM;
+        launch_pair_plans(a, plans, ctx->stream);
+        DM_LAUNCH_CHECK();
+        timing_begin(ctx);
+        launch_gen_bits_pipe(a, plans, ec != EC_NONE, ctx->num_cus, ctx->stream);
+        timing_end(ctx);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
     const int G = parents->gtype == DM_BITS ? pick_group_bits(a.words64)
                                             : pick_group_float(parents->dim);
     const int64_t groups_per_block = 256 / G;

@@ -526,5 +526,8 @@ void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, in
                          hipStream_t s);
 void launch_gen_pipe_f32(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s);
+// Packed-bit hot path (generation_pipe_bits.hip): rows of <= 64 words, one objective.
+void launch_gen_bits_pipe(const GenArgs& a, const PairPlan* plans, bool eval, int num_cus,
+                          hipStream_t s);
 
 }  // namespace dm

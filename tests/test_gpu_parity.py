@@ -385,6 +385,10 @@ def test_sel_best_large_ties(gpu):
     ("f32", 1000, 6001, "blend", "gaussian", "rastrigin", "tournament"),
     ("f64", 700, 5000, "blend", "gaussian", "rosenbrock", "random"),
     ("f64", 1000, 4099, "blend", "gaussian", "rastrigin", "tournament7"),
+    # packed bits (C2 hot path): ring of D pairs per wave wraps several times
+    ("bits", 4096, 40001, "twopoint", "flipbit", "onemax", "tournament"),
+    ("bits", 100, 3000, "twopoint", "flipbit", "onemax", "random"),
+    ("bits", 1000, 999, "twopoint", "flipbit", "onemax", "tournament7"),
 ])
 def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
     """The hot path (per-pair plan kernel + rolling-pipeline kernel, native
