@@ -183,7 +183,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(args.config),
-                "kernel": "gen_bits_kernel" if gtype == "bits" else "gen_pipe_kernel",
+                "kernel": "gen_bits_pipe_kernel" if gtype == "bits" else "gen_pipe_kernel",
                 "kernel_ms": round(kern_ms, 4), "bytes_per_ind_gen": bpi}
     out = {"metric": "individual-generations/sec @pop=2^20 Rastrigin-1000D, 1-8 GPU; % HBM peak",
            "value": round(value, 1), "unit": "individual-generations/sec", "n_gpus": world,

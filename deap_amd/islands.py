@@ -40,7 +40,7 @@ def migRingDistributed(demes, deme_ids, n_demes, k, selection, replacement=None,
     if migarray is None:
         migarray = list(range(1, n_demes)) + [0]
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    owner = _owner_map(deme_ids, n_demes, world, group)
+    owner = owner_map(deme_ids, n_demes, world, group)
     local = dict(zip(deme_ids, demes))
     emig, immig = {}, {}
     for d, pop in local.items():
@@ -50,26 +50,36 @@ def migRingDistributed(demes, deme_ids, n_demes, k, selection, replacement=None,
             immig[d] = emig[d]
         else:
             immig[d] = pack(pop, replacement_indices(replacement, pop, k, stream))
-    # route emigrant blocks: from_deme -> migarray[from_deme]
-    received = {}
-    ops = []
     me = dist.get_rank(group) if dist.is_initialized() else 0
-    for frm in range(n_demes):
-        to = migarray[frm]
+    received = route_blocks(emig, lambda d: torch.empty_like(immig[d]), owner, migarray,
+                            me, group)
+    for d, pop in local.items():
+        place(pop, immig[d], received[d], k)
+
+
+def route_blocks(emig, make_recv, owner, migarray, me, group=None):
+    """Move emigrant blocks ``from_deme -> migarray[from_deme]``.
+
+    ``emig``: this rank's {deme: block}; ``make_recv(d)`` allocates the receive
+    buffer for local deme ``d``; ``owner``: global deme -> rank.  Same-rank
+    hops are device references; cross-rank hops are one isend/irecv pair each,
+    issued as a single batched P2P group (RCCL groupStart/groupEnd).  Returns
+    {local deme: received block}."""
+    received, ops = {}, []
+    for frm, to in enumerate(migarray):
         src_rank, dst_rank = owner[frm], owner[to]
         if src_rank == me and dst_rank == me:
             received[to] = emig[frm]
         elif src_rank == me:
             ops.append(dist.P2POp(dist.isend, emig[frm], dst_rank, group))
         elif dst_rank == me:
-            buf = torch.empty_like(immig[to])
+            buf = make_recv(to)
             received[to] = buf
             ops.append(dist.P2POp(dist.irecv, buf, src_rank, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-    for d, pop in local.items():
-        place(pop, immig[d], received[d], k)
+    return received
 
 
 def _select(selection, pop, k, stream):
@@ -77,20 +87,16 @@ def _select(selection, pop, k, stream):
     return op(pop, k, *a, stream=stream, **kw)
 
 
-def _owner_map(deme_ids, n_demes, world, group):
+def owner_map(deme_ids, n_demes, world, group):
     """Global deme -> rank, agreed by all ranks."""
     if world == 1:
         return {d: 0 for d in range(n_demes)}
-    mine = torch.full((n_demes,), -1, dtype=torch.int64)
     me = dist.get_rank(group)
-    for d in deme_ids:
-        mine[d] = me
-    # all ranks contribute their ownership; CPU tensor all_reduce needs gloo,
-    # so derive it from the even split when possible
+    # ownership follows from the even contiguous split every rank agrees on
     per = n_demes // world
     if per * world == n_demes and list(deme_ids) == list(range(me * per, (me + 1) * per)):
         return {d: d // per for d in range(n_demes)}
     raise ValueError("demes must be split evenly and contiguously across ranks")
 
 
-__all__ = ["migRingDistributed"]
+__all__ = ["migRingDistributed", "route_blocks", "owner_map"]
