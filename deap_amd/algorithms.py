@@ -273,6 +273,57 @@ def varOr(population, toolbox, lambda_, cxpb, mutpb, *, decisions=None, mode=Non
     return offspring
 
 
+class MuPlusLambdaStep:
+    """One (mu + lambda) generation body (``deap/algorithms.py:316-329``) bound
+    to a toolbox: varOr of ``lambda_`` offspring appended after the parents
+    (with evaluation of the invalid ones fused in), HallOfFame update on the
+    offspring, ``select(population + offspring, mu)`` and the gather of the
+    chosen rows.  ``eaMuPlusLambda`` is a loop of these; ``bench.py`` times
+    them (config C5: selNSGA2 on DTLZ2)."""
+
+    def __init__(self, population, toolbox, mu, lambda_, cxpb, mutpb):
+        assert (cxpb + mutpb) <= 1.0, (
+            "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
+        self.mu, self.lambda_ = mu, lambda_
+        self.sel = _selection_spec(toolbox)
+        self.var = _variation(population, resolve(toolbox.mate), resolve(toolbox.mutate), cxpb,
+                              mutpb)
+        self.ev = _eval(population, resolve(toolbox.evaluate))
+        n0 = len(population)
+        cap = max(n0, mu) + lambda_
+        self.combined = population.like(n0 + lambda_, capacity=cap)
+        self.nxt = population.like(mu, capacity=cap)
+        self.n = n0
+        # combined rows [0, n) = population
+        _lib.call("dm_gather", population.ctx.bind(), ctypes.byref(population.c_pop()), None,
+                  ctypes.byref(self.combined.c_pop(0, n0)))
+
+    def step(self, stream, nevals_ptr=None, mode=None, decisions=None, gen_index=0,
+             halloffame=None):
+        comb, n, lam = self.combined, self.n, self.lambda_
+        ctx = comb.ctx.bind()
+        code, d = _mode_and_decisions(mode, decisions, gen_index, lam, comb, 0, self.var,
+                                      varor=True)
+        dec = d.c_struct() if d is not None else None
+        _lib.call("dm_var_or", ctx, ctypes.byref(comb.c_pop(0, n)),
+                  ctypes.byref(comb.c_pop(n, lam)), ctypes.byref(self.var), ctypes.byref(self.ev),
+                  stream.next(), code, ctypes.byref(dec) if dec is not None else None, nevals_ptr)
+        comb.resize(n + lam)
+        if halloffame is not None:
+            halloffame.update(_View(comb, n, lam))
+        sel_op, sel_args, sel_kw = self.sel
+        idx = sel_op(comb, self.mu, *sel_args, stream=stream, **sel_kw)
+        self.nxt.resize(self.mu)
+        _lib.call("dm_gather", ctx, ctypes.byref(comb.c_pop()), ctypes.c_void_p(idx.data_ptr()),
+                  ctypes.byref(self.nxt.c_pop(0, self.mu)))
+        if getattr(comb, "crowding_dist", None) is not None:
+            self.nxt.crowding_dist = comb.crowding_dist[idx.long()]
+        comb.swap_storage(self.nxt)
+        self.n = self.mu
+        comb.resize(self.mu)
+        return comb
+
+
 def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=None,
                    halloffame=None, verbose=__debug__, *, decisions=None, mode=None,
                    stream=None):
@@ -282,14 +333,9 @@ def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=No
     (the order matters to NSGA-II's front order)."""
     _check_pop(population)
     stream = stream or default_stream()
-    mate = resolve(toolbox.mate)
-    mutate = resolve(toolbox.mutate)
-    evaluate = resolve(toolbox.evaluate)
-    sel_op, sel_args, sel_kw = _selection_spec(toolbox)
-    var = _variation(population, mate, mutate, cxpb, mutpb)
     assert (cxpb + mutpb) <= 1.0, (
         "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
-    ev = _eval(population, evaluate)
+    ev = _eval(population, resolve(toolbox.evaluate))
     book = _Bookkeeping(population, ngen, stats, halloffame, verbose)
     ctx = population.ctx.bind()
 
@@ -297,38 +343,14 @@ def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=No
               book.nevals_ptr(0))
     book.record(0, population)
 
-    n0 = len(population)
-    cap = max(n0, mu) + lambda_
-    combined = population.like(n0 + lambda_, capacity=cap)
-    nxt = population.like(mu, capacity=cap)
-    # combined rows [0, n) = population
-    _lib.call("dm_gather", ctx, ctypes.byref(population.c_pop()), None,
-              ctypes.byref(combined.c_pop(0, n0)))
-    n = n0
+    step = MuPlusLambdaStep(population, toolbox, mu, lambda_, cxpb, mutpb)
     for gen in range(1, ngen + 1):
-        code, d = _mode_and_decisions(mode, decisions, gen - 1, lambda_, population, 0, var,
-                                      varor=True)
-        dec = d.c_struct() if d is not None else None
-        _lib.call("dm_var_or", ctx, ctypes.byref(combined.c_pop(0, n)),
-                  ctypes.byref(combined.c_pop(n, lambda_)), ctypes.byref(var), ctypes.byref(ev),
-                  stream.next(), code, ctypes.byref(dec) if dec is not None else None,
-                  book.nevals_ptr(gen))
-        combined.resize(n + lambda_)
-        if halloffame is not None:
-            halloffame.update(_View(combined, n, lambda_))
-        idx = sel_op(combined, mu, *sel_args, stream=stream, **sel_kw)
-        nxt.resize(mu)
-        _lib.call("dm_gather", ctx, ctypes.byref(combined.c_pop()),
-                  ctypes.c_void_p(idx.data_ptr()), ctypes.byref(nxt.c_pop(0, mu)))
-        if getattr(combined, "crowding_dist", None) is not None:
-            nxt.crowding_dist = combined.crowding_dist[idx.long()]
-        combined.swap_storage(nxt)
-        n = mu
-        combined.resize(mu)
+        combined = step.step(stream, book.nevals_ptr(gen), mode, decisions, gen - 1, halloffame)
         rec = stats.compile(combined) if stats else {}
         book.records.append((gen, rec))
         if verbose:
             book._flush_one(gen, rec)
+    combined = step.combined
     # hand the final population back in place
     final = population.like(mu, capacity=max(mu, 1))
     _lib.call("dm_gather", ctx, ctypes.byref(combined.c_pop(0, mu)), None,
@@ -350,4 +372,4 @@ class _View(DevicePopulation):
         self.capacity = count
 
 
-__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda"]
+__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda"]  # + GenerationStep, MuPlusLambdaStep

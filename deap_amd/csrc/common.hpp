@@ -43,11 +43,11 @@ void set_error(const char* fmt, ...);
 
 // Opaque context: one device, one stream, grow-only scratch arena.
 struct dm_ctx {
-    static constexpr int kSlots = 4;
+    static constexpr int kSlots = 5;
     int device = 0;
     hipStream_t stream = nullptr;
-    void* scratch[kSlots] = {nullptr, nullptr, nullptr, nullptr};
-    size_t scratch_bytes[kSlots] = {0, 0, 0, 0};
+    void* scratch[kSlots] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t scratch_bytes[kSlots] = {0, 0, 0, 0, 0};
     void* pinned = nullptr;  // small host staging area for host-synchronising calls
     size_t pinned_bytes = 0;
     int num_cus = 256;

@@ -119,7 +119,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         const int nch = parents->dim <= 512 ? 2 : 4;
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
         if (!plans) return DM_ERR_NOMEM;
-        launch_pair_plans(a, plans, ctx->stream);
+        launch_pair_plans(a, plans, nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
         PipeArgs q{};
         q.pgenes = a.pgenes;
@@ -153,14 +153,14 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
-    // packed-bit hot path (C2): same plan kernel + a pipelined one-wave-per-pair
-    // kernel (generation_pipe_bits.hip)
+    // packed-bit hot path (C2): same plan kernel (which also counts nevals) + a
+    // one-shot burst kernel (generation_pipe_bits.hip)
     if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 64 &&
         parents->nobj == 1 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
         !std::getenv("DM_DISABLE_PIPE")) {
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
         if (!plans) return DM_ERR_NOMEM;
-        launch_pair_plans(a, plans, ctx->stream);
+        launch_pair_plans(a, plans, ec != EC_NONE ? a.nevals : nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
         timing_begin(ctx);
         launch_gen_bits_pipe(a, plans, ec != EC_NONE, ctx->num_cus, ctx->stream);

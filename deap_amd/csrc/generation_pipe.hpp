@@ -520,7 +520,7 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 }
 
 // Decisions of every pair (thread per pair), generation_pipe_f64.hip.
-void launch_pair_plans(const GenArgs& a, PairPlan* plans, hipStream_t s);
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, int64_t* count_evals, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s);

@@ -6,12 +6,14 @@
 //  1. pair_plan_kernel (generation_pipe_f64.hip) — one thread per pair draws
 //     the tournaments, the crossover flag and cxTwoPoint cuts, the mutation
 //     flags (same Philox counters as gen_bits_kernel);
-//  2. gen_bits_pipe_kernel — one wave per pair on a persistent grid; lane L
-//     holds word L of both parent rows (one 512-B load instruction per row).
-//     The rows of the next D pairs of the wave are in flight while a pair is
-//     varied, so the per-pair latency chain (plan -> rows -> store) that
-//     bounds gen_bits_kernel (tournament loads, then row loads, per pair, in
-//     every wave) is paid once per wave instead of once per pair.
+//     With evaluation on it also counts `nevals` (one atomic per workgroup).
+//  2. gen_bits_burst_kernel — one-shot grid, each wave takes DM_BITS_PP
+//     consecutive pairs: all their plans (scalar loads) and then all their
+//     parent rows (lane L holds word L, one 512-B load per row) are issued
+//     before the first pair is varied.  A persistent grid with a D-deep row
+//     ring (r01c: 0.315 ms per C2 generation) ran at 3.5 TB/s where a
+//     one-shot copy of the same rows reaches 6.0-6.6 TB/s
+//     (tools_gpu/bwtest5.hip, profiles/r01f).
 //
 // Per pair: cxTwoPoint = masked word swap (crossover.py:37-60), mutFlipBit =
 // geometric-skip flip masks (flip_mask_word, mutation.py:124-142), OneMax =
@@ -23,61 +25,43 @@
 
 namespace dm {
 
-#ifndef DM_BITS_PIPE_DEPTH
-#define DM_BITS_PIPE_DEPTH 4
+#ifndef DM_BITS_PP
+#define DM_BITS_PP 4  // pairs per wave (tools_gpu/bwtest5.hip: 2-4 best)
 #endif
 
 template <int CX, int MUT, bool EVAL>
-__global__ __launch_bounds__(256) void gen_bits_pipe_kernel(GenArgs a, const PairPlan* plans) {
-    constexpr int D = DM_BITS_PIPE_DEPTH;
+__global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const PairPlan* plans) {
+    constexpr int PP = DM_BITS_PP;
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (p >= npairs) return;
+    const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PP;
+    if (p0 >= npairs) return;
     const int words = a.words64;
     const bool lw = lane < words;
-    auto clampq = [&](int64_t q) { return q < npairs ? q : p; };
     auto row = [&](int32_t s) {
         return reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)s * a.pstride);
     };
-
-    // ring: plans of pairs p + d*nw (d = 0..D), rows of pairs p + d*nw (d < D)
-    PairPlan pl[D + 1];
-    uint64_t y0[D], y1[D];
+    // every plan (scalar loads) and then every parent row of the wave's PP
+    // pairs are issued before the first pair is varied
+    PairPlan pl[PP];
 #pragma unroll
-    for (int d = 0; d <= D; ++d) pl[d] = load_plan(plans, clampq(p + d * nw));
+    for (int k = 0; k < PP; ++k) pl[k] = load_plan(plans, p0 + k < npairs ? p0 + k : p0);
+    uint64_t y0[PP], y1[PP];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-        y0[d] = 0;
-        y1[d] = 0;
-        if (lw && p + d * nw < npairs) {
-            y0[d] = row(pl[d].s0)[lane];
-            y1[d] = row(pl[d].s1)[lane];
+    for (int k = 0; k < PP; ++k) {
+        y0[k] = 0;
+        y1[k] = 0;
+        if (lw && p0 + k < npairs) {
+            y0[k] = row(pl[k].s0)[lane];
+            y1[k] = row(pl[k].s1)[lane];
         }
     }
-    int64_t evals = 0;
-    for (; p < npairs; p += nw) {
-        const PairPlan cur = pl[0];
-        // issue the rows of pair p + D*nw before touching this pair's rows
-        const int64_t pf = p + D * nw;
-        uint64_t n0 = 0, n1 = 0;
-        if (lw && pf < npairs) {
-            n0 = row(pl[D].s0)[lane];
-            n1 = row(pl[D].s1)[lane];
-        }
-        uint64_t x0 = y0[0], x1 = y1[0];
 #pragma unroll
-        for (int d = 0; d < D - 1; ++d) {
-            y0[d] = y0[d + 1];
-            y1[d] = y1[d + 1];
-        }
-        y0[D - 1] = n0;
-        y1[D - 1] = n1;
-#pragma unroll
-        for (int d = 0; d < D; ++d) pl[d] = pl[d + 1];
-        pl[D] = load_plan(plans, clampq(p + (D + 1) * nw));
-
+    for (int k = 0; k < PP; ++k) {
+        const int64_t p = p0 + k;
+        if (p >= npairs) break;
+        const PairPlan& cur = pl[k];
+        uint64_t x0 = y0[k], x1 = y1[k];
         const uint32_t fl = cur.flags;
         const bool has1 = fl & PF_HAS1, inv0 = fl & PF_INV0, inv1 = fl & PF_INV1;
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
@@ -107,7 +91,6 @@ __global__ __launch_bounds__(256) void gen_bits_pipe_kernel(GenArgs a, const Pai
                 if (has1) a.cwv[c1] = inv1 ? (double)(pc >> 16) * a.w0 : cur.f1;
                 a.cvalid[c0] = 1;
                 if (has1) a.cvalid[c1] = 1;
-                evals += (int64_t)inv0 + (int64_t)inv1;
             }
         } else if (lane == 0) {  // no evaluation requested: clones keep their fitness
             a.cwv[c0] = cur.f0;
@@ -116,14 +99,13 @@ __global__ __launch_bounds__(256) void gen_bits_pipe_kernel(GenArgs a, const Pai
             if (has1) a.cvalid[c1] = inv1 ? 0 : 1;
         }
     }
-    if (a.nevals && EVAL && lane == 0 && evals)
-        atomicAdd((unsigned long long*)a.nevals, (unsigned long long)evals);
 }
 
 template <int CX, int MUT, bool EVAL>
 static void launch_bp(const GenArgs& a, const PairPlan* plans, int num_cus, hipStream_t s) {
-    auto kern = gen_bits_pipe_kernel<CX, MUT, EVAL>;
-    kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a, plans);
+    // one-shot grid: every wave takes DM_BITS_PP consecutive pairs once
+    const int64_t waves = ((a.nc + 1) / 2 + DM_BITS_PP - 1) / DM_BITS_PP;
+    gen_bits_burst_kernel<CX, MUT, EVAL><<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(a, plans);
 }
 template <int CX, int MUT>
 static void launch_bp_e(const GenArgs& a, const PairPlan* plans, bool eval, int num_cus,

@@ -10,10 +10,9 @@ namespace dm {
 // cxTwoPoint cuts (algorithms.py:72-76, crossover.py:62-70), the two mutation
 // flags (algorithms.py:78-81) and which children need evaluation
 // (algorithms.py:75-81 `del fitness.values`, algorithms.py:155-158).
-__global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t npairs = (a.nc + 1) / 2;
-    if (p >= npairs) return;
+// Decisions of pair p -> plans[p]; returns the plan's flags.
+__device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
+                                             int64_t p) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
     const int m = a.nobj;
@@ -73,11 +72,36 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
     pl.f0 = a.pwv[(int64_t)s[0] * m];
     pl.f1 = a.pwv[(int64_t)s[1] * m];
     plans[p] = pl;
+    return fl;
 }
 
-void launch_pair_plans(const GenArgs& a, PairPlan* plans, hipStream_t s) {
+// With count_evals set, the plan kernel also adds the generation's `nevals`
+// (children whose fitness is invalidated, algorithms.py:171-174) to
+// *count_evals: one ballot per wave, one atomic per workgroup.
+__global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
+                                                        int64_t* __restrict__ count_evals) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
-    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans);
+    if (count_evals) {
+        __shared__ int32_t wave_evals[4];
+        uint32_t fl = 0;
+        if (p < npairs) fl = plan_one(a, plans, p);
+        const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
+                            __popcll(__ballot((fl & PF_INV1) != 0));
+        if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int64_t t = (int64_t)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
+            if (t) atomicAdd((unsigned long long*)count_evals, (unsigned long long)t);
+        }
+        return;
+    }
+    if (p < npairs) plan_one(a, plans, p);
+}
+
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, int64_t* count_evals, hipStream_t s) {
+    const int64_t npairs = (a.nc + 1) / 2;
+    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals);
 }
 
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,

@@ -121,17 +121,15 @@ __global__ __launch_bounds__(256) void dom_build_kernel(const double* ufit, int 
         uint64_t bits = 0;
         int cnt = 0;
         for (int b = 0; b < 64; ++b) {
-            bool ge = true, le = true, gt = false, lt = false;
+            bool gt = false, lt = false;  // NaN objectives compare equal (base.py:209-224)
             for (int o = 0; o < m; ++o) {
                 const double x = fu[o];
                 const double y = sfit[(o * 64 + b) * DT_WORDS + wl];
-                ge &= x >= y;
-                le &= x <= y;
                 gt |= x > y;
                 lt |= x < y;
             }
-            bits |= (uint64_t)(ge && gt) << b;  // u dominates v     (base.py:209-224)
-            cnt += (le && lt) ? 1 : 0;          // v dominates u
+            bits |= (uint64_t)(gt && !lt) << b;  // u dominates v
+            cnt += (lt && !gt) ? 1 : 0;          // v dominates u
         }
         if (w < W) D[u * W + w] = bits;
         // reduce cnt over the 32 lanes of this half-wave
@@ -139,6 +137,98 @@ __global__ __launch_bounds__(256) void dom_build_kernel(const double* ufit, int 
         for (int o = 16; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
         if (wl == 0 && cnt) atomicAdd(&count[u], cnt);
     }
+}
+
+// Ballot form (the path taken for 2..4 objectives).  A wave owns DB_WPW
+// consecutive words of v (lane L of word k <-> v = 64*(w0+k) + L, fitness in
+// VGPRs) and sweeps a tile of DB_ROWS rows u with u wave-uniform (fitness
+// from scalar loads).  Fitness.dominates (base.py:209-224) returns False at
+// the first objective with x < y and needs one with x > y — an objective where
+// either side is NaN counts as equal — so with one wave mask per objective
+// and compare over the 64 lanes:
+//   D[u][w]                = ANY(x > y) & ~ANY(x < y)     (u dominates v)
+//   #v in w dominating u   = popcount(ANY(x < y) & ~ANY(x > y))
+// The mask of row u is parked in lane u%64 and every 64 rows each lane stores
+// its row's DB_WPW words; dominator counts go to per-word-group partials
+// cpart[g][u] (summed by dom_count_reduce_kernel, no atomics).
+constexpr int DB_WPW = 8;     // words per wave (512 v)
+constexpr int DB_ROWS = 512;  // rows u per wave
+
+template <int M>
+__global__ __launch_bounds__(256) void dom_ballot_kernel(const double* __restrict__ ufit, int64_t U,
+                                                         int64_t W, int64_t ngroups,
+                                                         int64_t ntiles, uint64_t* __restrict__ D,
+                                                         int32_t* __restrict__ cpart) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (gw >= ngroups * ntiles) return;
+    const int64_t grp = gw % ngroups, tile = gw / ngroups;
+    const int64_t w0 = grp * DB_WPW;
+    double y[DB_WPW][M];
+    uint64_t vmask[DB_WPW];
+#pragma unroll
+    for (int k = 0; k < DB_WPW; ++k) {
+        const int64_t v = (w0 + k) * 64 + lane;
+        const bool in = v < U;
+#pragma unroll
+        for (int o = 0; o < M; ++o) y[k][o] = in ? ufit[v * M + o] : 0.0;
+        vmask[k] = __ballot(in);
+    }
+    const int64_t u_begin = tile * DB_ROWS;
+    const int64_t u_end = u_begin + DB_ROWS < U ? u_begin + DB_ROWS : U;
+    for (int64_t ub = u_begin; ub < u_end; ub += 64) {
+        const int nb = (int)(u_end - ub < 64 ? u_end - ub : 64);
+        uint64_t acc[DB_WPW];
+#pragma unroll
+        for (int k = 0; k < DB_WPW; ++k) acc[k] = 0;
+        int32_t cacc = 0;
+        for (int j = 0; j < nb; ++j) {
+            const int64_t u = ub + j;
+            double x[M];
+#pragma unroll
+            for (int o = 0; o < M; ++o) x[o] = ufit[u * M + o];
+            int32_t cnt = 0;
+#pragma unroll
+            for (int k = 0; k < DB_WPW; ++k) {
+                uint64_t gt = 0, lt = 0;
+#pragma unroll
+                for (int o = 0; o < M; ++o) {
+                    gt |= __ballot(x[o] > y[k][o]);
+                    lt |= __ballot(x[o] < y[k][o]);
+                }
+                const uint64_t dom = gt & ~lt & vmask[k];
+                cnt += __popcll(lt & ~gt & vmask[k]);
+                acc[k] = lane == j ? dom : acc[k];
+            }
+            cacc = lane == j ? cnt : cacc;
+        }
+        if (lane < nb) {
+            uint64_t* row = D + (ub + lane) * W + w0;
+#pragma unroll
+            for (int k = 0; k < DB_WPW; ++k)
+                if (w0 + k < W) row[k] = acc[k];
+            cpart[grp * U + ub + lane] = cacc;
+        }
+    }
+}
+
+__global__ void dom_count_reduce_kernel(const int32_t* __restrict__ cpart, int64_t ngroups,
+                                        int64_t U, int32_t* __restrict__ count) {
+    GRID_LOOP(u, U) {
+        int32_t c = 0;
+        for (int64_t g = 0; g < ngroups; ++g) c += cpart[g * U + u];
+        count[u] = c;
+    }
+}
+
+template <int M>
+static void launch_dom_ballot(const double* ufit, int64_t U, int64_t W, uint64_t* D,
+                              int32_t* cpart, hipStream_t s) {
+    const int64_t ngroups = (W + DB_WPW - 1) / DB_WPW;
+    const int64_t ntiles = (U + DB_ROWS - 1) / DB_ROWS;
+    const int64_t waves = ngroups * ntiles;
+    dom_ballot_kernel<M><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(ufit, U, W, ngroups,
+                                                                        ntiles, D, cpart);
 }
 
 // ---------------------------------------------------------------------------
@@ -380,7 +470,19 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     zero_i32_kernel<<<g1(U), 256, 0, s>>>(count, U);
     fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
     unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
-    {
+    if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
+        const int64_t ngroups = (W + DB_WPW - 1) / DB_WPW;
+        int32_t* cpart = (int32_t*)scratch_slot(ctx, 4, (size_t)ngroups * U * 4);
+        if (!cpart) return DM_ERR_NOMEM;
+        if (m == 2)
+            launch_dom_ballot<2>(ufit, U, W, D, cpart, s);
+        else if (m == 3)
+            launch_dom_ballot<3>(ufit, U, W, D, cpart, s);
+        else
+            launch_dom_ballot<4>(ufit, U, W, D, cpart, s);
+        DM_LAUNCH_CHECK();
+        dom_count_reduce_kernel<<<g1(U), 256, 0, s>>>(cpart, ngroups, U, count);
+    } else {
         dim3 grid((unsigned)((W + DT_WORDS - 1) / DT_WORDS), (unsigned)((U + DT_ROWS - 1) / DT_ROWS));
         const size_t lds = (size_t)m * 64 * DT_WORDS * sizeof(double);
         dom_build_kernel<<<grid, 256, lds, s>>>(ufit, m, U, W, D, count);

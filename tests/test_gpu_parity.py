@@ -360,6 +360,47 @@ def test_sort_nondominated_large_random(gpu):
         assert chosen == want_c
 
 
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_sort_nondominated_with_nan_fitness(gpu, m):
+    """NaN objectives (e.g. ZDT1 of an out-of-range gene): Fitness.dominates
+    (base.py:209-224) treats an objective with a NaN side as equal.  The NaN
+    rows' other objectives are all -1, below every finite row, so every finite
+    row dominates them, they never dominate one another and the relation stays
+    acyclic (a cycle would hang the reference's peel loop too)."""
+    from deap_amd import tools
+    rng = np.random.default_rng(11 + m)
+    n = 700
+    wv = rng.uniform(0, 1, size=(n, m))
+    rows = rng.choice(n, 40, replace=False)
+    wv[rows] = -1.0
+    wv[rows, rng.integers(0, m, 40)] = np.nan
+    pop = _dp().from_numpy(np.zeros((n, 2)), weights=(1.0,) * m, gtype="f64", wvalues=wv,
+                           valid=np.ones(n))
+    fronts = tools.sortNondominated(pop, n)
+    want = ops.sort_nondominated(wv, n)
+    assert [f.cpu().numpy().tolist() for f in fronts] == want
+
+
+def test_dominance_ballot_equals_lds_kernel_large(gpu, monkeypatch):
+    """At sizes the oracle cannot finish: the ballot dominance kernel and the
+    LDS-tiled one (DM_DOM_LDS) give identical fronts and selNSGA2 choices."""
+    from deap_amd import tools
+    rng = np.random.default_rng(31)
+    n = 30011
+    wv = np.round(rng.uniform(0, 1, size=(n, 3)), 2)  # many equal fitnesses
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0, -1.0, 1.0), gtype="f64",
+                           wvalues=wv, valid=np.ones(n))
+    got = []
+    for lds in (False, True):
+        if lds:
+            monkeypatch.setenv("DM_DOM_LDS", "1")
+        fronts = tools.sortNondominated(pop, n)
+        got.append(([f.cpu().numpy().tolist() for f in fronts],
+                    tools.selNSGA2(pop, n // 2).cpu().numpy().tolist()))
+    assert got[0] == got[1]
+    assert sum(len(f) for f in got[0][0]) == n
+
+
 def test_sel_best_large_ties(gpu):
     from deap_amd import tools
     rng = np.random.default_rng(6)
@@ -385,7 +426,7 @@ def test_sel_best_large_ties(gpu):
     ("f32", 1000, 6001, "blend", "gaussian", "rastrigin", "tournament"),
     ("f64", 700, 5000, "blend", "gaussian", "rosenbrock", "random"),
     ("f64", 1000, 4099, "blend", "gaussian", "rastrigin", "tournament7"),
-    # packed bits (C2 hot path): ring of D pairs per wave wraps several times
+    # packed bits (C2 hot path): partial last wave of DM_BITS_PP pairs, odd n
     ("bits", 4096, 40001, "twopoint", "flipbit", "onemax", "tournament"),
     ("bits", 100, 3000, "twopoint", "flipbit", "onemax", "random"),
     ("bits", 1000, 999, "twopoint", "flipbit", "onemax", "tournament7"),
