@@ -18,6 +18,7 @@ from .ops import seed  # noqa: F401
 def __getattr__(name):
     # lazy: tools/algorithms/benchmarks import torch
     import importlib
-    if name in ("tools", "algorithms", "benchmarks", "device", "islands", "decisions"):
+    if name in ("tools", "algorithms", "benchmarks", "device", "islands", "decisions",
+                "checkpoint"):
         return importlib.import_module("." + name, __name__)
     raise AttributeError(name)

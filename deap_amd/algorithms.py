@@ -281,7 +281,10 @@ class MuPlusLambdaStep:
     chosen rows.  ``eaMuPlusLambda`` is a loop of these; ``bench.py`` times
     them (config C5: selNSGA2 on DTLZ2)."""
 
-    def __init__(self, population, toolbox, mu, lambda_, cxpb, mutpb):
+    def __init__(self, population, toolbox, mu, lambda_, cxpb, mutpb, comma=False):
+        if comma:
+            assert lambda_ >= mu, "lambda must be greater or equal to mu."
+        self.comma = comma
         assert (cxpb + mutpb) <= 1.0, (
             "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
         self.mu, self.lambda_ = mu, lambda_
@@ -312,12 +315,15 @@ class MuPlusLambdaStep:
         if halloffame is not None:
             halloffame.update(_View(comb, n, lam))
         sel_op, sel_args, sel_kw = self.sel
-        idx = sel_op(comb, self.mu, *sel_args, stream=stream, **sel_kw)
+        # (mu + lambda): select(population + offspring, mu); (mu, lambda):
+        # select(offspring, mu) (algorithms.py:428-429)
+        pool = _View(comb, n, lam) if self.comma else comb
+        idx = sel_op(pool, self.mu, *sel_args, stream=stream, **sel_kw)
         self.nxt.resize(self.mu)
-        _lib.call("dm_gather", ctx, ctypes.byref(comb.c_pop()), ctypes.c_void_p(idx.data_ptr()),
+        _lib.call("dm_gather", ctx, ctypes.byref(pool.c_pop()), ctypes.c_void_p(idx.data_ptr()),
                   ctypes.byref(self.nxt.c_pop(0, self.mu)))
-        if getattr(comb, "crowding_dist", None) is not None:
-            self.nxt.crowding_dist = comb.crowding_dist[idx.long()]
+        if getattr(pool, "crowding_dist", None) is not None:
+            self.nxt.crowding_dist = pool.crowding_dist[idx.long()]
         comb.swap_storage(self.nxt)
         self.n = self.mu
         comb.resize(self.mu)
@@ -332,6 +338,12 @@ def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=No
     The concatenation keeps parents first, then offspring, as in the reference
     (the order matters to NSGA-II's front order)."""
     _check_pop(population)
+    return _mu_lambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats, halloffame,
+                      verbose, decisions, mode, stream, comma=False)
+
+
+def _mu_lambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats, halloffame, verbose,
+               decisions, mode, stream, comma):
     stream = stream or default_stream()
     assert (cxpb + mutpb) <= 1.0, (
         "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
@@ -343,7 +355,7 @@ def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=No
               book.nevals_ptr(0))
     book.record(0, population)
 
-    step = MuPlusLambdaStep(population, toolbox, mu, lambda_, cxpb, mutpb)
+    step = MuPlusLambdaStep(population, toolbox, mu, lambda_, cxpb, mutpb, comma=comma)
     for gen in range(1, ngen + 1):
         combined = step.step(stream, book.nevals_ptr(gen), mode, decisions, gen - 1, halloffame)
         rec = stats.compile(combined) if stats else {}
@@ -360,6 +372,18 @@ def eaMuPlusLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=No
     return population, book.finish()
 
 
+def eaMuCommaLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats=None,
+                    halloffame=None, verbose=__debug__, *, decisions=None, mode=None,
+                    stream=None):
+    """(mu, lambda) evolution (``deap/algorithms.py:340-437``): varOr ->
+    evaluate invalid -> HallOfFame.update(offspring) ->
+    ``population[:] = select(offspring, mu)``."""
+    _check_pop(population)
+    assert lambda_ >= mu, "lambda must be greater or equal to mu."
+    return _mu_lambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats, halloffame,
+                      verbose, decisions, mode, stream, comma=True)
+
+
 class _View(DevicePopulation):
     """Row range of a population, sharing its buffers (no copy)."""
 
@@ -372,4 +396,4 @@ class _View(DevicePopulation):
         self.capacity = count
 
 
-__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda"]  # + GenerationStep, MuPlusLambdaStep
+__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda", "eaMuCommaLambda"]  # + GenerationStep, MuPlusLambdaStep

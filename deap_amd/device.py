@@ -206,6 +206,17 @@ class DevicePopulation:
         return (self.genes_numpy(), self.wvalues[: self.n].cpu().numpy().copy(),
                 self.valid[: self.n].cpu().numpy().astype(bool))
 
+    def rows_numpy(self, indices):
+        """(genes, wvalues, valid) of the rows ``indices`` only: gathered on the
+        device, then copied (a HallOfFame candidate set, not the population)."""
+        torch = _torch()
+        idx = torch.as_tensor(list(indices), dtype=torch.int64).to(self.device)
+        g = self.genes_view()[idx].cpu().numpy()
+        if self.gtype == _lib.DM_BITS:
+            g = unpack_bits(g.view(np.uint64), self.dim)
+        return (np.ascontiguousarray(g), self.wvalues[: self.n][idx].cpu().numpy().copy(),
+                self.valid[: self.n][idx].cpu().numpy().astype(bool))
+
     @classmethod
     def from_numpy(cls, genes, weights=(1.0,), gtype=None, wvalues=None, valid=None,
                    device=None, capacity=None, individual_class=None):
@@ -264,9 +275,13 @@ class DevicePopulation:
         when valid).  ``individual_class`` defaults to the creator type the
         population was built from; plain lists otherwise."""
         from .base import Fitness
-        genes, wv, valid = self.to_numpy()
         cls_ = individual_class or self.individual_class
-        rows = range(self.n) if indices is None else indices
+        if indices is None:
+            genes, wv, valid = self.to_numpy()
+            rows = range(self.n)
+        else:
+            genes, wv, valid = self.rows_numpy(indices)
+            rows = range(len(genes))
         out = []
         for i in rows:
             vals = genes[i].tolist()

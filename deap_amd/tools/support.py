@@ -234,20 +234,53 @@ class HallOfFame:
         n = len(pop)
         if n == 0 or self.maxsize == 0:
             return
-        if self.maxsize == 1 and self.similar is operator.eq:
-            # The reference keeps the first individual whose fitness is the
-            # strict maximum seen so far: a lexicographic first-argmax.
-            best = _first_lex_argmax(pop)
-            cand = pop.to_individuals(indices=[best])[0]
-            if len(self) == 0:
-                first = pop.to_individuals(indices=[0])[0]
-                self.insert(first)
-            if cand.fitness > self[-1].fitness:
-                if not any(self.similar(cand, h) for h in self):
+        # maxsize 1 too: a first-argmax shortcut is wrong when the argmax is
+        # similar to the hofer but a lesser non-similar row beats the hofer
+        self._update_candidates(pop)
+
+    def _update_candidates(self, pop):
+        """HallOfFame.update for any maxsize / similar without copying the
+        population: the reference loop (support.py:528-548) runs on host over a
+        candidate set C = the K best rows (device selBest: wvalues desc, index
+        asc) in population order.  With t the fitness of the K-th row, the loop
+        is accepted once it leaves a full hall whose every entry is strictly
+        better than t (else K grows): a row outside C (fitness <= t) is then
+        never in the final hall — it would be the worst entry when a better
+        row of C arrives and be evicted, or be skipped as not better than the
+        worst — and while present it only holds a slot a row of C later takes
+        (equal genomes have equal fitness within one evaluated population)."""
+        from .selection import selBest
+        n = len(pop)
+        K = min(n, max(4 * self.maxsize, 64))
+        while True:
+            order = selBest(pop, K).cpu().tolist()
+            trial = copy.copy(self)
+            trial.keys, trial.items = list(self.keys), list(self.items)
+            rows = sorted(set(order) | ({0} if len(self) == 0 else set()))
+            inds = dict(zip(rows, pop.to_individuals(indices=rows)))
+            trial._loop(rows, inds)
+            if K >= n:
+                break
+            t = inds[order[-1]].fitness
+            if len(trial) == self.maxsize and trial[-1].fitness > t:
+                break
+            K = min(n, 4 * K)
+        self.keys, self.items = trial.keys, trial.items
+
+    def _loop(self, rows, inds):
+        """support.py:528-548 over the rows of a candidate set, in order."""
+        for i in rows:
+            ind = inds[i]
+            if len(self) == 0 and self.maxsize != 0:
+                # first iteration with an empty hall: population[0] goes in
+                self.insert(inds[0])
+                continue
+            if ind.fitness > self[-1].fitness or len(self) < self.maxsize:
+                if any(self.similar(ind, hofer) for hofer in self):
+                    continue
+                if len(self) >= self.maxsize:
                     self.remove(-1)
-                    self.insert(cand)
-            return
-        self.update(pop.to_individuals())
+                self.insert(ind)
 
     def insert(self, item):
         item = copy.deepcopy(item)
@@ -277,20 +310,6 @@ class HallOfFame:
 
     def __str__(self):
         return str(self.items)
-
-
-def _first_lex_argmax(pop):
-    """Index of the first row whose wvalues tuple is the lexicographic maximum
-    among valid rows (device reductions, one objective at a time)."""
-    import torch
-    wv = pop.wvalues[: len(pop)]
-    alive = pop.valid[: len(pop)].bool()
-    for j in range(pop.nobj):
-        col = torch.where(alive, wv[:, j], torch.full_like(wv[:, j], -float("inf")))
-        m = col.max()
-        alive = alive & (col == m)
-    idx = torch.nonzero(alive)[0, 0]
-    return int(idx.item())
 
 
 __all__ = ["Statistics", "MultiStatistics", "Logbook", "HallOfFame"]

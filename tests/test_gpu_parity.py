@@ -460,3 +460,101 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
     assert np.array_equal(ok1, ok2)
     assert _rel_close(wv1, wv2, 1e-12)
     assert nev1 == nev2
+
+
+@pytest.mark.parametrize("maxsize,weights", [(1, (1.0,)), (5, (1.0,)), (12, (1.0, -1.0)),
+                                             (40, (-1.0,))])
+def test_hall_of_fame_device_equals_reference_loop(gpu, maxsize, weights):
+    """HallOfFame.update on a DevicePopulation (candidate set on device) keeps
+    exactly what the reference loop (support.py:528-548) keeps when it walks
+    every individual on the host — duplicates, fitness ties, several updates."""
+    from deap_amd import tools
+    rng = np.random.default_rng(maxsize)
+    hof_dev, hof_host = tools.HallOfFame(maxsize), tools.HallOfFame(maxsize)
+    for gen in range(4):
+        n = 3000
+        genes = rng.integers(0, 4, size=(n, 6)).astype(np.float64)
+        genes[rng.integers(0, n, 300)] = genes[rng.integers(0, n, 300)]  # duplicates
+        wv = np.stack([genes.sum(1) // 2 + gen * 0.5] +
+                      ([-genes[:, 0]] if len(weights) > 1 else []), 1) * np.array(weights)
+        pop = _dp().from_numpy(genes, weights=weights, gtype="f64", wvalues=wv,
+                               valid=np.ones(n))
+        hof_dev.update(pop)
+        hof_host.update(pop.to_individuals())
+        assert [list(h) for h in hof_dev] == [list(h) for h in hof_host]
+        assert [h.fitness.wvalues for h in hof_dev] == [h.fitness.wvalues for h in hof_host]
+
+
+@pytest.mark.parametrize("comma", [False, True])
+def test_mu_lambda_drivers_replay_in_oracle(gpu, comma):
+    """eaMuCommaLambda / eaMuPlusLambda (algorithms.py:248-437) with selBest:
+    one generation in dump mode replayed through the oracle's varOr,
+    evaluation and selBest over offspring (comma) or parents + offspring."""
+    from deap_amd import algorithms, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim, mu, lam = 300, 40, 300, 500
+    stream = RandomStream(5)
+    pop = tools.initPopulation(n=n, dim=dim, low=-2, high=2, gtype="f64", weights=(-1.0,),
+                               stream=stream)
+    benchmarks.sphere(pop)
+    g0, wv0, ok0 = pop.to_numpy()
+    tb = _toolbox("blend", "gaussian", 0.1, 0.5, evaluate="sphere")
+    tb.register("select", tools.selBest)
+    decs = []
+    drv = algorithms.eaMuCommaLambda if comma else algorithms.eaMuPlusLambda
+    pop, log = drv(pop, tb, mu, lam, 0.5, 0.3, 1, verbose=False, decisions=decs, mode="dump",
+                   stream=stream)
+    dn = decs[0].numpy()
+    dec = {"varor_op": dn["varor_op"], "varor_idx": dn["varor_idx"], "blend_u": dn["blend_u"],
+           "mut_mask": ops.unpack_mask(dn["mut_mask"], dim), "gauss": dn["gauss"]}
+    og, owv, ook = ops.var_or(g0, wv0, ok0, lam, 0.5, 0.3, "blend", "gaussian", dec)
+    inv = ~ook
+    for i in np.nonzero(inv)[0]:
+        owv[i] = -ops.sphere(og[i].tolist())[0]
+    assert log.select("nevals")[1] == int(inv.sum())
+    pool_g = og if comma else np.concatenate([g0, og])
+    pool_w = owv if comma else np.concatenate([wv0, owv])
+    want = ops.sel_best(pool_w, mu)
+    g1, wv1, _ = pop.to_numpy()
+    assert np.array_equal(g1, pool_g[want])
+    assert _rel_close(wv1, pool_w[want], 1e-12)
+
+
+def test_checkpoint_resume_is_bit_exact(gpu, tmp_path):
+    """Checkpoint after 2 of 4 eaSimple generations, reload, finish: the same
+    population, hall of fame and logbook as the uninterrupted run
+    (doc/tutorials/advanced/checkpoint.rst:21-65 pattern, no pickle)."""
+    from deap_amd import algorithms, checkpoint, tools
+    from deap_amd.ops import RandomStream
+
+    def start():
+        stream = RandomStream(42, island=2)
+        pop = tools.initPopulation(n=1001, dim=300, low=-5.12, high=5.12, gtype="f64",
+                                   weights=(-1.0,), stream=stream)
+        return pop, stream
+
+    tb = _toolbox("blend", "gaussian", 0.05, 0.5, evaluate="rastrigin")
+    pop, stream = start()
+    hof = tools.HallOfFame(7)
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 4, halloffame=hof, verbose=False,
+                                   stream=stream)
+    full = pop.to_numpy()
+
+    pop2, stream2 = start()
+    hof2 = tools.HallOfFame(7)
+    pop2, log2 = algorithms.eaSimple(pop2, tb, 0.5, 0.2, 2, halloffame=hof2, verbose=False,
+                                     stream=stream2)
+    path = str(tmp_path / "ck.npz")
+    checkpoint.save(path, pop2, stream2, generation=2, halloffame=hof2, logbook=log2)
+    del pop2, stream2, hof2
+    ck = checkpoint.load(path)
+    assert ck["generation"] == 2
+    pop3, log3 = algorithms.eaSimple(ck["population"], tb, 0.5, 0.2, 2,
+                                     halloffame=ck["halloffame"], verbose=False,
+                                     stream=ck["stream"])
+    resumed = pop3.to_numpy()
+    for a, b in zip(full, resumed):
+        assert np.array_equal(a, b)
+    assert [list(h) for h in hof] == [list(h) for h in ck["halloffame"]]
+    assert log.select("nevals")[1:3] == ck["logbook"].select("nevals")[1:3]
+    assert log.select("nevals")[3:] == log3.select("nevals")[1:]
