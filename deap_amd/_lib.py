@@ -94,6 +94,8 @@ SIGNATURES = {
                                             _PP(_i64), _PP(_i32)]),
     "dm_crowding_dist": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _p, _p, _i32, _p]),
     "dm_sel_nsga2": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _i64, _p, _p]),
+    "dm_sel_tournament_dcd": (ctypes.c_int, [_p, _PP(DevicePop), _p, _i64, Rng, _i32, _p, _p, _p,
+                                             _p]),
     "dm_pack_rows": (ctypes.c_int, [_p, _PP(DevicePop), _p, _i64, _p]),
     "dm_pack_bytes": (_i64, [_PP(DevicePop), _i64]),
     "dm_mig_place": (ctypes.c_int, [_p, _PP(DevicePop), _p, _p, _i64, _p]),

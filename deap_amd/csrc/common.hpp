@@ -101,6 +101,8 @@ enum Stage : uint32_t {
     ST_FLIP = 7,    // packed-bit geometric skips: sub = (word << 8) | call
     ST_VAROR = 8,   // varOr op choice + indices: item = child
     ST_INIT = 9,    // initial population
+    ST_DCD = 10,    // selTournamentDCD: permutation keys (item = i, sub = 0/1),
+                    // tie coins (item = tournament slot, sub = 2)
 };
 
 struct u32x4 {

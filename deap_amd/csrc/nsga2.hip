@@ -747,3 +747,125 @@ extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weight
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
+
+// ---------------------------------------------------------------------------
+// selTournamentDCD (emo.py:145-195)
+// ---------------------------------------------------------------------------
+namespace dm {
+
+// Fitness.dominates on wvalues (base.py:209-224): an objective with a NaN side
+// compares equal.
+__device__ __forceinline__ bool dominates_wv(const double* a, const double* b, int m) {
+    bool not_equal = false;
+    for (int o = 0; o < m; ++o) {
+        if (a[o] > b[o])
+            not_equal = true;
+        else if (a[o] < b[o])
+            return false;
+    }
+    return not_equal;
+}
+
+__global__ void dcd_keys_kernel(Rng rng, int64_t n, uint32_t which, uint64_t* keys,
+                                int32_t* vals) {
+    GRID_LOOP(i, n) {
+        const u32x4 w = rng(ST_DCD, (uint32_t)i, which);
+        keys[i] = ((uint64_t)w.x << 32) | w.y;
+        vals[i] = (int32_t)i;
+    }
+}
+
+// Slot j of the output: tournament j%4 of group j/4 — (P1[i], P1[i+1]),
+// (P1[i+2], P1[i+3]), (P2[i], P2[i+1]), (P2[i+2], P2[i+3]) with i = 4*(j/4)
+// (emo.py:188-192); dominance, then the larger crowding distance, then
+// random() <= 0.5 keeps the first (emo.py:170-183).
+__global__ void dcd_kernel(const double* wv, int m, const double* crowd, const int32_t* p1,
+                           const int32_t* p2, int64_t k4, Rng rng, int mode, uint8_t* coin,
+                           int32_t* out) {
+    GRID_LOOP(j, k4) {
+        const int64_t i = (j >> 2) << 2;
+        const int r = (int)(j & 3);
+        const int32_t* P = r < 2 ? p1 : p2;
+        const int64_t o = i + 2 * (r & 1);
+        const int32_t a = P[o], b = P[o + 1];
+        int32_t res;
+        if (dominates_wv(wv + (int64_t)a * m, wv + (int64_t)b * m, m)) {
+            res = a;
+        } else if (dominates_wv(wv + (int64_t)b * m, wv + (int64_t)a * m, m)) {
+            res = b;
+        } else if (crowd[a] < crowd[b]) {
+            res = b;
+        } else if (crowd[a] > crowd[b]) {
+            res = a;
+        } else {
+            bool first;
+            if (mode == DM_RNG_INJECT) {
+                first = coin[j] != 0;
+            } else {
+                const u32x4 w = rng(ST_DCD, (uint32_t)j, 2u);
+                first = u01_53(w.x, w.y) <= 0.5;
+                if (mode == DM_RNG_DUMP) coin[j] = first ? 1 : 0;
+            }
+            res = first ? a : b;
+        }
+        out[j] = res;
+    }
+}
+
+}  // namespace dm
+
+extern "C" int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const double* crowd,
+                                     int64_t k, dm_rng rng, int32_t mode, int32_t* perm1,
+                                     int32_t* perm2, uint8_t* coin, int32_t* out_idx) {
+    using namespace dm;
+    DM_CHECK_ARG(ctx && crowd && out_idx, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    const int64_t n = pop->n;
+    DM_CHECK_ARG(k >= 0, "bad k");
+    DM_CHECK_ARG(n < (1ll << 31), "population too large");
+    if (k > n) {
+        set_error("selTournamentDCD: k must be less than or equal to individuals length");
+        return DM_ERR_INVALID;
+    }
+    if (k == n && k % 4 != 0) {
+        set_error("selTournamentDCD: k must be divisible by four if k == len(individuals)");
+        return DM_ERR_INVALID;
+    }
+    const int64_t k4 = (k + 3) / 4 * 4;
+    if (k4 > n) {  // individuals_1[i+3] past the end (emo.py:188-192)
+        set_error("list index out of range");
+        return DM_ERR_INDEX;
+    }
+    if (mode == DM_RNG_INJECT) {
+        DM_CHECK_ARG(perm1 && perm2 && coin, "decisions perm1 / perm2 / coin required");
+    } else if (mode == DM_RNG_DUMP) {
+        DM_CHECK_ARG(perm1 && perm2 && coin, "dump buffers perm1 / perm2 / coin required");
+    }
+    if (k == 0) return DM_OK;
+    hipStream_t s = ctx->stream;
+    if (mode != DM_RNG_INJECT) {
+        // random.sample(individuals, len(individuals)): permutations from
+        // sorting Philox keys (stable radix sort, ties by index)
+        const size_t kb = align_up((size_t)n * 8, 256), vb = align_up((size_t)n * 4, 256);
+        char* w = (char*)scratch(ctx, 2 * kb + 3 * vb + radix_sort_temp_bytes(n));
+        if (!w) return DM_ERR_NOMEM;
+        uint64_t* keys = (uint64_t*)w;
+        uint64_t* ktmp = (uint64_t*)(w + kb);
+        int32_t* vtmp = (int32_t*)(w + 2 * kb);
+        int32_t* own1 = (int32_t*)(w + 2 * kb + vb);
+        int32_t* own2 = (int32_t*)(w + 2 * kb + 2 * vb);
+        void* rtemp = w + 2 * kb + 3 * vb;
+        if (!perm1) perm1 = own1;
+        if (!perm2) perm2 = own2;
+        int32_t* perms[2] = {perm1, perm2};
+        for (uint32_t q = 0; q < 2; ++q) {
+            dcd_keys_kernel<<<g1(n), 256, 0, s>>>(Rng(rng), n, q, keys, perms[q]);
+            if ((rc = radix_sort_pairs(s, keys, perms[q], ktmp, vtmp, n, 0, 64, rtemp))) return rc;
+        }
+    }
+    dcd_kernel<<<g1(k4), 256, 0, s>>>(pop->wvalues, pop->nobj, crowd, perm1, perm2, k4, Rng(rng),
+                                      mode, coin, out_idx);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}

@@ -2,12 +2,13 @@
 
 Crossover: ``cxTwoPoint``, ``cxBlend``; mutation: ``mutFlipBit``,
 ``mutGaussian``; selection: ``selTournament``, ``selRandom``, ``selBest``,
-``selWorst``, ``selNSGA2``, ``sortNondominated`` (``emo.assignCrowdingDist``);
+``selWorst``, ``selNSGA2``, ``selTournamentDCD``, ``sortNondominated``
+(``emo.assignCrowdingDist``);
 migration: ``migRing``; bookkeeping: ``Statistics``, ``MultiStatistics``,
 ``Logbook``, ``HallOfFame``; initialisation: ``initPopulation``.
 """
 from .crossover import cxBlend, cxTwoPoint
-from .emo import selNSGA2, sortNondominated
+from .emo import selNSGA2, selTournamentDCD, sortNondominated
 from . import emo
 from .init import initPopulation
 from .migration import migRing
@@ -16,5 +17,5 @@ from .selection import selBest, selRandom, selTournament, selWorst
 from .support import HallOfFame, Logbook, MultiStatistics, Statistics
 
 __all__ = ["cxTwoPoint", "cxBlend", "mutFlipBit", "mutGaussian", "selTournament", "selRandom",
-           "selBest", "selWorst", "selNSGA2", "sortNondominated", "migRing", "Statistics",
+           "selBest", "selWorst", "selNSGA2", "selTournamentDCD", "sortNondominated", "migRing", "Statistics",
            "MultiStatistics", "Logbook", "HallOfFame", "initPopulation", "emo"]

@@ -120,8 +120,45 @@ class _SelNSGA2(DeviceOperator):
         return out[: min(k, n)]
 
 
+class _SelTournamentDCD(DeviceOperator):
+    kind = "select"
+
+    def __call__(self, individuals, k, *, stream=None, mode=None, decisions=None, **_):
+        """Returns 4*ceil(k/4) indices (the reference appends four per step of
+        ``range(0, k, 4)``).  Needs ``individuals.crowding_dist`` (set by
+        selNSGA2 / assignCrowdingDist) as the reference needs
+        ``fitness.crowding_dist``.  ``decisions``: dict with int32 device
+        tensors ``perm1``, ``perm2`` [n] and uint8 ``coin`` [4*ceil(k/4)],
+        read in mode "inject", filled in mode "dump"."""
+        from ..ops import default_stream, mode_code
+        _check(individuals)
+        torch = _torch()
+        if individuals.crowding_dist is None:
+            raise AttributeError("'Fitness' object has no attribute 'crowding_dist'")
+        stream = stream or default_stream()
+        n, k = len(individuals), int(k)
+        k4 = (k + 3) // 4 * 4
+        dev = individuals.device
+        out = torch.empty((max(k4, 1),), dtype=torch.int32, device=dev)
+        code = mode_code(mode or "native")
+        p1 = p2 = coin = None
+        if code != _lib.DM_RNG_NATIVE:
+            if code == _lib.DM_RNG_DUMP:
+                decisions["perm1"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
+                decisions["perm2"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
+                decisions["coin"] = torch.zeros((max(k4, 1),), dtype=torch.uint8, device=dev)
+            p1, p2, coin = decisions["perm1"], decisions["perm2"], decisions["coin"]
+        ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+        ctx = individuals.ctx.bind()
+        _lib.call("dm_sel_tournament_dcd", ctx, ctypes.byref(individuals.c_pop()),
+                  ctypes.c_void_p(individuals.crowding_dist.data_ptr()), k, stream.next(), code,
+                  ptr(p1), ptr(p2), ptr(coin), ctypes.c_void_p(out.data_ptr()))
+        return out[:k4]
+
+
 sortNondominated = _SortNondominated("sortNondominated", "deap/tools/emo.py:53-117")
 assignCrowdingDist = _CrowdingDist("assignCrowdingDist", "deap/tools/emo.py:119-143")
 selNSGA2 = _SelNSGA2("selNSGA2", "deap/tools/emo.py:15-50")
+selTournamentDCD = _SelTournamentDCD("selTournamentDCD", "deap/tools/emo.py:145-195")
 
-__all__ = ["selNSGA2", "sortNondominated"]  # assignCrowdingDist is not exported (emo.py:842-843)
+__all__ = ["selNSGA2", "sortNondominated", "selTournamentDCD"]  # assignCrowdingDist is not exported (emo.py:842-843)

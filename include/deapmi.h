@@ -234,6 +234,20 @@ int dm_crowding_dist(dm_ctx* ctx, const dm_pop* pop, const double* weights,
 int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                  int64_t k, int32_t* out_idx, double* crowd);
 
+/* selTournamentDCD (emo.py:145-195): out_idx[4*ceil(k/4)] — for every group
+ * of four slots, tournaments (P1[i],P1[i+1]), (P1[i+2],P1[i+3]),
+ * (P2[i],P2[i+1]), (P2[i+2],P2[i+3]) where P1, P2 are the two
+ * random.sample(individuals, n) permutations; a tournament keeps the
+ * dominating individual, else the larger crowd[] (device [n],
+ * fitness.crowding_dist), else the first one iff random() <= 0.5.
+ * perm1/perm2 [n] and coin [4*ceil(k/4)] (1 = first kept on a tie) are read
+ * (INJECT), written (DUMP) or optional scratch (NATIVE).  k > n or
+ * (k == n, k % 4 != 0): DM_ERR_INVALID (the reference's ValueError);
+ * 4*ceil(k/4) > n: DM_ERR_INDEX (its IndexError). */
+int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const double* crowd, int64_t k,
+                          dm_rng rng, int32_t mode, int32_t* perm1, int32_t* perm2,
+                          uint8_t* coin, int32_t* out_idx);
+
 /* ---- island migration (deap/tools/migration.py:4-51) --------------------- */
 /* Pack rows idx[0..k) of pop into a contiguous emigrant block:
  * [k][stride] genomes, then [k][nobj] wvalues, then [k] valid (padded to 8 B),

@@ -403,6 +403,37 @@ def sel_nsga2(wvalues, weights, k):
 # ---------------------------------------------------------------------------
 # migRing (deap/tools/migration.py:4-51) on demes of (genes, wvalues, valid)
 # ---------------------------------------------------------------------------
+def sel_tournament_dcd(wvalues, crowd, k, perm1, perm2, coin):
+    """selTournamentDCD (emo.py:145-195) over row indices with the two
+    random.sample permutations and, per output slot, the random() <= 0.5 coin
+    (1 = keep the first) used only when neither dominates and the crowding
+    distances are equal."""
+    n = len(wvalues)
+    if k > n:
+        raise ValueError("selTournamentDCD: k must be less than or equal to individuals length")
+    if k == n and k % 4 != 0:
+        raise ValueError("selTournamentDCD: k must be divisible by four if k == len(individuals)")
+
+    def tourn(a, b, j):
+        if dominates(wvalues[a], wvalues[b]):
+            return a
+        if dominates(wvalues[b], wvalues[a]):
+            return b
+        if crowd[a] < crowd[b]:
+            return b
+        if crowd[a] > crowd[b]:
+            return a
+        return a if coin[j] else b
+
+    chosen = []
+    for i in range(0, k, 4):
+        chosen.append(tourn(perm1[i], perm1[i + 1], len(chosen)))
+        chosen.append(tourn(perm1[i + 2], perm1[i + 3], len(chosen)))
+        chosen.append(tourn(perm2[i], perm2[i + 1], len(chosen)))
+        chosen.append(tourn(perm2[i + 2], perm2[i + 3], len(chosen)))
+    return chosen
+
+
 def mig_ring(demes, emigrant_idx, immigrant_idx=None, migarray=None):
     """demes: list of dicts {genes, wvalues, valid} (modified in place).
     emigrant_idx[d]: selection(pop_d, k) row indices; immigrant_idx[d]:

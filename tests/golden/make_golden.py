@@ -422,6 +422,43 @@ def gen_nsga2(D, rng):
     return out
 
 
+def gen_dcd(D, rng):
+    """selTournamentDCD (emo.py:145-195): two random.sample permutations and a
+    random() coin for each tied tournament, fed in DEAP's call order."""
+    tools = D["deap.tools"]
+    out = {}
+    cases = [(64, 2, 64), (100, 3, 37), (40, 2, 40), (200, 3, 120), (33, 2, 30)]
+    for j, (n, m, k) in enumerate(cases):
+        weights = tuple([-1.0, 1.0, -1.0][:m])
+        Ind = make_types(D, "d", weights)
+        vals = rng.integers(0, 4, size=(n, m)).astype(np.float64)  # many mutual non-dominance
+        wv = vals * np.array(weights)
+        crowd = rng.choice([0.0, 0.25, 0.5, np.inf], size=n)      # many crowding ties
+        pop = to_inds(Ind, rng.uniform(0, 1, size=(n, 2)), wv)
+        for ind, c in zip(pop, crowd):
+            ind.fitness.crowding_dist = float(c)
+        ident = {id(p): i for i, p in enumerate(pop)}
+        p1, p2 = rng.permutation(n), rng.permutation(n)
+        k4 = (k + 3) // 4 * 4
+        coin = rng.integers(0, 2, size=k4).astype(np.uint8)
+        floats = []
+        for i in range(0, k, 4):
+            for slot, (a, b) in enumerate([(p1[i], p1[i + 1]), (p1[i + 2], p1[i + 3]),
+                                           (p2[i], p2[i + 1]), (p2[i + 2], p2[i + 3])]):
+                fa, fb = pop[a].fitness, pop[b].fitness
+                if not fa.dominates(fb) and not fb.dominates(fa) and \
+                        fa.crowding_dist == fb.crowding_dist:
+                    floats.append(0.25 if coin[i + slot] else 0.75)
+        with Replay(floats=floats, samples=[list(p1), list(p2)]):
+            chosen = tools.selTournamentDCD(pop, k)
+        key = "dcd%d_" % j
+        out.update({key + "wv": wv, key + "crowd": crowd, key + "k": np.array(k),
+                    key + "perm1": p1.astype(np.int32), key + "perm2": p2.astype(np.int32),
+                    key + "coin": coin,
+                    key + "chosen": np.array([ident[id(c)] for c in chosen], np.int32)})
+    return out
+
+
 def gen_migration(D, rng):
     tools = D["deap.tools"]
     out = {}
@@ -540,6 +577,10 @@ def gen_c1_trajectory(D):
 
 def main():
     D = load_reference()
+    if sys.argv[1:] == ["dcd"]:  # regenerate one fixture without touching the rest
+        np.savez_compressed(os.path.join(HERE, "dcd.npz"),
+                            **gen_dcd(D, np.random.default_rng(77)))
+        return
     rng = np.random.default_rng(20260415)
     os.makedirs(HERE, exist_ok=True)
     np.savez_compressed(os.path.join(HERE, "eval.npz"), **gen_eval(D, rng))
@@ -550,6 +591,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "nsga2.npz"), **gen_nsga2(D, rng))
     np.savez_compressed(os.path.join(HERE, "migration.npz"), **gen_migration(D, rng))
     np.savez_compressed(os.path.join(HERE, "c1_trajectory.npz"), **gen_c1_trajectory(D))
+    np.savez_compressed(os.path.join(HERE, "dcd.npz"), **gen_dcd(D, np.random.default_rng(77)))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

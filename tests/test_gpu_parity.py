@@ -558,3 +558,62 @@ def test_checkpoint_resume_is_bit_exact(gpu, tmp_path):
     assert [list(h) for h in hof] == [list(h) for h in ck["halloffame"]]
     assert log.select("nevals")[1:3] == ck["logbook"].select("nevals")[1:3]
     assert log.select("nevals")[3:] == log3.select("nevals")[1:]
+
+
+def _dcd_pop(wv, crowd):
+    import torch
+    n = len(wv)
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0,) * wv.shape[1], gtype="f64",
+                           wvalues=wv, valid=np.ones(n))
+    pop.crowding_dist = torch.tensor(crowd, dtype=torch.float64, device=pop.device)
+    return pop
+
+
+def test_sel_tournament_dcd_matches_reference(gpu):
+    """selTournamentDCD (emo.py:145-195), injected permutations and tie coins
+    vs the reference's choices (golden)."""
+    import torch
+    from deap_amd import tools
+    d = golden("dcd.npz")
+    for j in range(5):
+        key = "dcd%d_" % j
+        pop = _dcd_pop(d[key + "wv"], d[key + "crowd"])
+        dec = {name: torch.tensor(d[key + name], device=pop.device)
+               for name in ("perm1", "perm2", "coin")}
+        got = tools.selTournamentDCD(pop, int(d[key + "k"]), mode="inject", decisions=dec)
+        assert got.cpu().numpy().tolist() == d[key + "chosen"].tolist(), j
+
+
+def test_sel_tournament_dcd_native_replays_in_oracle(gpu):
+    from deap_amd import tools
+    from deap_amd.ops import RandomStream
+    rng = np.random.default_rng(3)
+    n, k = 50000, 30001
+    wv = rng.integers(0, 6, size=(n, 2)).astype(np.float64)
+    crowd = rng.choice([0.0, 1.0, np.inf], size=n)
+    pop = _dcd_pop(wv, crowd)
+    dec = {}
+    got = tools.selTournamentDCD(pop, k, mode="dump", decisions=dec,
+                                 stream=RandomStream(9)).cpu().numpy()
+    p1, p2 = dec["perm1"].cpu().numpy(), dec["perm2"].cpu().numpy()
+    assert np.array_equal(np.sort(p1), np.arange(n)) and np.array_equal(np.sort(p2), np.arange(n))
+    assert not np.array_equal(p1, p2)
+    want = ops.sel_tournament_dcd(wv, crowd, k, p1, p2, dec["coin"].cpu().numpy())
+    assert got.tolist() == want
+    assert len(got) == 30004
+    # native mode draws the same stream as dump mode
+    again = tools.selTournamentDCD(pop, k, stream=RandomStream(9)).cpu().numpy()
+    assert np.array_equal(again, got)
+    # each individual appears at most twice per permutation pass (4 per call)
+    assert np.bincount(got, minlength=n).max() <= 4
+
+
+def test_sel_tournament_dcd_errors(gpu):
+    from deap_amd import tools
+    pop = _dcd_pop(np.zeros((10, 2)), np.zeros(10))
+    with pytest.raises(ValueError):
+        tools.selTournamentDCD(pop, 11)
+    with pytest.raises(ValueError):
+        tools.selTournamentDCD(pop, 10)
+    with pytest.raises(IndexError):
+        tools.selTournamentDCD(pop, 9)   # 4*ceil(9/4) = 12 > 10: the reference's IndexError

@@ -159,3 +159,12 @@ def test_c1_trajectory_replays_in_oracle():
     assert np.array_equal(genes, d["c1_final"])
     assert np.array_equal(wv, d["c1_final_wv"])
     assert nevals == d["c1_nevals"].tolist()
+
+
+def test_sel_tournament_dcd_matches_reference():
+    d = golden("dcd.npz")
+    for j in range(5):
+        key = "dcd%d_" % j
+        got = ops.sel_tournament_dcd(d[key + "wv"], d[key + "crowd"], int(d[key + "k"]),
+                                     d[key + "perm1"], d[key + "perm2"], d[key + "coin"])
+        assert got == d[key + "chosen"].tolist(), j
