@@ -66,6 +66,12 @@ class Decisions(ctypes.Structure):
                 ("varor_idx", _p)]
 
 
+class BoundedVar(ctypes.Structure):
+    """struct dm_bounded_var"""
+    _fields_ = [("cx", _i32), ("mut", _i32), ("cxpb", _f64), ("eta_cx", _f64), ("eta_mut", _f64),
+                ("indpb", _f64), ("low", _f64), ("up", _f64), ("low_vec", _p), ("up_vec", _p)]
+
+
 # name -> (restype, argtypes); mirrors include/deapmi.h one to one.
 _PP = ctypes.POINTER
 SIGNATURES = {
@@ -96,6 +102,8 @@ SIGNATURES = {
     "dm_sel_nsga2": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _i64, _p, _p]),
     "dm_sel_tournament_dcd": (ctypes.c_int, [_p, _PP(DevicePop), _p, _i64, Rng, _i32, _p, _p, _p,
                                              _p]),
+    "dm_vary_bounded": (ctypes.c_int, [_p, _PP(DevicePop), _p, _PP(DevicePop), _PP(BoundedVar),
+                                       Rng, _i32, _p, _p, _p]),
     "dm_pack_rows": (ctypes.c_int, [_p, _PP(DevicePop), _p, _i64, _p]),
     "dm_pack_bytes": (_i64, [_PP(DevicePop), _i64]),
     "dm_mig_place": (ctypes.c_int, [_p, _PP(DevicePop), _p, _p, _i64, _p]),

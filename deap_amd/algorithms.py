@@ -118,6 +118,36 @@ def varAnd(population, toolbox, cxpb, mutpb, *, decisions=None, mode=None, strea
     return _var_and(population, mate, mutate, cxpb, mutpb, decisions, mode, stream)
 
 
+def varBounded(population, toolbox, cxpb, index=None, *, decisions=None, mode=None,
+               stream=None):
+    """The variation body of DEAP's NSGA-II loop (``examples/ga/nsga2.py:96-105``;
+    also ``tests/test_algorithms.py:96-104``), one fused launch
+    (``dm_vary_bounded``)::
+
+        offspring = [toolbox.clone(ind) for ind in population[index]]
+        for ind1, ind2 in zip(offspring[::2], offspring[1::2]):
+            if random.random() <= cxpb:
+                toolbox.mate(ind1, ind2)
+            toolbox.mutate(ind1); toolbox.mutate(ind2)
+            del ind1.fitness.values, ind2.fitness.values
+
+    ``toolbox.mate`` must be ``cxSimulatedBinaryBounded`` and ``toolbox.mutate``
+    ``mutPolynomialBounded`` (same low/up).  ``index``: device int tensor of
+    selected rows (e.g. from ``selTournamentDCD``), default all rows.  Returns
+    the offspring population (fitness invalid except an odd last clone)."""
+    from .tools._bounded import vary_bounded
+    from .tools.crossover import cxSimulatedBinaryBounded
+    from .tools.mutation import mutPolynomialBounded
+    _check_pop(population)
+    mop, ma, mkw = resolve(toolbox.mate)
+    uop, ua, ukw = resolve(toolbox.mutate)
+    if mop is not cxSimulatedBinaryBounded or uop is not mutPolynomialBounded:
+        raise TypeError("varBounded needs mate=cxSimulatedBinaryBounded and "
+                        "mutate=mutPolynomialBounded, got %r / %r" % (mop, uop))
+    return vary_bounded(population, index, mop.params(ma, mkw), uop.params(ua, ukw), cxpb,
+                        decisions, mode, stream)
+
+
 def _selection_spec(toolbox):
     op, a, kw = resolve(toolbox.select)
     return op, a, kw
@@ -396,4 +426,4 @@ class _View(DevicePopulation):
         self.capacity = count
 
 
-__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda", "eaMuCommaLambda"]  # + GenerationStep, MuPlusLambdaStep
+__all__ = ["varAnd", "eaSimple", "varOr", "eaMuPlusLambda", "eaMuCommaLambda", "varBounded"]  # + GenerationStep, MuPlusLambdaStep

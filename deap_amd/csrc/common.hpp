@@ -103,6 +103,10 @@ enum Stage : uint32_t {
     ST_INIT = 9,    // initial population
     ST_DCD = 10,    // selTournamentDCD: permutation keys (item = i, sub = 0/1),
                     // tie coins (item = tournament slot, sub = 2)
+    ST_SBX_PAIR = 11,  // NSGA-II loop pair random() <= cxpb: item = pair
+    ST_SBX = 12,       // cxSimulatedBinaryBounded per gene: item = pair, sub = gene
+                       // (| 1 << 24 for the swap coin)
+    ST_POLY = 13,      // mutPolynomialBounded per gene: item = child, sub = gene
 };
 
 struct u32x4 {

@@ -45,7 +45,26 @@ class _Blend(_Crossover):
         return {"alpha": float(alpha)}
 
 
+class _SimulatedBinaryBounded(DeviceOperator):
+    """Batch form mates every pair (2i, 2i+1); inside ``varBounded`` it
+    parameterises the fused NSGA-II variation kernel (``dm_vary_bounded``)."""
+    kind = "mate"
+
+    def params(self, args, kwargs):
+        from ._bounded import sbx_params
+        return sbx_params(args, kwargs)
+
+    def __call__(self, population, *args, decisions=None, mode=None, stream=None, **kwargs):
+        from ._bounded import vary_bounded
+        # every pair is mated: the pair gate random() <= 1.0 always holds
+        return vary_bounded(population, None, self.params(args, kwargs), None, 1.0,
+                            decisions, mode, stream)
+
+
 cxTwoPoint = _TwoPoint("cxTwoPoint", "deap/tools/crossover.py:37-60")
 cxBlend = _Blend("cxBlend", "deap/tools/crossover.py:241-260")
 
-__all__ = ["cxTwoPoint", "cxBlend"]
+cxSimulatedBinaryBounded = _SimulatedBinaryBounded("cxSimulatedBinaryBounded",
+                                                   "deap/tools/crossover.py:291-360")
+
+__all__ = ["cxTwoPoint", "cxBlend", "cxSimulatedBinaryBounded"]

@@ -74,7 +74,24 @@ class _Gaussian(_Mutation):
             setattr(var, k, v)
 
 
+class _PolynomialBounded(DeviceOperator):
+    """Batch form mutates every individual; inside ``varBounded`` it
+    parameterises the fused NSGA-II variation kernel (``dm_vary_bounded``)."""
+    kind = "mutate"
+
+    def params(self, args, kwargs, population=None):
+        from ._bounded import poly_params
+        return poly_params(args, kwargs)
+
+    def __call__(self, population, *args, decisions=None, mode=None, stream=None, **kwargs):
+        from ._bounded import vary_bounded
+        return vary_bounded(population, None, None, self.params(args, kwargs), 0.0,
+                            decisions, mode, stream)
+
+
 mutFlipBit = _FlipBit("mutFlipBit", "deap/tools/mutation.py:124-142")
 mutGaussian = _Gaussian("mutGaussian", "deap/tools/mutation.py:17-48")
 
-__all__ = ["mutFlipBit", "mutGaussian"]
+mutPolynomialBounded = _PolynomialBounded("mutPolynomialBounded", "deap/tools/mutation.py:51-95")
+
+__all__ = ["mutFlipBit", "mutGaussian", "mutPolynomialBounded"]

@@ -248,6 +248,40 @@ int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const double* crowd, i
                           dm_rng rng, int32_t mode, int32_t* perm1, int32_t* perm2,
                           uint8_t* coin, int32_t* out_idx);
 
+/* ---- bounded real-valued variation (NSGA-II example loop) ---------------- */
+/* Parameters of cxSimulatedBinaryBounded(eta, low, up) (crossover.py:291-360)
+ * and mutPolynomialBounded(eta, low, up, indpb) (mutation.py:51-95).  low/up
+ * are the scalars unless low_vec/up_vec (device [dim]) are given. */
+typedef struct dm_bounded_var {
+    int32_t cx;        /* 1 = apply cxSimulatedBinaryBounded to pairs          */
+    int32_t mut;       /* 1 = apply mutPolynomialBounded to both children      */
+    double cxpb;       /* pair crossed iff random() <= cxpb (nsga2.py:100)     */
+    double eta_cx;
+    double eta_mut;
+    double indpb;
+    double low, up;
+    const double* low_vec;
+    const double* up_vec;
+} dm_bounded_var;
+
+/* The variation body of the NSGA-II loop (examples/ga/nsga2.py:96-105):
+ *   offspring = [clone(pop[i]) for i in idx]          (idx NULL: identity)
+ *   for ind1, ind2 in zip(offspring[::2], offspring[1::2]):
+ *       if random() <= cxpb: cxSimulatedBinaryBounded(ind1, ind2)   (if cx)
+ *       mutPolynomialBounded(ind1); mutPolynomialBounded(ind2)      (if mut)
+ *       del ind1.fitness.values, ind2.fitness.values
+ * children->n = k offspring; an odd last child is a plain clone (fitness
+ * kept) — except with cx == 0 (mutation only, the batch form of
+ * mutPolynomialBounded), which mutates every child.  F64 genomes only.  Decisions (INJECT read / DUMP write / NATIVE
+ * unused, may be NULL): cx_u[k/2] the pair random(); sbx_u[k/2][dim][3] the
+ * per-gene (gate, rand, swap) random()s of SBX; mut_u[2*(k/2)][dim][2] the
+ * per-gene (gate, rand) random()s of the polynomial mutation ([k] rows when
+ * cx == 0).  A value is
+ * only consumed where the reference would draw it. */
+int dm_vary_bounded(dm_ctx* ctx, const dm_pop* parents, const int32_t* idx, dm_pop* children,
+                    const dm_bounded_var* var, dm_rng rng, int32_t mode, double* cx_u,
+                    double* sbx_u, double* mut_u);
+
 /* ---- island migration (deap/tools/migration.py:4-51) --------------------- */
 /* Pack rows idx[0..k) of pop into a contiguous emigrant block:
  * [k][stride] genomes, then [k][nobj] wvalues, then [k] valid (padded to 8 B),

@@ -224,6 +224,83 @@ def mut_gaussian(x, mask, gauss, store):
         x[i] = store(float(x[i]) + float(gauss[i]))
 
 
+def _sbx_beta_q(beta, rand, eta):
+    """beta_q of cxSimulatedBinaryBounded                 (crossover.py:333-338)"""
+    alpha = 2.0 - beta ** -(eta + 1)
+    if rand <= 1.0 / alpha:
+        return (rand * alpha) ** (1.0 / (eta + 1))
+    return (1.0 / (2.0 - rand * alpha)) ** (1.0 / (eta + 1))
+
+
+def cx_sbx_bounded(a, b, u, eta, low, up):
+    """cxSimulatedBinaryBounded with per-gene (gate, rand, swap) random()s
+    u[dim][3], each used only where the reference draws it (crossover.py:324-358).
+    low / up: per-gene sequences."""
+    for i in range(min(len(a), len(b))):
+        gate, rand, swap = (float(v) for v in u[i])
+        xl, xu = float(low[i]), float(up[i])
+        if gate <= 0.5:
+            if abs(float(a[i]) - float(b[i])) > 1e-14:
+                x1 = min(float(a[i]), float(b[i]))
+                x2 = max(float(a[i]), float(b[i]))
+                c1 = 0.5 * (x1 + x2 - _sbx_beta_q(1.0 + (2.0 * (x1 - xl) / (x2 - x1)), rand, eta)
+                            * (x2 - x1))
+                c2 = 0.5 * (x1 + x2 + _sbx_beta_q(1.0 + (2.0 * (xu - x2) / (x2 - x1)), rand, eta)
+                            * (x2 - x1))
+                c1 = min(max(c1, xl), xu)
+                c2 = min(max(c2, xl), xu)
+                if swap <= 0.5:
+                    a[i], b[i] = c2, c1
+                else:
+                    a[i], b[i] = c1, c2
+
+
+def mut_poly_bounded(x, u, eta, low, up, indpb):
+    """mutPolynomialBounded with per-gene (gate, rand) random()s u[dim][2]
+    (mutation.py:75-94)."""
+    for i in range(len(x)):
+        gate, rand = float(u[i][0]), float(u[i][1])
+        if gate <= indpb:
+            xi, xl, xu = float(x[i]), float(low[i]), float(up[i])
+            delta_1 = (xi - xl) / (xu - xl)
+            delta_2 = (xu - xi) / (xu - xl)
+            mut_pow = 1.0 / (eta + 1.)
+            if rand < 0.5:
+                xy = 1.0 - delta_1
+                val = 2.0 * rand + (1.0 - 2.0 * rand) * xy ** (eta + 1)
+                delta_q = val ** mut_pow - 1.0
+            else:
+                xy = 1.0 - delta_2
+                val = 2.0 * (1.0 - rand) + 2.0 * (rand - 0.5) * xy ** (eta + 1)
+                delta_q = 1.0 - val ** mut_pow
+            xi = xi + delta_q * (xu - xl)
+            x[i] = min(max(xi, xl), xu)
+
+
+def vary_bounded(genes, wvalues, valid, idx, cxpb, dec, sbx=None, poly=None):
+    """The NSGA-II loop body (examples/ga/nsga2.py:96-105) replaying decisions
+    cx_u[k//2], sbx_u[k//2][dim][3], mut_u[rows][dim][2] (rows = 2*(k//2) with
+    SBX, k without).  sbx = (eta, low, up), poly = (eta, low, up, indpb) with
+    per-gene low/up.  Returns (genes, wvalues, valid) of the k offspring."""
+    idx = np.arange(len(genes)) if idx is None else np.asarray(idx)
+    g = genes[idx].astype(np.float64).copy()
+    wv = wvalues[idx].copy()
+    ok = valid[idx].copy()
+    k = len(idx)
+    for p in range(k // 2):
+        a, b = g[2 * p], g[2 * p + 1]
+        if sbx is not None and float(dec["cx_u"][p]) <= cxpb:
+            cx_sbx_bounded(a, b, dec["sbx_u"][p], *sbx)
+        if poly is not None:
+            mut_poly_bounded(a, dec["mut_u"][2 * p], *poly)
+            mut_poly_bounded(b, dec["mut_u"][2 * p + 1], *poly)
+        ok[2 * p] = ok[2 * p + 1] = False
+    if k % 2 and sbx is None and poly is not None:
+        mut_poly_bounded(g[k - 1], dec["mut_u"][k - 1], *poly)
+        ok[k - 1] = False
+    return g, wv, ok
+
+
 def _store_for(genes):
     if genes.dtype == np.float32:
         return lambda v: np.float32(v)  # array('f'): round to nearest on store

@@ -459,6 +459,77 @@ def gen_dcd(D, rng):
     return out
 
 
+def gen_sbx(D, rng):
+    """The NSGA-II variation loop (examples/ga/nsga2.py:96-105) with
+    cxSimulatedBinaryBounded (crossover.py:291-360) and mutPolynomialBounded
+    (mutation.py:51-95): position-indexed random() decisions cx_u / sbx_u /
+    mut_u are fed to DEAP in its consumption order."""
+    tools = D["deap.tools"]
+    base = D["deap.base"]
+    out = {}
+    cases = [  # n, dim, k, cxpb, eta_cx, eta_mut, indpb, vector bounds
+        (40, 30, 40, 0.9, 20.0, 20.0, 1.0 / 30, False),
+        (33, 12, 31, 0.9, 20.0, 20.0, 0.25, True),
+        (24, 7, 24, 0.6, 0.5, 2.0, 0.5, False),
+        (50, 5, 18, 1.0, 100.0, 100.0, 1.0, True),
+    ]
+    for j, (n, dim, k, cxpb, eta_c, eta_m, indpb, vec) in enumerate(cases):
+        if vec:
+            low = [float(v) for v in rng.uniform(-3, 0, size=dim)]
+            up = [float(v) for v in rng.uniform(0.5, 3, size=dim)]
+        else:
+            low, up = 0.0, 1.0
+        lo = np.broadcast_to(np.asarray(low, np.float64), (dim,))
+        hi = np.broadcast_to(np.asarray(up, np.float64), (dim,))
+        genes = lo + (hi - lo) * rng.uniform(0, 1, size=(n, dim))
+        # duplicated genes (|x1 - x2| <= 1e-14 branch) and genes on the bounds
+        genes[1::5, :] = genes[0::5, :][: len(genes[1::5])]
+        edge = rng.uniform(size=(n, dim))
+        genes = np.where(edge < 0.05, lo, np.where(edge > 0.95, hi, genes))
+        idx = rng.integers(0, n, size=k).astype(np.int32)
+        if j == 0:
+            idx = np.arange(k, dtype=np.int32)
+        pairs = k // 2
+        cx_u = rng.uniform(0, 1, size=pairs)
+        sbx_u = rng.uniform(0, 1, size=(pairs, dim, 3))
+        mut_u = rng.uniform(0, 1, size=(2 * pairs, dim, 2))
+        Ind = make_types(D, "d", (-1.0, -1.0))
+        pop = to_inds(Ind, genes, np.zeros((n, 2)))
+        tb = base.Toolbox()
+        tb.register("mate", tools.cxSimulatedBinaryBounded, low=low, up=up, eta=eta_c)
+        tb.register("mutate", tools.mutPolynomialBounded, low=low, up=up, eta=eta_m, indpb=indpb)
+        floats = []
+        for p in range(pairs):
+            a, b = genes[idx[2 * p]], genes[idx[2 * p + 1]]
+            floats.append(float(cx_u[p]))
+            if cx_u[p] <= cxpb:
+                for i in range(dim):
+                    floats.append(float(sbx_u[p, i, 0]))
+                    if sbx_u[p, i, 0] <= 0.5 and abs(a[i] - b[i]) > 1e-14:
+                        floats += [float(sbx_u[p, i, 1]), float(sbx_u[p, i, 2])]
+            for c in (2 * p, 2 * p + 1):
+                for i in range(dim):
+                    floats.append(float(mut_u[c, i, 0]))
+                    if mut_u[c, i, 0] <= indpb:
+                        floats.append(float(mut_u[c, i, 1]))
+        with Replay(floats=floats):
+            offspring = [tb.clone(pop[i]) for i in idx]
+            for ind1, ind2 in zip(offspring[::2], offspring[1::2]):
+                if random.random() <= cxpb:
+                    tb.mate(ind1, ind2)
+                tb.mutate(ind1)
+                tb.mutate(ind2)
+                del ind1.fitness.values, ind2.fitness.values
+        key = "sbx%d_" % j
+        out.update({key + "genes": genes, key + "idx": idx, key + "low": lo.copy(),
+                    key + "up": hi.copy(), key + "vec": np.array(int(vec)),
+                    key + "meta": np.array([cxpb, eta_c, eta_m, indpb]),
+                    key + "cx_u": cx_u, key + "sbx_u": sbx_u, key + "mut_u": mut_u,
+                    key + "out": np.array([list(o) for o in offspring], np.float64),
+                    key + "valid": np.array([o.fitness.valid for o in offspring])})
+    return out
+
+
 def gen_migration(D, rng):
     tools = D["deap.tools"]
     out = {}
@@ -577,6 +648,10 @@ def gen_c1_trajectory(D):
 
 def main():
     D = load_reference()
+    if sys.argv[1:] == ["sbx"]:
+        np.savez_compressed(os.path.join(HERE, "sbx.npz"),
+                            **gen_sbx(D, np.random.default_rng(91)))
+        return
     if sys.argv[1:] == ["dcd"]:  # regenerate one fixture without touching the rest
         np.savez_compressed(os.path.join(HERE, "dcd.npz"),
                             **gen_dcd(D, np.random.default_rng(77)))
@@ -592,6 +667,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "migration.npz"), **gen_migration(D, rng))
     np.savez_compressed(os.path.join(HERE, "c1_trajectory.npz"), **gen_c1_trajectory(D))
     np.savez_compressed(os.path.join(HERE, "dcd.npz"), **gen_dcd(D, np.random.default_rng(77)))
+    np.savez_compressed(os.path.join(HERE, "sbx.npz"), **gen_sbx(D, np.random.default_rng(91)))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

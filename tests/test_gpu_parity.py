@@ -617,3 +617,114 @@ def test_sel_tournament_dcd_errors(gpu):
         tools.selTournamentDCD(pop, 10)
     with pytest.raises(IndexError):
         tools.selTournamentDCD(pop, 9)   # 4*ceil(9/4) = 12 > 10: the reference's IndexError
+
+
+def _sbx_toolbox(low, up, eta_c, eta_m, indpb):
+    from deap_amd import base, tools
+    tb = base.Toolbox()
+    tb.register("mate", tools.cxSimulatedBinaryBounded, low=low, up=up, eta=eta_c)
+    tb.register("mutate", tools.mutPolynomialBounded, low=low, up=up, eta=eta_m, indpb=indpb)
+    return tb
+
+
+def _sbx_bounds(d, key):
+    if int(d[key + "vec"]):
+        return [float(v) for v in d[key + "low"]], [float(v) for v in d[key + "up"]]
+    return float(d[key + "low"][0]), float(d[key + "up"][0])
+
+
+SBX_TOL = 1e-12  # relative: Python `**` is glibc pow, the device ocml pow (both ~1 ulp)
+
+
+def test_vary_bounded_matches_reference(gpu):
+    """NSGA-II loop body (examples/ga/nsga2.py:96-105): cxSimulatedBinaryBounded +
+    mutPolynomialBounded on injected random()s against DEAP's own output."""
+    import torch
+    from deap_amd import algorithms
+    d = golden("sbx.npz")
+    for j in range(4):
+        key = "sbx%d_" % j
+        cxpb, eta_c, eta_m, indpb = (float(v) for v in d[key + "meta"])
+        genes = d[key + "genes"]
+        n = len(genes)
+        pop = _dp().from_numpy(genes, weights=(-1.0, -1.0), wvalues=np.zeros((n, 2)),
+                               valid=np.ones(n, np.uint8))
+        low, up = _sbx_bounds(d, key)
+        tb = _sbx_toolbox(low, up, eta_c, eta_m, indpb)
+        dec = {k: torch.from_numpy(np.ascontiguousarray(d[key + k])).cuda()
+               for k in ("cx_u", "sbx_u", "mut_u")}
+        idx = torch.from_numpy(d[key + "idx"]).cuda()
+        off = algorithms.varBounded(pop, tb, cxpb, idx, mode="inject", decisions=dec)
+        g, _wv, ok = off.to_numpy()
+        assert _rel_close(g, d[key + "out"], SBX_TOL), j
+        assert np.array_equal(ok.astype(bool), d[key + "valid"]), j
+
+
+def test_vary_bounded_native_replays_in_oracle(gpu):
+    """Native Philox decisions dumped by the kernel, replayed in the oracle
+    (ZDT1-like [0,1]^30 population, 2^12 offspring from a random index)."""
+    import torch
+    from deap_amd import algorithms
+    rng = np.random.default_rng(5)
+    n, dim, k = 4096, 30, 4095
+    genes = rng.uniform(0, 1, size=(n, dim))
+    dup = np.arange(3, n - 1, 11)
+    genes[dup] = genes[dup + 1]  # equal genes: the |x1 - x2| <= 1e-14 branch
+    genes[rng.uniform(size=(n, dim)) < 0.02] = 0.0
+    pop = _dp().from_numpy(genes, weights=(-1.0, -1.0), wvalues=rng.normal(size=(n, 2)),
+                           valid=np.ones(n, np.uint8))
+    idx_h = rng.integers(0, n, size=k).astype(np.int32)
+    tb = _sbx_toolbox(0.0, 1.0, 20.0, 20.0, 1.0 / dim)
+    dec = {}
+    off = algorithms.varBounded(pop, tb, 0.9, torch.from_numpy(idx_h).cuda(), mode="dump",
+                                decisions=dec)
+    g, wv, ok = off.to_numpy()
+    hd = {kk: v.cpu().numpy() for kk, v in dec.items()}
+    lo, hi = np.zeros(dim), np.ones(dim)
+    eg, _ewv, eok = ops.vary_bounded(genes, np.zeros((n, 2)), np.ones(n, bool), idx_h, 0.9, hd,
+                                     (20.0, lo, hi), (20.0, lo, hi, 1.0 / dim))
+    assert _rel_close(g, eg, SBX_TOL)
+    assert np.array_equal(ok.astype(bool), eok)
+    assert (g != genes[idx_h]).any(axis=1).mean() > 0.5  # the operators did act
+    assert (g >= 0).all() and (g <= 1).all()
+    # native == dump: the same stream state gives the same offspring
+    from deap_amd.ops import RandomStream
+    s1, s2 = RandomStream(9), RandomStream(9)
+    a = algorithms.varBounded(pop, tb, 0.9, torch.from_numpy(idx_h).cuda(), stream=s1)
+    b = algorithms.varBounded(pop, tb, 0.9, torch.from_numpy(idx_h).cuda(), stream=s2,
+                              mode="dump", decisions={})
+    assert np.array_equal(a.to_numpy()[0], b.to_numpy()[0])
+
+
+def test_bounded_operators_batch_form(gpu):
+    """cxSimulatedBinaryBounded / mutPolynomialBounded called on a population
+    (every pair mated / every individual mutated, odd n) against the oracle;
+    short bound sequences raise the reference's IndexError."""
+    from deap_amd import tools
+    rng = np.random.default_rng(8)
+    n, dim = 257, 9
+    low, up = [-1.0] * dim, [2.0] * dim
+    genes = rng.uniform(-1, 2, size=(n, dim))
+    pop = _dp().from_numpy(genes, weights=(1.0,), wvalues=np.zeros((n, 1)),
+                           valid=np.ones(n, np.uint8))
+    dec = {}
+    off = tools.cxSimulatedBinaryBounded(pop, 15.0, low, up, mode="dump", decisions=dec)
+    hd = {kk: v.cpu().numpy() for kk, v in dec.items()}
+    lo, hi = np.array(low), np.array(up)
+    eg, _w, eok = ops.vary_bounded(genes, np.zeros((n, 1)), np.ones(n, bool), None, 1.0, hd,
+                                   (15.0, lo, hi), None)
+    g, _wv, ok = off.to_numpy()
+    assert _rel_close(g, eg, SBX_TOL) and np.array_equal(ok.astype(bool), eok)
+    dec = {}
+    off = tools.mutPolynomialBounded(pop, eta=3.0, low=low, up=up, indpb=0.4, mode="dump",
+                                     decisions=dec)
+    hd = {kk: v.cpu().numpy() for kk, v in dec.items()}
+    eg, _w, eok = ops.vary_bounded(genes, np.zeros((n, 1)), np.ones(n, bool), None, 0.0, hd,
+                                   None, (3.0, lo, hi, 0.4))
+    g, _wv, ok = off.to_numpy()
+    assert _rel_close(g, eg, SBX_TOL) and np.array_equal(ok.astype(bool), eok)
+    assert not ok.any()
+    with pytest.raises(IndexError):
+        tools.mutPolynomialBounded(pop, 3.0, low[:-1], up, 0.4)
+    with pytest.raises(IndexError):
+        tools.cxSimulatedBinaryBounded(pop, 3.0, low, up[:2])

@@ -46,6 +46,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Variation) == 8 + 6 * 8 + 2 * 8
     assert ctypes.sizeof(_lib.Rng) == 16
     assert ctypes.sizeof(_lib.Decisions) == 9 * 8
+    assert ctypes.sizeof(_lib.BoundedVar) == 2 * 4 + 6 * 8 + 2 * 8
 
 
 def test_missing_library_fails_loudly(tmp_path):

@@ -168,3 +168,24 @@ def test_sel_tournament_dcd_matches_reference():
         got = ops.sel_tournament_dcd(d[key + "wv"], d[key + "crowd"], int(d[key + "k"]),
                                      d[key + "perm1"], d[key + "perm2"], d[key + "coin"])
         assert got == d[key + "chosen"].tolist(), j
+
+
+def _sbx_case(d, j):
+    k = "sbx%d_" % j
+    cxpb, eta_c, eta_m, indpb = (float(v) for v in d[k + "meta"])
+    low, up = d[k + "low"], d[k + "up"]
+    dec = {"cx_u": d[k + "cx_u"], "sbx_u": d[k + "sbx_u"], "mut_u": d[k + "mut_u"]}
+    return k, cxpb, (eta_c, low, up), (eta_m, low, up, indpb), dec
+
+
+def test_vary_bounded_matches_reference():
+    """NSGA-II loop body: cxSimulatedBinaryBounded + mutPolynomialBounded
+    (examples/ga/nsga2.py:96-105), bit-exact against DEAP on replayed random()s."""
+    d = golden("sbx.npz")
+    for j in range(4):
+        k, cxpb, sbx, poly, dec = _sbx_case(d, j)
+        n = len(d[k + "genes"])
+        g, _wv, ok = ops.vary_bounded(d[k + "genes"], np.zeros((n, 2)), np.ones(n, bool),
+                                      d[k + "idx"], cxpb, dec, sbx, poly)
+        assert np.array_equal(g, d[k + "out"]), j
+        assert np.array_equal(ok, d[k + "valid"]), j
