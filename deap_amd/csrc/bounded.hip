@@ -96,8 +96,25 @@ __global__ __launch_bounds__(256) void bounded_vary_kernel(BoundedArgs a) {
         const int64_t p = t / a.dim;
         const int g = (int)(t - p * a.dim);
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
-        const int64_t s0 = a.idx ? a.idx[c0] : c0;
+        int64_t s0 = a.idx ? a.idx[c0] : c0;
         double* w0 = reinterpret_cast<double*>(a.cgenes + c0 * a.cstride);
+        // out-of-range selection index: never read outside the parent rows;
+        // the child becomes NaN + invalid (the host layer raises IndexError
+        // for host-side indices before launching)
+        bool bad = s0 < 0 || s0 >= a.np;
+        if (p < a.pairs) {
+            const int64_t s1c = a.idx ? a.idx[c1] : c1;
+            bad = bad || s1c < 0 || s1c >= a.np;
+        }
+        if (bad) {
+            w0[g] = __builtin_nan("");
+            if (p < a.pairs) reinterpret_cast<double*>(a.cgenes + c1 * a.cstride)[g] = __builtin_nan("");
+            if (g == 0) {
+                a.cvalid[c0] = 0;
+                if (p < a.pairs) a.cvalid[c1] = 0;
+            }
+            continue;
+        }
         const double x0 = reinterpret_cast<const double*>(a.pgenes + s0 * a.pstride)[g];
         if (p == a.pairs) {
             // odd last offspring: outside zip(offspring[::2], offspring[1::2]) a

@@ -12,6 +12,8 @@ would call ``random.random()``.
 import ctypes
 from collections.abc import Sequence
 
+import numpy as np
+
 from .. import _lib
 
 
@@ -88,10 +90,17 @@ def vary_bounded(population, index, sbx, poly, cxpb, decisions=None, mode=None, 
             setattr(v, name, b)
 
     if index is not None:
+        on_device = isinstance(index, torch.Tensor) and index.device.type != "cpu"
+        if not on_device:
+            # host indices are checked here (the reference's IndexError); device
+            # indices (e.g. from selTournamentDCD) are not synced back — the
+            # kernel turns an out-of-range row into a NaN, invalid child
+            h = np.asarray(index.cpu() if isinstance(index, torch.Tensor) else index)
+            if h.size and (int(h.min()) < 0 or int(h.max()) >= len(population)):
+                raise IndexError("list index out of range")
+            index = torch.from_numpy(np.ascontiguousarray(h, dtype=np.int32))
         idx = index.to(device=dev, dtype=torch.int32).contiguous()
         k = len(idx)
-        if k and (int(idx.min()) < 0 or int(idx.max()) >= len(population)):
-            raise IndexError("list index out of range")
     else:
         idx = None
         k = len(population)

@@ -277,7 +277,9 @@ typedef struct dm_bounded_var {
  * per-gene (gate, rand, swap) random()s of SBX; mut_u[2*(k/2)][dim][2] the
  * per-gene (gate, rand) random()s of the polynomial mutation ([k] rows when
  * cx == 0).  A value is
- * only consumed where the reference would draw it. */
+ * only consumed where the reference would draw it.  An idx entry outside
+ * [0, parents->n) is never dereferenced: its pair's children become NaN rows
+ * with invalid fitness. */
 int dm_vary_bounded(dm_ctx* ctx, const dm_pop* parents, const int32_t* idx, dm_pop* children,
                     const dm_bounded_var* var, dm_rng rng, int32_t mode, double* cx_u,
                     double* sbx_u, double* mut_u);

@@ -728,3 +728,24 @@ def test_bounded_operators_batch_form(gpu):
         tools.mutPolynomialBounded(pop, 3.0, low[:-1], up, 0.4)
     with pytest.raises(IndexError):
         tools.cxSimulatedBinaryBounded(pop, 3.0, low, up[:2])
+
+
+def test_vary_bounded_index_guard(gpu):
+    """Host-side out-of-range indices raise IndexError; device-side ones are
+    never dereferenced (their pair becomes NaN, invalid) and the rest match."""
+    import torch
+    from deap_amd import algorithms
+    rng = np.random.default_rng(3)
+    n, dim = 16, 5
+    genes = rng.uniform(0, 1, size=(n, dim))
+    pop = _dp().from_numpy(genes, weights=(-1.0,), wvalues=np.zeros((n, 1)),
+                           valid=np.ones(n, np.uint8))
+    tb = _sbx_toolbox(0.0, 1.0, 20.0, 20.0, 0.5)
+    with pytest.raises(IndexError):
+        algorithms.varBounded(pop, tb, 0.9, [0, 1, 2, n])
+    idx = torch.tensor([0, 1, 2, n + 1000, 4, 5], dtype=torch.int32, device="cuda")
+    dec = {}
+    off = algorithms.varBounded(pop, tb, 0.9, idx, mode="dump", decisions=dec)
+    g, _wv, ok = off.to_numpy()
+    assert np.isnan(g[2:4]).all() and not ok[2:4].any()
+    assert np.isfinite(g[[0, 1, 4, 5]]).all()
