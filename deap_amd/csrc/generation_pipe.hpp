@@ -480,11 +480,12 @@ dim3 pipe_grid(K kern, int num_cus, int64_t npairs) {
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1)
         occ = 1;
-    // 16x the resident workgroups: the grid drains in many waves of blocks,
-    // so late blocks fill CUs whose first blocks finished early (A/B on C3,
-    // profiles/r01m: 2 resident/CU 3.47 ms; 8/CU 3.33-3.40; 32-64/CU
-    // 2.88-3.10 ms; 128/CU 2.95; one pair per wave 4.84)
-    occ = std::min(occ, 6) * 16;
+    // 64 workgroups per CU (>= 16x the resident ones): the grid drains in many
+    // waves of blocks, so late blocks fill CUs whose first blocks finished
+    // early (A/B on C3, profiles/r01m: 2 resident/CU 3.47 ms; 8/CU 3.33-3.40;
+    // 32/CU 3.10; 48-64/CU 2.88; 128/CU 2.95; one pair per wave 4.84;
+    // r01s on a slower box: 32/CU 3.31 ms, 64/CU 3.25)
+    occ = 64;
     if (const char* bpc = std::getenv("DM_PIPE_BPC")) occ = std::max(1, atoi(bpc));
     const int64_t blocks = std::min<int64_t>((npairs + 3) / 4, (int64_t)num_cus * occ);
     return dim3((unsigned)std::max<int64_t>(blocks, 1));

@@ -8,7 +8,7 @@ migration: ``migRing``; bookkeeping: ``Statistics``, ``MultiStatistics``,
 ``Logbook``, ``HallOfFame``; initialisation: ``initPopulation``.
 """
 from .crossover import cxBlend, cxSimulatedBinaryBounded, cxTwoPoint
-from .emo import selNSGA2, selTournamentDCD, sortNondominated
+from .emo import selNSGA2, selTournamentDCD, sortLogNondominated, sortNondominated
 from . import emo
 from .init import initPopulation
 from .migration import migRing
@@ -18,5 +18,5 @@ from .support import HallOfFame, Logbook, MultiStatistics, Statistics
 
 __all__ = ["cxTwoPoint", "cxBlend", "cxSimulatedBinaryBounded", "mutFlipBit", "mutGaussian",
            "mutPolynomialBounded", "selTournament", "selRandom",
-           "selBest", "selWorst", "selNSGA2", "selTournamentDCD", "sortNondominated", "migRing", "Statistics",
+           "selBest", "selWorst", "selNSGA2", "selTournamentDCD", "sortNondominated", "sortLogNondominated", "migRing", "Statistics",
            "MultiStatistics", "Logbook", "HallOfFame", "initPopulation", "emo"]

@@ -98,10 +98,9 @@ class _SelNSGA2(DeviceOperator):
 
     def __call__(self, individuals, k, nd="standard", *, stream=None, **_):
         _check(individuals)
+        if nd == "log":
+            return _sel_nsga2_log(individuals, int(k))
         if nd != "standard":
-            if nd == "log":
-                raise NotImplementedError("selNSGA2(nd='log') (sortLogNondominated) is not on "
-                                          "the device yet; use nd='standard'")
             raise Exception('selNSGA2: The choice of non-dominated sorting '
                             'method "{0}" is invalid.'.format(nd))
         torch = _torch()
@@ -118,6 +117,63 @@ class _SelNSGA2(DeviceOperator):
                   ctypes.c_void_p(out.data_ptr()),
                   ctypes.c_void_p(individuals.crowding_dist.data_ptr()))
         return out[: min(k, n)]
+
+
+def _log_fronts(individuals, k, first_front_only):
+    """Fronts in sortLogNondominated's order (emo.py:246-276): the Pareto ranks
+    come from the device sort (Fortin et al.'s divide and conquer computes the
+    same ranks); inside a front the unique fitnesses follow
+    ``fitnesses.sort(reverse=True)`` (lexicographic wvalues, descending) and
+    equal fitnesses keep population order (``unique_fits[...].append``).
+    Ordering: stable device sorts, last objective first, then by rank."""
+    torch = _torch()
+    n = len(individuals)
+    _order, _fstart, rank, _ns, nf = _sort(individuals, k, first_front_only)
+    r = rank[:n].long()
+    perm = torch.nonzero(r >= 0).flatten()  # ascending row index
+    wv = individuals.wvalues[:n].reshape(n, individuals.nobj)
+    for j in reversed(range(individuals.nobj)):
+        _, o = torch.sort(wv[perm, j], descending=True, stable=True)
+        perm = perm[o]
+    _, o = torch.sort(r[perm], stable=True)
+    perm = perm[o].to(torch.int32)
+    counts = torch.bincount(r[perm.long()], minlength=nf)[:nf].cpu().tolist()
+    fronts, at = [], 0
+    for c in counts:
+        fronts.append(perm[at:at + c])
+        at += c
+    return fronts
+
+
+class _SortLogNondominated(DeviceOperator):
+    kind = "sort"
+
+    def __call__(self, individuals, k, first_front_only=False):
+        _check(individuals)
+        if k == 0:
+            return []
+        if len(individuals) == 0:
+            raise IndexError("list index out of range")  # individuals[0] (emo.py:252)
+        fronts = _log_fronts(individuals, k, first_front_only)
+        return fronts[0] if first_front_only else fronts
+
+
+def _sel_nsga2_log(individuals, k):
+    """selNSGA2(nd='log') (emo.py:15-50 over sortLogNondominated): crowding on
+    every front in its log order, all fronts but the last, then the last one
+    by decreasing crowding distance (stable, as ``sorted(..., reverse=True)``)."""
+    torch = _torch()
+    if k == 0 or len(individuals) == 0:
+        return torch.empty((0,), dtype=torch.int32, device=individuals.device)
+    fronts = _log_fronts(individuals, k, False)
+    crowd = assignCrowdingDist(individuals, fronts)
+    chosen = fronts[:-1]
+    rest = k - sum(len(f) for f in chosen)
+    if rest > 0:
+        last = fronts[-1]
+        _, o = torch.sort(crowd[last.long()], descending=True, stable=True)
+        chosen = chosen + [last[o][:rest]]
+    return torch.cat(chosen) if chosen else fronts[0][:0]
 
 
 class _SelTournamentDCD(DeviceOperator):
@@ -157,8 +213,9 @@ class _SelTournamentDCD(DeviceOperator):
 
 
 sortNondominated = _SortNondominated("sortNondominated", "deap/tools/emo.py:53-117")
+sortLogNondominated = _SortLogNondominated("sortLogNondominated", "deap/tools/emo.py:234-441")
 assignCrowdingDist = _CrowdingDist("assignCrowdingDist", "deap/tools/emo.py:119-143")
 selNSGA2 = _SelNSGA2("selNSGA2", "deap/tools/emo.py:15-50")
 selTournamentDCD = _SelTournamentDCD("selTournamentDCD", "deap/tools/emo.py:145-195")
 
-__all__ = ["selNSGA2", "sortNondominated", "selTournamentDCD"]  # assignCrowdingDist is not exported (emo.py:842-843)
+__all__ = ["selNSGA2", "sortNondominated", "sortLogNondominated", "selTournamentDCD"]  # assignCrowdingDist is not exported (emo.py:842-843)

@@ -477,6 +477,32 @@ def sel_nsga2(wvalues, weights, k):
     return chosen, crowd
 
 
+def sort_log_nondominated(wvalues, k, first_front_only=False):
+    """sortLogNondominated (emo.py:234-276): the same Pareto ranks as
+    sort_nondominated; fronts list unique fitnesses in descending
+    lexicographic order (emo.py:257), equal ones in population order."""
+    if k == 0:
+        return []
+    fronts = sort_nondominated(wvalues, k, first_front_only)
+    out = [sorted(f, key=lambda i: (tuple(-float(x) for x in wvalues[i]), i)) for f in fronts]
+    return out[0] if first_front_only else out
+
+
+def sel_nsga2_log(wvalues, weights, k):
+    """emo.py:15-50 with nd='log'."""
+    fronts = sort_log_nondominated(wvalues, k)
+    crowd = {}
+    for front in fronts:
+        vals = [[float(w) / float(x) for w, x in zip(wvalues[i], weights)] for i in front]
+        for i, d in zip(front, assign_crowding_dist(vals)):
+            crowd[i] = d
+    chosen = [i for f in fronts[:-1] for i in f]
+    kk = k - len(chosen)
+    if kk > 0:
+        chosen.extend(sorted(fronts[-1], key=lambda i: crowd[i], reverse=True)[:kk])
+    return chosen
+
+
 # ---------------------------------------------------------------------------
 # migRing (deap/tools/migration.py:4-51) on demes of (genes, wvalues, valid)
 # ---------------------------------------------------------------------------

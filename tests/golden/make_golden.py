@@ -530,6 +530,29 @@ def gen_sbx(D, rng):
     return out
 
 
+def gen_nsga2log(D, rng):
+    """sortLogNondominated (emo.py:234-441) and selNSGA2(nd='log') (emo.py:15-50)
+    on tie-heavy integer fitnesses (deterministic: no random draws)."""
+    tools = D["deap.tools"]
+    out = {}
+    cases = [(40, 2, 30), (120, 3, 60), (200, 3, 199), (64, 2, 64), (90, 4, 45), (50, 3, 500)]
+    for j, (n, m, k) in enumerate(cases):
+        weights = tuple([-1.0, 1.0, -1.0, 1.0][:m])
+        Ind = make_types(D, "d", weights)
+        vals = rng.integers(0, 6 if m < 4 else 4, size=(n, m)).astype(np.float64)
+        wv = vals * np.array(weights)
+        pop = to_inds(Ind, rng.uniform(0, 1, size=(n, 2)), wv)
+        ident = {id(p): i for i, p in enumerate(pop)}
+        fronts = tools.emo.sortLogNondominated(pop, k)
+        chosen = tools.selNSGA2(pop, k, nd="log")
+        key = "log%d_" % j
+        out.update({key + "wv": wv, key + "k": np.array(k),
+                    key + "order": np.array([ident[id(x)] for f in fronts for x in f], np.int32),
+                    key + "sizes": np.array([len(f) for f in fronts], np.int32),
+                    key + "chosen": np.array([ident[id(c)] for c in chosen], np.int32)})
+    return out
+
+
 def gen_migration(D, rng):
     tools = D["deap.tools"]
     out = {}
@@ -648,6 +671,10 @@ def gen_c1_trajectory(D):
 
 def main():
     D = load_reference()
+    if sys.argv[1:] == ["log"]:
+        np.savez_compressed(os.path.join(HERE, "nsga2log.npz"),
+                            **gen_nsga2log(D, np.random.default_rng(13)))
+        return
     if sys.argv[1:] == ["sbx"]:
         np.savez_compressed(os.path.join(HERE, "sbx.npz"),
                             **gen_sbx(D, np.random.default_rng(91)))
@@ -668,6 +695,8 @@ def main():
     np.savez_compressed(os.path.join(HERE, "c1_trajectory.npz"), **gen_c1_trajectory(D))
     np.savez_compressed(os.path.join(HERE, "dcd.npz"), **gen_dcd(D, np.random.default_rng(77)))
     np.savez_compressed(os.path.join(HERE, "sbx.npz"), **gen_sbx(D, np.random.default_rng(91)))
+    np.savez_compressed(os.path.join(HERE, "nsga2log.npz"),
+                        **gen_nsga2log(D, np.random.default_rng(13)))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

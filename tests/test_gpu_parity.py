@@ -749,3 +749,24 @@ def test_vary_bounded_index_guard(gpu):
     g, _wv, ok = off.to_numpy()
     assert np.isnan(g[2:4]).all() and not ok[2:4].any()
     assert np.isfinite(g[[0, 1, 4, 5]]).all()
+
+
+def test_sort_log_nondominated_matches_reference(gpu):
+    """Device sortLogNondominated / selNSGA2(nd='log') against DEAP's output."""
+    from deap_amd import tools
+    d = golden("nsga2log.npz")
+    for j in range(6):
+        key = "log%d_" % j
+        wv, k = d[key + "wv"], int(d[key + "k"])
+        n, m = wv.shape
+        weights = tuple([-1.0, 1.0, -1.0, 1.0][:m])
+        pop = _dp().from_numpy(np.zeros((n, 2)), weights=weights, wvalues=wv,
+                               valid=np.ones(n, np.uint8))
+        fronts = tools.sortLogNondominated(pop, k)
+        assert [len(f) for f in fronts] == d[key + "sizes"].tolist(), j
+        assert np.concatenate([f.cpu().numpy() for f in fronts]).tolist() == \
+            d[key + "order"].tolist(), j
+        assert tools.selNSGA2(pop, k, nd="log").cpu().numpy().tolist() == \
+            d[key + "chosen"].tolist(), j
+    first = tools.sortLogNondominated(pop, 5, first_front_only=True)
+    assert first.cpu().numpy().tolist() == d["log5_order"][: d["log5_sizes"][0]].tolist()

@@ -189,3 +189,16 @@ def test_vary_bounded_matches_reference():
                                       d[k + "idx"], cxpb, dec, sbx, poly)
         assert np.array_equal(g, d[k + "out"]), j
         assert np.array_equal(ok, d[k + "valid"]), j
+
+
+def test_sort_log_nondominated_matches_reference():
+    """sortLogNondominated front order + selNSGA2(nd='log') (emo.py:15-50,234-276)."""
+    d = golden("nsga2log.npz")
+    for j in range(6):
+        key = "log%d_" % j
+        wv, k = d[key + "wv"], int(d[key + "k"])
+        weights = [-1.0, 1.0, -1.0, 1.0][:wv.shape[1]]
+        fronts = ops.sort_log_nondominated(wv, k)
+        assert [len(f) for f in fronts] == d[key + "sizes"].tolist(), j
+        assert [i for f in fronts for i in f] == d[key + "order"].tolist(), j
+        assert ops.sel_nsga2_log(wv, weights, k) == d[key + "chosen"].tolist(), j
