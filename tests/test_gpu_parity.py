@@ -770,3 +770,52 @@ def test_sort_log_nondominated_matches_reference(gpu):
             d[key + "chosen"].tolist(), j
     first = tools.sortLogNondominated(pop, 5, first_front_only=True)
     assert first.cpu().numpy().tolist() == d["log5_order"][: d["log5_sizes"][0]].tolist()
+
+
+def test_nsga2_example_loop_steps_replay_in_oracle(gpu):
+    """Three generations of DEAP's NSGA-II example loop (examples/ga/nsga2.py:94-114)
+    on ZDT1, every stage checked against the oracle from the GPU's own state:
+    selTournamentDCD (dumped permutations/coins, exact) -> varBounded (dumped
+    random()s, 1e-12 rel) -> evaluate -> selNSGA2(pop + offspring) (exact)."""
+    import torch
+    from deap_amd import algorithms, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    rng = np.random.default_rng(11)
+    n, dim, w = 64, 30, (-1.0, -1.0)
+    genes = rng.uniform(0, 1, size=(n, dim))
+    pop = _dp().from_numpy(genes, weights=w)
+    benchmarks.zdt1(pop)
+    idx = tools.selNSGA2(pop, n)  # assigns crowding distances (nsga2.py:92)
+    tb = _sbx_toolbox(0.0, 1.0, 20.0, 20.0, 1.0 / dim)
+    stream = RandomStream(21)
+    for _gen in range(3):
+        g0, wv0, _ = pop.to_numpy()
+        crowd = pop.crowding_dist[:n].cpu().numpy()
+        dcd = {}
+        sel = tools.selTournamentDCD(pop, n, mode="dump", decisions=dcd, stream=stream)
+        want = ops.sel_tournament_dcd(wv0, crowd, n, dcd["perm1"].cpu().numpy(),
+                                      dcd["perm2"].cpu().numpy(), dcd["coin"].cpu().numpy())
+        assert sel.cpu().numpy().tolist() == want
+        dec = {}
+        off = algorithms.varBounded(pop, tb, 0.9, sel, mode="dump", decisions=dec, stream=stream)
+        hd = {kk: v.cpu().numpy() for kk, v in dec.items()}
+        lo, hi = np.zeros(dim), np.ones(dim)
+        eg, _ewv, eok = ops.vary_bounded(g0, wv0, np.ones(n, bool), np.array(want), 0.9, hd,
+                                         (20.0, lo, hi), (20.0, lo, hi, 1.0 / dim))
+        og, _owv, ook = off.to_numpy()
+        assert _rel_close(og, eg, SBX_TOL) and np.array_equal(ook, eok)
+        benchmarks.zdt1(off)
+        og, owv, _ = off.to_numpy()
+        ewv = np.array([[f * x for f, x in zip(ops.zdt1(list(r)), w)] for r in og])
+        assert _rel_close(owv, ewv, 1e-12)
+        both = np.concatenate([g0, og])
+        bwv = np.concatenate([wv0, owv])
+        comb = _dp().from_numpy(both, weights=w, wvalues=bwv, valid=np.ones(2 * n, np.uint8))
+        chosen = tools.selNSGA2(comb, n).cpu().numpy()
+        echosen, ecrowd = ops.sel_nsga2(bwv, w, n)
+        assert chosen.tolist() == echosen
+        # pop[:] = chosen, carrying the crowding distances
+        pop = _dp().from_numpy(both[chosen], weights=w, wvalues=bwv[chosen],
+                               valid=np.ones(n, np.uint8))
+        pop.crowding_dist = comb.crowding_dist[torch.from_numpy(chosen).long().cuda()].contiguous()
+        assert np.allclose(pop.crowding_dist.cpu().numpy(), [ecrowd[i] for i in chosen])
