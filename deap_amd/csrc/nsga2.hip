@@ -151,8 +151,16 @@ __global__ __launch_bounds__(256) void dom_build_kernel(const double* ufit, int 
 // The mask of row u is parked in lane u%64 and every 64 rows each lane stores
 // its row's DB_WPW words; dominator counts go to per-word-group partials
 // cpart[g][u] (summed by dom_count_reduce_kernel, no atomics).
-constexpr int DB_WPW = 8;     // words per wave (512 v)
-constexpr int DB_ROWS = 512;  // rows u per wave
+// Tile A/B on C5 (2^18 rows, M = 3; r01t): 8 words x 512 rows 29.8 ms/gen,
+// 4 x 1024 29.0-29.4, 4 x 512 29.2, 16 x 512 35.0, 2 x 2048 36.4.
+#ifndef DM_DB_WPW
+#define DM_DB_WPW 4
+#endif
+#ifndef DM_DB_ROWS
+#define DM_DB_ROWS 1024
+#endif
+constexpr int DB_WPW = DM_DB_WPW;    // words per wave (256 v)
+constexpr int DB_ROWS = DM_DB_ROWS;  // rows u per wave
 
 template <int M>
 __global__ __launch_bounds__(256) void dom_ballot_kernel(const double* __restrict__ ufit, int64_t U,
