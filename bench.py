@@ -10,8 +10,12 @@ in HBM, synthetic random-init genomes (U[-5.12, 5.12]).
 
 N=1: config C3 (one island of 2^20).  N>1 (torchrun, one rank per GPU): one
 2^20 island per GPU (weak scaling, config C4) with migRing every 5 gens (k=15,
-selBest, ring i -> i+1) exchanged with RCCL point-to-point; value = all ranks'
-individual-generations / max-over-ranks time.
+selBest, ring i -> i+1) exchanged with RCCL point-to-point from inside
+libdeapmi (dm_mig_ring_rccl); value = all ranks' individual-generations /
+max-over-ranks time.  ``--islands-per-gpu I`` runs I demes of --pop per GPU
+(weak); ``--islands 8`` is config C4 literally: 8 demes of 2^20 split over the
+N GPUs (8/4/2/1 per GPU, strong scaling); ``migration`` reports the cost of
+the migrations (HIP events) separately.
 
 ``roofline``: algorithmic bytes per individual-generation B = 2G + (t+1)F
 (2*8000 + 4*8 = 16,032 B for C3) x individuals per launch /
@@ -47,6 +51,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c5", "c5x"])
     ap.add_argument("--pop", type=int, default=1 << 20)
+    ap.add_argument("--islands-per-gpu", type=int, default=1,
+                    help="demes of --pop individuals per GPU (weak scaling)")
+    ap.add_argument("--islands", type=int, default=0,
+                    help="total demes, split evenly over the GPUs (C4: 8; strong scaling)")
     ap.add_argument("--mig-every", type=int, default=5)
     ap.add_argument("--mig-k", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -55,20 +63,47 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_workers():
+    """Worker processes for the CPU baseline: every CPU this process may run
+    on (sched_getaffinity), capped at the 16-CPU share the GPU box grants one
+    GPU (its os.cpu_count() reports the whole machine)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(avail, int(os.environ.get("DM_CPU_WORKERS", "16")))), avail
+
+
 def cpu_baseline(problem, sample):
-    import multiprocessing
     from oracle import deap_port
-    workers = max(1, min(os.cpu_count() or 1, 16))
+    workers, avail = host_workers()
     dim = CONFIGS_DIM[problem]
-    rate, secs, used = deap_port.run(problem if problem != "onemax" else "onemax", n=sample,
-                                     dim=dim, ngen=2, workers=workers)
+    rate, secs, used = deap_port.run(problem, n=sample, dim=dim, ngen=2, workers=workers)
     return {"value": rate, "unit": "individual-generations/sec", "cores": used, "kind": "port",
-            "sample": "DEAP-faithful eaSimple (oracle/deap_port.py: array genomes, deepcopy clone, "
-                      "Pool(%d).map evaluate), pop %d x %d genes, 2 timed generations (%.1f s)"
+            "cpu_model": cpu_model(), "cpus_visible": avail,
+            "sample": "DEAP-faithful eaSimple (oracle/deap_port.py, bit-exact with the reference on "
+                      "tests/golden/port.npz: array genomes, deepcopy clone, Pool(%d).map "
+                      "evaluate), pop %d x %d genes, 2 timed generations (%.1f s)"
                       % (used, sample, dim, secs)}
 
 
 CONFIGS_DIM = {"rastrigin": 1000, "rosenbrock": 1000, "onemax": 4096}
+METRICS = {
+    "c3": "individual-generations/sec @pop=2^20 Rastrigin-1000D, 1-8 GPU; % HBM peak",
+    "c3r": "individual-generations/sec @pop=2^20 Rosenbrock-1000D (C3), 1-8 GPU; % HBM peak",
+    "c2": "individual-generations/sec @pop=2^20 OneMax-4096 packed bits (C2); % HBM peak",
+}
 
 
 def load_traffic(config):
@@ -87,6 +122,7 @@ def main():
         return bench_nsga2(args)
     if args.config == "c5x":
         return bench_nsga2_example(args)
+    import ctypes
     import torch
     import torch.distributed as dist
 
@@ -100,16 +136,24 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd import _lib, algorithms, base, benchmarks, tools
     from deap_amd.ops import RandomStream
 
     problem, gtype, dim, cx, mut, weights, bpi = CONFIGS[args.config]
     n = args.pop
-    stream = RandomStream(args.seed, island=rank)
+    if args.islands:
+        if args.islands % world:
+            raise SystemExit("--islands must be a multiple of the GPU count")
+        per, scaling = args.islands // world, "strong"
+    else:
+        per, scaling = args.islands_per_gpu, "weak"
+    n_demes = per * world
+    ids = list(range(rank * per, (rank + 1) * per))
     low, high = {"rastrigin": (-5.12, 5.12), "rosenbrock": (-2.048, 2.048),
                  "onemax": (0, 1)}[problem]
-    pop = tools.initPopulation(n=n, dim=dim, low=low, high=high, gtype=gtype, weights=weights,
-                               device=device, stream=stream)
+    streams = [RandomStream(args.seed, island=d) for d in ids]
+    pops = [tools.initPopulation(n=n, dim=dim, low=low, high=high, gtype=gtype, weights=weights,
+                                 device=device, stream=s) for s in streams]
     tb = base.Toolbox()
     tb.register("evaluate", getattr(benchmarks, problem))
     tb.register("select", tools.selTournament, tournsize=3)
@@ -122,40 +166,51 @@ def main():
     else:
         tb.register("mutate", tools.mutFlipBit, indpb=0.05)
     cxpb, mutpb = 0.5, 0.2
-    getattr(benchmarks, problem)(pop)  # generation 0: evaluate everyone
-    step = algorithms.GenerationStep(pop, tb, cxpb, mutpb)
-    off = pop.like(n, capacity=n)
-    nevals = torch.zeros(args.warmup + args.steps + 1, dtype=torch.int64, device=device)
+    for p in pops:
+        getattr(benchmarks, problem)(p)  # generation 0: evaluate everyone
+    steps = [algorithms.GenerationStep(p, tb, cxpb, mutpb) for p in pops]
+    offs = [p.like(n, capacity=n) for p in pops]
+    total_gens = args.warmup + args.steps + 1
+    nevals = torch.zeros((per, total_gens), dtype=torch.int64, device=device)
+    mig_events = []
 
-    def migrate():
+    def migrate(timed):
         from deap_amd.islands import migRingDistributed
-        migRingDistributed([pop], [rank], world, args.mig_k, tools.selBest, stream=stream)
+        a = b = None
+        if timed:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+        if world == 1:
+            tools.migRing(pops, args.mig_k, tools.selBest, stream=streams[0])
+        else:
+            migRingDistributed(pops, ids, n_demes, args.mig_k, tools.selBest, stream=streams[0])
+        if timed:
+            b.record()
+            mig_events.append((a, b))
 
-    def one_gen(g):
-        step.step(pop, off, stream, ctypes_ptr(nevals, g))
-        pop.swap_storage(off)
-        if world > 1 and (g + 1) % args.mig_every == 0:
-            migrate()
-
-    import ctypes
-
-    def ctypes_ptr(t, i):
-        return ctypes.c_void_p(t.data_ptr() + 8 * i)
+    def one_gen(g, timed):
+        for i in range(per):
+            steps[i].step(pops[i], offs[i], streams[i],
+                          ctypes.c_void_p(nevals[i].data_ptr() + 8 * g))
+            pops[i].swap_storage(offs[i])
+        if n_demes > 1 and (g + 1) % args.mig_every == 0:
+            migrate(timed)
 
     for g in range(args.warmup):
-        one_gen(g)
+        one_gen(g, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # HIP event pairs recorded by the library itself around the generation
-    # kernel (gen_pipe_kernel), on the stream it is launched on
-    from deap_amd import _lib
-    ctx = pop.ctx.bind()
-    _lib.call("dm_ctx_set_timing", ctx, args.steps)
+    # HIP event pairs recorded by the library itself around every generation
+    # kernel launch (gen_pipe_kernel / gen_bits_burst_kernel), on the stream
+    # it is launched on
+    ctx = pops[0].ctx.bind()
+    launches = args.steps * per
+    _lib.call("dm_ctx_set_timing", ctx, launches)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        one_gen(args.warmup + s)
+        one_gen(args.warmup + s, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -165,23 +220,25 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    times = (ctypes.c_float * args.steps)()
+    times = (ctypes.c_float * launches)()
     cnt = ctypes.c_int32(0)
-    _lib.call("dm_ctx_kernel_times", ctx, times, args.steps, ctypes.byref(cnt))
+    _lib.call("dm_ctx_kernel_times", ctx, times, launches, ctypes.byref(cnt))
     _lib.call("dm_ctx_set_timing", ctx, 0)
-    assert cnt.value == args.steps, "expected one generation kernel per step, got %d" % cnt.value
-    kern_ms = sum(times) / args.steps
+    assert cnt.value == launches, "expected one generation kernel per deme and step, got %d" % cnt.value
+    kern_ms = sum(times) / launches
+    mig_ms = (sum(a.elapsed_time(b) for a, b in mig_events) / len(mig_events)
+              if mig_events else 0.0)
     if world > 1:
-        t = torch.tensor([kern_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([kern_ms, mig_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        kern_ms = float(t.item())
+        kern_ms, mig_ms = (float(x) for x in t.tolist())
     nev = nevals.cpu().tolist()
-    # sanity: the population stays valid and finite
-    wv = pop.wvalues[:n]
-    assert bool(pop.valid[:n].bool().all()), "invalid fitness left after a generation"
-    assert bool(torch.isfinite(wv).all()), "non-finite fitness"
+    # sanity: the populations stay valid and finite
+    for p in pops:
+        assert bool(p.valid[:n].bool().all()), "invalid fitness left after a generation"
+        assert bool(torch.isfinite(p.wvalues[:n]).all()), "non-finite fitness"
 
-    total = n * args.steps * world
+    total = n * args.steps * n_demes
     value = total / elapsed
     achieved = (n * bpi) / (kern_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -189,23 +246,30 @@ def main():
                 "traffic": load_traffic(args.config),
                 "kernel": "gen_bits_burst_kernel" if gtype == "bits" else "gen_pipe_kernel",
                 "kernel_ms": round(kern_ms, 4), "bytes_per_ind_gen": bpi}
-    out = {"metric": "individual-generations/sec @pop=2^20 Rastrigin-1000D, 1-8 GPU; % HBM peak",
+    workload = {"c3": "C3 Rastrigin-1000D fp64 eaSimple",
+                "c3r": "C3 Rosenbrock-1000D fp64 eaSimple",
+                "c2": "C2 OneMax-4096 packed-bit eaSimple"}[args.config]
+    if n_demes > 1:
+        workload = ("C4 %d islands x %d (%s) with migRing k=%d selBest every %d gens"
+                    % (n_demes, n, workload.split(" ", 1)[1], args.mig_k, args.mig_every))
+    out = {"metric": METRICS[args.config],
            "value": round(value, 1), "unit": "individual-generations/sec", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None,
+           "scaling": scaling, "vs_baseline": None,
            "dtype": {"f64": "f64", "f32": "f32", "bits": "u64"}[gtype], "data": "synthetic",
-           "config": {"workload": {"c3": "C3 Rastrigin-1000D fp64 eaSimple",
-                                   "c3r": "C3 Rosenbrock-1000D fp64 eaSimple",
-                                   "c2": "C2 OneMax-4096 packed-bit eaSimple"}[args.config]
-                      + (" islands (C4), migRing k=%d every %d gens" % (args.mig_k, args.mig_every)
-                         if world > 1 else ""),
-                      "pop_per_gpu": n, "genes": dim, "islands": world,
+           "config": {"workload": workload, "pop_per_island": n, "islands": n_demes,
+                      "islands_per_gpu": per, "genes": dim,
                       "operators": "selTournament(t=3) cx%s mut%s cxpb=0.5 mutpb=0.2 indpb=0.05"
                                    % (cx.capitalize(), mut.capitalize()),
-                      "parallelism": "islands%d" % world},
+                      "parallelism": "islands%d" % n_demes},
            "roofline": roofline,
-           "nevals_mean": round(sum(nev[args.warmup:args.warmup + args.steps]) / args.steps, 1)}
+           "nevals_mean": round(sum(sum(r[args.warmup:args.warmup + args.steps]) for r in nev)
+                                / (args.steps * per), 1)}
+    if n_demes > 1:
+        out["migration"] = {"ms_per_migration": round(mig_ms, 4), "every": args.mig_every,
+                            "k": args.mig_k,
+                            "frac_of_time": round(mig_ms * len(mig_events) / (elapsed * 1e3), 5)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(problem, args.cpu_sample)
     else:

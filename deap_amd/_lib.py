@@ -108,7 +108,26 @@ SIGNATURES = {
     "dm_pack_bytes": (_i64, [_PP(DevicePop), _i64]),
     "dm_mig_place": (ctypes.c_int, [_p, _PP(DevicePop), _p, _p, _i64, _p]),
     "dm_fitness_stats": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _p]),
+    "dm_sel_sample": (ctypes.c_int, [_p, _i64, _i64, Rng, _p]),
+    "dm_mig_plan": (ctypes.c_int, [_i32, _PP(_i32), _PP(_i32), _i32, _i32, _p, _i32,
+                                   _PP(_i32)]),
+    "dm_mig_ring": (ctypes.c_int, [_p, _i32, _PP(DevicePop), _PP(_i32), _i64, _PP(_p), _PP(_p),
+                                   _PP(_p)]),
+    "dm_comm_get_unique_id": (ctypes.c_int, [_p]),
+    "dm_comm_init": (ctypes.c_int, [_p, _i32, _i32, _p, _PP(_p)]),
+    "dm_comm_destroy": (ctypes.c_int, [_p]),
+    "dm_mig_ring_rccl": (ctypes.c_int, [_p, _p, _i32, _PP(DevicePop), _PP(_i32), _i32, _PP(_i32),
+                                        _PP(_i32), _i64, _PP(_p), _PP(_p), _PP(_p), _i32]),
 }
+
+DM_HOP_LOCAL, DM_HOP_SEND, DM_HOP_RECV = 0, 1, 2
+DM_MIG_FORCE_P2P = 1
+DM_COMM_ID_BYTES = 128
+
+
+class MigHop(ctypes.Structure):
+    """struct dm_mig_hop"""
+    _fields_ = [("kind", _i32), ("from_", _i32), ("to", _i32), ("peer", _i32)]
 
 
 class DeviceUnavailable(RuntimeError):

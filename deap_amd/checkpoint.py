@@ -48,6 +48,25 @@ def _jsonable(v):
     return v
 
 
+def _logbook_json(logbook):
+    """A Logbook with its chapters (MultiStatistics records are split into
+    chapters by ``Logbook.record``, support.py:342-349), recursively."""
+    return {"header": _jsonable(logbook.header), "records": _jsonable(list(logbook)),
+            "buffindex": logbook.buffindex,
+            "chapters": {name: _logbook_json(ch) for name, ch in logbook.chapters.items()}}
+
+
+def _logbook_from_json(h):
+    from .tools.support import Logbook
+    lb = Logbook()
+    lb.header = h["header"]
+    lb.extend(dict(r) for r in h["records"])
+    lb.buffindex = h.get("buffindex", 0)
+    for name, ch in h.get("chapters", {}).items():
+        lb.chapters[name] = _logbook_from_json(ch)
+    return lb
+
+
 def header(population, stream=None, generation=None, halloffame=None, logbook=None,
            extra=None):
     """The JSON-serialisable part of a checkpoint."""
@@ -55,7 +74,7 @@ def header(population, stream=None, generation=None, halloffame=None, logbook=No
          "stream": list(stream.getstate()) if stream is not None else None,
          "generation": generation, "extra": _jsonable(extra)}
     if logbook is not None:
-        h["logbook"] = {"header": logbook.header, "records": _jsonable(list(logbook))}
+        h["logbook"] = _logbook_json(logbook)
     if halloffame is not None:
         h["halloffame"] = {"maxsize": halloffame.maxsize,
                            "items": [[_jsonable(list(ind)), list(ind.fitness.wvalues)]
@@ -113,11 +132,7 @@ def load(path, device=None, individual_class=None, capacity=None):
         st.setstate(tuple(h["stream"]))
         out["stream"] = st
     if h.get("logbook") is not None:
-        lb = Logbook()
-        lb.header = h["logbook"]["header"]
-        for rec in h["logbook"]["records"]:
-            lb.record(**rec)
-        out["logbook"] = lb
+        out["logbook"] = _logbook_from_json(h["logbook"])
     if h.get("halloffame") is not None:
         hof = HallOfFame(h["halloffame"]["maxsize"])
         items = h["halloffame"]["items"]

@@ -320,86 +320,87 @@ __global__ void gather_kernel(const char* sg, const double* swv, const uint8_t* 
     }
 }
 
-// Fitness statistics: per-objective min/max/sum/sumsq/argmin/argmax of values.
+// Fitness statistics (tools.Statistics over fitness.values, support.py:199-210):
+// per objective the min / max with first-occurrence argmin / argmax (numpy
+// semantics), the count, mean and M2 = sum of squared deviations combined with
+// Chan et al.'s pairwise update (stable where sumsq - n*mean^2 cancels), the
+// plain sum, and NaN propagation as numpy's reducers do.
 struct StatAcc {
-    double mn, mx, sum, sq;
-    int64_t amn, amx;
+    double mn, mx, mean, m2, sum;
+    int64_t amn, amx, cnt, nan;
 };
-__global__ void stats_kernel(const double* wv, const uint8_t* valid, int64_t n, int nobj,
-                             dm_eval w, double* part, int64_t nparts) {
-    // w.weights used as weights; one block per partial, obj = blockIdx.y
+__device__ __forceinline__ void stat_merge(StatAcc& x, const StatAcc& y) {
+    if (y.amn >= 0 && (x.amn < 0 || y.mn < x.mn || (y.mn == x.mn && y.amn < x.amn))) {
+        x.mn = y.mn;
+        x.amn = y.amn;
+    }
+    if (y.amx >= 0 && (x.amx < 0 || y.mx > x.mx || (y.mx == x.mx && y.amx < x.amx))) {
+        x.mx = y.mx;
+        x.amx = y.amx;
+    }
+    if (y.cnt) {
+        const int64_t n = x.cnt + y.cnt;
+        const double d = y.mean - x.mean;
+        x.mean += d * ((double)y.cnt / (double)n);
+        x.m2 += y.m2 + d * d * ((double)x.cnt * (double)y.cnt / (double)n);
+        x.cnt = n;
+    }
+    x.sum += y.sum;
+    x.nan += y.nan;
+}
+__global__ __launch_bounds__(256) void stats_kernel(const double* wv, const uint8_t* valid,
+                                                    int64_t n, int nobj, dm_eval w, StatAcc* part,
+                                                    int64_t nparts) {
+    // w.weights: the fitness weights (values = wvalues / weights, base.py:184-185)
     const int o = blockIdx.y;
-    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, -1, -1};
+    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (!valid[i]) continue;
         const double v = wv[i * nobj + o] / w.weights[o];
-        if (v < a.mn || a.amn < 0) {
+        if (v != v) {
+            ++a.nan;
+            continue;
+        }
+        if (a.amn < 0 || v < a.mn) {
             a.mn = v;
             a.amn = i;
         }
-        if (v > a.mx || a.amx < 0) {
+        if (a.amx < 0 || v > a.mx) {
             a.mx = v;
             a.amx = i;
         }
+        ++a.cnt;  // Welford step
+        const double d = v - a.mean;
+        a.mean += d / (double)a.cnt;
+        a.m2 += d * (v - a.mean);
         a.sum += v;
-        a.sq += v * v;
     }
     __shared__ StatAcc sh[256];
     sh[threadIdx.x] = a;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            StatAcc& x = sh[threadIdx.x];
-            const StatAcc& y = sh[threadIdx.x + s];
-            // first-occurrence argmin/argmax (numpy semantics): lower index wins ties
-            if (y.amn >= 0 && (x.amn < 0 || y.mn < x.mn || (y.mn == x.mn && y.amn < x.amn))) {
-                x.mn = y.mn;
-                x.amn = y.amn;
-            }
-            if (y.amx >= 0 && (x.amx < 0 || y.mx > x.mx || (y.mx == x.mx && y.amx < x.amx))) {
-                x.mx = y.mx;
-                x.amx = y.amx;
-            }
-            x.sum += y.sum;
-            x.sq += y.sq;
-        }
+        if (threadIdx.x < s) stat_merge(sh[threadIdx.x], sh[threadIdx.x + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        double* p = part + ((int64_t)o * nparts + blockIdx.x) * 6;
-        p[0] = sh[0].mn;
-        p[1] = sh[0].mx;
-        p[2] = sh[0].sum;
-        p[3] = sh[0].sq;
-        p[4] = (double)sh[0].amn;
-        p[5] = (double)sh[0].amx;
-    }
+    if (threadIdx.x == 0) part[(int64_t)o * nparts + blockIdx.x] = sh[0];
 }
-__global__ void stats_combine_kernel(const double* part, int64_t nparts, int nobj, double* out) {
+__global__ void stats_combine_kernel(const StatAcc* part, int64_t nparts, int nobj, double* out) {
     const int o = threadIdx.x;
     if (o >= nobj) return;
-    double mn = INFINITY, mx = -INFINITY, sum = 0, sq = 0, amn = -1, amx = -1;
-    for (int64_t b = 0; b < nparts; ++b) {  // in block order: deterministic
-        const double* p = part + ((int64_t)o * nparts + b) * 6;
-        if (p[4] >= 0 && (amn < 0 || p[0] < mn)) {
-            mn = p[0];
-            amn = p[4];
-        }
-        if (p[5] >= 0 && (amx < 0 || p[1] > mx)) {
-            mx = p[1];
-            amx = p[5];
-        }
-        sum += p[2];
-        sq += p[3];
-    }
-    double* q = out + o * 6;
-    q[0] = mn;
-    q[1] = mx;
-    q[2] = sum;
-    q[3] = sq;
-    q[4] = amn;
-    q[5] = amx;
+    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0};
+    for (int64_t b = 0; b < nparts; ++b) stat_merge(a, part[(int64_t)o * nparts + b]);  // block order
+    double* q = out + o * 8;
+    const double qnan = __longlong_as_double(0x7FF8000000000000ll);
+    const bool nan = a.nan > 0;
+    q[0] = nan ? qnan : a.mn;
+    q[1] = nan ? qnan : a.mx;
+    q[2] = nan || a.cnt == 0 ? qnan : a.mean;
+    q[3] = nan || a.cnt == 0 ? qnan : a.m2;
+    q[4] = nan ? qnan : a.sum;
+    q[5] = (double)a.amn;
+    q[6] = (double)a.amx;
+    q[7] = (double)(a.cnt + a.nan);
 }
 
 }  // namespace dm
@@ -472,7 +473,18 @@ int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count) {
 
 int dm_ctx_set_stream(dm_ctx* ctx, void* hip_stream) {
     DM_CHECK_ARG(ctx != nullptr, "null ctx");
-    ctx->stream = (hipStream_t)hip_stream;
+    hipStream_t next = (hipStream_t)hip_stream;
+    if (next != ctx->stream) {
+        // The scratch slots are reused by the next launch on the new stream:
+        // order it after everything already queued on the old one.
+        hipEvent_t e;
+        DM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        hipError_t err = hipEventRecord(e, ctx->stream);
+        if (err == hipSuccess) err = hipStreamWaitEvent(next, e, 0);
+        (void)hipEventDestroy(e);
+        DM_HIP(err);
+    }
+    ctx->stream = next;
     return DM_OK;
 }
 
@@ -624,8 +636,8 @@ int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights, doub
         DM_CHECK_ARG(weights[o] != 0.0, "zero fitness weight");
         w.weights[o] = weights[o];
     }
-    const int64_t nparts = std::min<int64_t>(std::max<int64_t>((pop->n + 4095) / 4096, 1), 512);
-    double* part = (double*)scratch(ctx, (size_t)nparts * pop->nobj * 6 * sizeof(double));
+    const int64_t nparts = std::min<int64_t>(std::max<int64_t>((pop->n + 4095) / 4096, 1), 1024);
+    StatAcc* part = (StatAcc*)scratch(ctx, (size_t)nparts * pop->nobj * sizeof(StatAcc));
     if (!part) return DM_ERR_NOMEM;
     stats_kernel<<<dim3((unsigned)nparts, pop->nobj), 256, 0, ctx->stream>>>(
         pop->wvalues, pop->valid, pop->n, pop->nobj, w, part, nparts);

@@ -77,7 +77,8 @@ inline void timing_end(dm_ctx* ctx) {
 namespace dm {
 // Grow-only scratch arenas; returns nullptr on failure (error set).  Growing
 // a slot discards its contents.  Slot 0 = general temporaries, 1 = NSGA-II
-// dominance matrix, 2 = NSGA-II order buffers, 3 = migration.
+// dominance matrix, 2 = NSGA-II order buffers, 3 = migration placement,
+// 4 = migration emigrant / immigrant / receive blocks.
 void* scratch_slot(dm_ctx* ctx, int slot, size_t bytes);
 inline void* scratch(dm_ctx* ctx, size_t bytes) { return scratch_slot(ctx, 0, bytes); }
 void* pinned(dm_ctx* ctx, size_t bytes);
@@ -107,6 +108,7 @@ enum Stage : uint32_t {
     ST_SBX = 12,       // cxSimulatedBinaryBounded per gene: item = pair, sub = gene
                        // (| 1 << 24 for the swap coin)
     ST_POLY = 13,      // mutPolynomialBounded per gene: item = child, sub = gene
+    ST_SAMPLE = 14,    // random.sample: item = attempt (rejection) or row (keys), sub = 0 / 1
 };
 
 struct u32x4 {

@@ -95,6 +95,12 @@ __global__ void match_kernel(const char* genes, const double* wv, const uint8_t*
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         for (int64_t j = 0; j < k; ++j) {
+            // list.index tests `is` before `==` (PyObject_RichCompareBool): the
+            // immigrant's own row matches even when its genome holds a NaN
+            if (r == im.src[j]) {
+                atomicOr(&bitmap[j * words + (r >> 6)], 1ull << (r & 63));
+                continue;
+            }
             if (!fit_prefilter(wv + r * nobj, valid[r], im.wv + j * nobj, im.valid[j], nobj))
                 continue;
             if (genome_eq(genes + r * stride, im.genes + j * stride, gtype, dim))
@@ -124,8 +130,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
                                                       int32_t* content, int32_t* err) {
     Block em = block_view((void*)em_block, stride, nobj, k);
     __shared__ int64_t best;
-    __shared__ int32_t placed_slot[256];
-    __shared__ int32_t placed_em[256];
+    __shared__ int32_t placed_slot[4096];
+    __shared__ int32_t placed_em[4096];
     __shared__ int nplaced;
     if (threadIdx.x == 0) nplaced = 0;
     __syncthreads();
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
                 best = slot;
                 slots[j] = (int32_t)slot;
                 content[slot] = (int32_t)j;
-                if (nplaced < 256) {
+                if (nplaced < 4096) {
                     placed_slot[nplaced] = (int32_t)slot;
                     placed_em[nplaced] = (int32_t)j;
                     ++nplaced;
@@ -242,5 +248,299 @@ extern "C" int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_bloc
     DM_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
     DM_CHECK_ARG(herr == 0, "migRing: immigrant %d is not in the receiving population", herr - 1);
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// random.sample(range(n), k) on the device (migRing's `replacement`).
+// ---------------------------------------------------------------------------
+namespace dm {
+
+// k <= 4096 and 2k <= n: sequential rejection sampling in one workgroup —
+// candidate a = Philox(SAMPLE, a, 0) mod n (64-bit bounded), rejected when it
+// is already among the accepted ones (the 256 threads test the accepted list
+// in parallel).  Expected attempts <= 2k.
+__global__ __launch_bounds__(256) void sample_reject_kernel(Rng rng, int64_t n, int64_t k,
+                                                            int32_t* out) {
+    __shared__ int32_t acc[4096];
+    __shared__ int dup;
+    int cnt = 0;
+    for (uint32_t a = 0; cnt < k; ++a) {
+        const u32x4 w = rng(ST_SAMPLE, a, 0u);
+        const int32_t c = (int32_t)bounded64(w.x, w.y, (uint32_t)n);
+        if (threadIdx.x == 0) dup = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x)
+            if (acc[i] == c) dup = 1;
+        __syncthreads();
+        if (!dup) {
+            if (threadIdx.x == 0) {
+                acc[cnt] = c;
+                out[cnt] = c;
+            }
+            ++cnt;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void sample_keys_kernel(Rng rng, int64_t n, uint64_t* keys, int32_t* vals) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const u32x4 w = rng(ST_SAMPLE, (uint32_t)i, 1u);
+        keys[i] = ((uint64_t)w.x << 32) | w.y;
+        vals[i] = (int32_t)i;
+    }
+}
+
+}  // namespace dm
+
+#include "sort.hpp"
+
+extern "C" int dm_sel_sample(dm_ctx* ctx, int64_t n, int64_t k, dm_rng rng, int32_t* out_idx) {
+    DM_CHECK_ARG(ctx && out_idx, "null argument");
+    DM_CHECK_ARG(n >= 0 && n < (1ll << 31), "bad population size");
+    if (k < 0 || k > n) {
+        set_error("Sample larger than population or is negative");
+        return DM_ERR_INVALID;
+    }
+    if (k == 0) return DM_OK;
+    hipStream_t s = ctx->stream;
+    if (k <= 4096 && 2 * k <= n) {
+        sample_reject_kernel<<<1, 256, 0, s>>>(Rng(rng), n, k, out_idx);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    // otherwise: the first k rows of a random permutation (Philox keys, stable
+    // radix sort, ties by index)
+    const size_t kb = align_up((size_t)n * 8, 256), vb = align_up((size_t)n * 4, 256);
+    char* w = (char*)scratch(ctx, 2 * kb + 2 * vb + radix_sort_temp_bytes(n));
+    if (!w) return DM_ERR_NOMEM;
+    uint64_t* keys = (uint64_t*)w;
+    uint64_t* ktmp = (uint64_t*)(w + kb);
+    int32_t* vals = (int32_t*)(w + 2 * kb);
+    int32_t* vtmp = (int32_t*)(w + 2 * kb + vb);
+    void* rtemp = w + 2 * kb + 2 * vb;
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    sample_keys_kernel<<<g, 256, 0, s>>>(Rng(rng), n, keys, vals);
+    DM_LAUNCH_CHECK();
+    int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, n, 0, 64, rtemp);
+    if (rc) return rc;
+    DM_HIP(hipMemcpyAsync(out_idx, vals, (size_t)k * 4, hipMemcpyDeviceToDevice, s));
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Whole migRing in one call: local demes (dm_mig_ring) and across ranks over
+// RCCL point-to-point (dm_mig_ring_rccl).
+// ---------------------------------------------------------------------------
+#include <rccl/rccl.h>
+#include <cstring>
+
+struct dm_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+namespace dm {
+
+static int plan_hops(int32_t n_demes, const int32_t* migarray, const int32_t* owner, int32_t me,
+                     int32_t flags, std::vector<dm_mig_hop>& hops) {
+    hops.clear();
+    for (int32_t from = 0; from < n_demes; ++from) {
+        const int32_t to = migarray ? migarray[from] : (from + 1) % n_demes;
+        DM_CHECK_ARG(to >= 0 && to < n_demes, "migarray[%d] = %d is not a deme index", from, to);
+        const int32_t src = owner ? owner[from] : 0, dst = owner ? owner[to] : 0;
+        if (src == me && dst == me) {
+            if ((flags & DM_MIG_FORCE_P2P) && from != to) {
+                hops.push_back(dm_mig_hop{DM_HOP_SEND, from, to, me});
+                hops.push_back(dm_mig_hop{DM_HOP_RECV, from, to, me});
+            } else {
+                hops.push_back(dm_mig_hop{DM_HOP_LOCAL, from, to, me});
+            }
+        } else if (src == me) {
+            hops.push_back(dm_mig_hop{DM_HOP_SEND, from, to, dst});
+        } else if (dst == me) {
+            hops.push_back(dm_mig_hop{DM_HOP_RECV, from, to, src});
+        }
+    }
+    return DM_OK;
+}
+
+#define DM_NCCL(expr)                                                              \
+    do {                                                                           \
+        ncclResult_t r_ = (expr);                                                  \
+        if (r_ != ncclSuccess) {                                                   \
+            ::dm::set_error("RCCL error %s at %s:%d: %s", ncclGetErrorString(r_),  \
+                            __FILE__, __LINE__, #expr);                            \
+            return DM_ERR_HIP;                                                     \
+        }                                                                          \
+    } while (0)
+
+static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
+                         const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
+                         const int32_t* owner, int64_t k, int32_t* const* emig_idx,
+                         int32_t* const* immig_idx, int32_t* const* out_slots, int32_t flags) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    DM_CHECK_ARG(n_demes >= 1 && n_local >= 0 && n_local <= n_demes, "bad deme counts");
+    DM_CHECK_ARG(n_local == 0 || (demes && deme_ids && emig_idx), "null deme arrays");
+    DM_CHECK_ARG(k >= 0 && k <= 4096, "k must be in [0, 4096]");
+    const int me = comm ? comm->rank : 0;
+    // local index of every global deme held here
+    std::vector<int32_t> local_of(n_demes, -1);
+    for (int32_t i = 0; i < n_local; ++i) {
+        DM_CHECK_ARG(deme_ids[i] >= 0 && deme_ids[i] < n_demes, "deme id %d out of range",
+                     deme_ids[i]);
+        DM_CHECK_ARG(local_of[deme_ids[i]] < 0, "deme %d listed twice", deme_ids[i]);
+        if (owner) DM_CHECK_ARG(owner[deme_ids[i]] == me, "deme %d is not owned by rank %d",
+                                deme_ids[i], me);
+        local_of[deme_ids[i]] = i;
+        int rc = validate_pop(&demes[i], "deme");
+        if (rc) return rc;
+        DM_CHECK_ARG(emig_idx[i] != nullptr || k == 0, "null emigrant indices");
+        DM_CHECK_ARG(k <= demes[i].n, "k exceeds deme size");
+    }
+    if (owner)
+        for (int32_t d = 0; d < n_demes; ++d)
+            DM_CHECK_ARG(owner[d] >= 0 && (!comm || owner[d] < comm->nranks), "bad owner[%d]", d);
+    if (!owner) DM_CHECK_ARG(n_local == n_demes, "without owner every deme must be local");
+    std::vector<dm_mig_hop> hops;
+    int rc = plan_hops(n_demes, migarray, owner, me, flags, hops);
+    if (rc) return rc;
+    if (k == 0 || n_local == 0) return DM_OK;
+    // every deme shares one layout (the blocks travel between them)
+    for (int32_t i = 1; i < n_local; ++i)
+        DM_CHECK_ARG(demes[i].stride == demes[0].stride && demes[i].dim == demes[0].dim &&
+                         demes[i].gtype == demes[0].gtype && demes[i].nobj == demes[0].nobj,
+                     "demes differ in layout");
+    const size_t bb = align_up((size_t)block_bytes(&demes[0], k), 256);
+    int nrecv = 0;
+    for (const dm_mig_hop& h : hops) nrecv += h.kind == DM_HOP_RECV;
+    // [emigrant block | immigrant block] per local deme, then one per receive
+    char* base = (char*)scratch_slot(ctx, 4, bb * (2 * (size_t)n_local + nrecv));
+    if (!base) return DM_ERR_NOMEM;
+    hipStream_t s = ctx->stream;
+    std::vector<char*> emig(n_local), immig(n_local);
+    // migration.py:39-46: every deme's emigrants / immigrants first
+    for (int32_t i = 0; i < n_local; ++i) {
+        emig[i] = base + 2 * (size_t)i * bb;
+        if ((rc = dm_pack_rows(ctx, &demes[i], emig_idx[i], k, emig[i]))) return rc;
+        if (immig_idx && immig_idx[i]) {
+            immig[i] = emig[i] + bb;
+            if ((rc = dm_pack_rows(ctx, &demes[i], immig_idx[i], k, immig[i]))) return rc;
+        } else {
+            immig[i] = emig[i];
+        }
+    }
+    // exchange: the incoming block of every hop into a local deme
+    std::vector<char*> incoming(hops.size(), nullptr);
+    const bool p2p = std::any_of(hops.begin(), hops.end(),
+                                 [](const dm_mig_hop& h) { return h.kind != DM_HOP_LOCAL; });
+    if (p2p) {
+        DM_CHECK_ARG(comm != nullptr, "cross-rank hops need an RCCL communicator");
+        const size_t bytes = (size_t)block_bytes(&demes[0], k);
+        char* rb = base + 2 * (size_t)n_local * bb;
+        DM_NCCL(ncclGroupStart());
+        for (size_t h = 0; h < hops.size(); ++h) {
+            const dm_mig_hop& hp = hops[h];
+            if (hp.kind == DM_HOP_SEND) {
+                DM_NCCL(ncclSend(emig[local_of[hp.from]], bytes, ncclUint8, hp.peer, comm->comm, s));
+            } else if (hp.kind == DM_HOP_RECV) {
+                incoming[h] = rb;
+                rb += bb;
+                DM_NCCL(ncclRecv(incoming[h], bytes, ncclUint8, hp.peer, comm->comm, s));
+            }
+        }
+        DM_NCCL(ncclGroupEnd());
+    }
+    for (size_t h = 0; h < hops.size(); ++h)
+        if (hops[h].kind == DM_HOP_LOCAL) incoming[h] = emig[local_of[hops[h].from]];
+    // migration.py:48-51: placements in from_deme order
+    for (size_t h = 0; h < hops.size(); ++h) {
+        if (!incoming[h]) continue;
+        const int32_t t = local_of[hops[h].to];
+        int32_t* slots = out_slots && out_slots[t] ? out_slots[t] : nullptr;
+        if (!slots) {
+            slots = (int32_t*)scratch(ctx, (size_t)k * 4);
+            if (!slots) return DM_ERR_NOMEM;
+        }
+        if ((rc = dm_mig_place(ctx, &demes[t], immig[t], incoming[h], k, slots))) return rc;
+    }
+    return DM_OK;
+}
+
+}  // namespace dm
+
+extern "C" int dm_mig_plan(int32_t n_demes, const int32_t* migarray, const int32_t* owner,
+                           int32_t me, int32_t flags, dm_mig_hop* hops, int32_t cap,
+                           int32_t* nhops) {
+    DM_CHECK_ARG(nhops != nullptr && n_demes >= 1 && cap >= 0 && (hops || cap == 0),
+                 "bad argument");
+    std::vector<dm_mig_hop> v;
+    int rc = plan_hops(n_demes, migarray, owner, me, flags, v);
+    if (rc) return rc;
+    *nhops = (int32_t)v.size();
+    DM_CHECK_ARG((int32_t)v.size() <= cap, "hop buffer too small (%d needed)", (int)v.size());
+    std::copy(v.begin(), v.end(), hops);
+    return DM_OK;
+}
+
+extern "C" int dm_mig_ring(dm_ctx* ctx, int32_t n_demes, dm_pop* demes, const int32_t* migarray,
+                           int64_t k, int32_t* const* emig_idx, int32_t* const* immig_idx,
+                           int32_t* const* out_slots) {
+    DM_CHECK_ARG(n_demes >= 1 && n_demes <= 65536, "bad deme count");
+    std::vector<int32_t> ids(n_demes);
+    for (int32_t i = 0; i < n_demes; ++i) ids[i] = i;
+    return mig_ring_impl(ctx, nullptr, n_demes, demes, ids.data(), n_demes, migarray, nullptr, k,
+                         emig_idx, immig_idx, out_slots, 0);
+}
+
+extern "C" int dm_mig_ring_rccl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
+                                const int32_t* deme_ids, int32_t n_demes,
+                                const int32_t* migarray, const int32_t* owner, int64_t k,
+                                int32_t* const* emig_idx, int32_t* const* immig_idx,
+                                int32_t* const* out_slots, int32_t flags) {
+    DM_CHECK_ARG(comm != nullptr && owner != nullptr, "null comm / owner");
+    return mig_ring_impl(ctx, comm, n_local, demes, deme_ids, n_demes, migarray, owner, k,
+                         emig_idx, immig_idx, out_slots, flags);
+}
+
+extern "C" int dm_comm_get_unique_id(uint8_t* id_out) {
+    DM_CHECK_ARG(id_out != nullptr, "null id");
+    static_assert(sizeof(ncclUniqueId) == DM_COMM_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    DM_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return DM_OK;
+}
+
+extern "C" int dm_comm_init(dm_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id,
+                            dm_comm** out) {
+    DM_CHECK_ARG(ctx && id && out, "null argument");
+    DM_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d of %d", rank, nranks);
+    DM_HIP(hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    dm_comm* c = new dm_comm();
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        set_error("ncclCommInitRank failed: %s", ncclGetErrorString(r));
+        delete c;
+        return DM_ERR_HIP;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    *out = c;
+    return DM_OK;
+}
+
+extern "C" int dm_comm_destroy(dm_comm* comm) {
+    if (!comm) return DM_OK;
+    ncclResult_t r = comm->comm ? ncclCommDestroy(comm->comm) : ncclSuccess;
+    delete comm;
+    if (r != ncclSuccess) {
+        set_error("ncclCommDestroy failed: %s", ncclGetErrorString(r));
+        return DM_ERR_HIP;
+    }
     return DM_OK;
 }

@@ -54,8 +54,12 @@ class _SortNondominated(DeviceOperator):
 
     def __call__(self, individuals, k, first_front_only=False):
         _check(individuals)
-        if k == 0 or len(individuals) == 0:
+        if k == 0:
             return []
+        if len(individuals) == 0:
+            # the reference builds `fronts = [[]]` before any peel (emo.py:96-117)
+            torch = _torch()
+            return [torch.empty((0,), dtype=torch.int32, device=individuals.device)]
         order, fstart, _rank, _ns, nf = _sort(individuals, k, first_front_only)
         bounds = fstart[: nf + 1].cpu().tolist()
         return [order[bounds[f]:bounds[f + 1]] for f in range(nf)]
@@ -193,6 +197,9 @@ class _SelTournamentDCD(DeviceOperator):
             raise AttributeError("'Fitness' object has no attribute 'crowding_dist'")
         stream = stream or default_stream()
         n, k = len(individuals), int(k)
+        if len(individuals.crowding_dist) < n:
+            raise ValueError("crowding_dist holds %d values for %d individuals"
+                             % (len(individuals.crowding_dist), n))
         k4 = (k + 3) // 4 * 4
         dev = individuals.device
         out = torch.empty((max(k4, 1),), dtype=torch.int32, device=dev)
@@ -203,6 +210,24 @@ class _SelTournamentDCD(DeviceOperator):
                 decisions["perm1"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
                 decisions["perm2"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
                 decisions["coin"] = torch.zeros((max(k4, 1),), dtype=torch.uint8, device=dev)
+            else:
+                # injected decisions: device tensors of the kernel's dtypes, long
+                # enough, and permutations of range(n) (the kernel dereferences
+                # fitness rows through them)
+                decisions = dict(decisions)
+                for name, dt, need in (("perm1", torch.int32, n), ("perm2", torch.int32, n),
+                                       ("coin", torch.uint8, k4)):
+                    t = torch.as_tensor(decisions[name]).to(device=dev, dtype=dt).contiguous()
+                    if t.numel() < need:
+                        raise ValueError("decisions[%r] holds %d values, %d needed"
+                                         % (name, t.numel(), need))
+                    decisions[name] = t
+                for name in ("perm1", "perm2"):
+                    p = decisions[name][:n]
+                    if n and not bool(torch.equal(torch.sort(p).values,
+                                                  torch.arange(n, dtype=torch.int32, device=dev))):
+                        raise ValueError("decisions[%r] is not a permutation of range(%d)"
+                                         % (name, n))
             p1, p2, coin = decisions["perm1"], decisions["perm2"], decisions["coin"]
         ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
         ctx = individuals.ctx.bind()

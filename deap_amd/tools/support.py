@@ -7,8 +7,10 @@ HallOfFame, with device-side reductions for :class:`DevicePopulation` inputs.
   flush; any other registered function receives the host values exactly as in
   the reference (``support.py:199-210``).
 * ``HallOfFame.update`` keeps the reference's insertion semantics
-  (``support.py:517-560``); with ``maxsize == 1`` the device computes the
-  first lexicographic argmax, otherwise the candidates are materialised.
+  (``support.py:517-560``).  With value-equality ``similar`` (the default
+  ``operator.eq`` or ``numpy.array_equal``) only a candidate set of the best
+  rows (device ``selBest``) is materialised; any other ``similar`` walks the
+  whole population on the host, as the reference does.
 """
 import bisect
 import copy
@@ -89,21 +91,71 @@ class Statistics:
             inds = pop.to_individuals()
             values = tuple(self.key(ind) for ind in inds)
             return {name: fn(values) for name, fn in self.functions.items()}
-        vals = pop.fitness_values()
         out = {}
         host = None
+        vals = None
+        kstats = None
         for name, fn in self.functions.items():
-            red = _device_reducer(fn.func)
             kw = dict(fn.keywords or {})
             axis = kw.pop("axis", None)
+            pick = _KERNEL_STATS.get(fn.func)
+            if pick is not None and not fn.args and not kw and \
+                    (axis == 0 or (axis is None and pop.nobj == 1)):
+                # one dm_fitness_stats pass serves every such reducer
+                if kstats is None:
+                    kstats = _KernelStats(pop)
+                out[name] = functools.partial(kstats.value, pick, axis)
+                continue
+            red = _device_reducer(fn.func)
             if red is not None and not fn.args and not kw:
-                t = red(vals, axis)
-                out[name] = functools.partial(_to_numpy, t)
+                if vals is None:
+                    vals = pop.fitness_values()
+                out[name] = functools.partial(_to_numpy, red(vals, axis))
             else:
                 if host is None:
-                    host = tuple(tuple(r) for r in vals.cpu().numpy().tolist())
+                    host = tuple(tuple(r) for r in pop.fitness_values().cpu().numpy().tolist())
                 out[name] = fn(host)
         return out
+
+
+# numpy reducer -> value from a dm_fitness_stats row
+# {min, max, mean, m2, sum, argmin, argmax, count} (include/deapmi.h)
+_KERNEL_STATS = {
+    np.min: lambda r: r[0], np.amin: lambda r: r[0], np.max: lambda r: r[1],
+    np.amax: lambda r: r[1], np.mean: lambda r: r[2], np.sum: lambda r: r[4],
+    np.var: lambda r: r[3] / r[7] if r[7] else np.float64("nan"),
+    np.std: lambda r: np.sqrt(r[3] / r[7]) if r[7] else np.float64("nan"),
+    np.argmin: lambda r: np.int64(r[5]), np.argmax: lambda r: np.int64(r[6]),
+}
+
+
+class _KernelStats:
+    """One asynchronous ``dm_fitness_stats`` launch; the host copy happens on
+    the first value read (the logbook flush), not in the generation loop."""
+
+    def __init__(self, pop):
+        import torch
+        from .. import _lib
+        self.nobj = pop.nobj
+        self.out = torch.empty((pop.nobj * 8,), dtype=torch.float64, device=pop.device)
+        w = (ctypes.c_double * pop.nobj)(*pop.weights)
+        _lib.call("dm_fitness_stats", pop.ctx.bind(), ctypes.byref(pop.c_pop()), w,
+                  ctypes.c_void_p(self.out.data_ptr()))
+        self._host = None
+
+    def rows(self):
+        if self._host is None:
+            self._host = self.out.cpu().numpy().reshape(self.nobj, 8)
+        return self._host
+
+    def value(self, pick, axis):
+        rows = self.rows()
+        if axis is None:
+            return np.float64(pick(rows[0])) if pick not in _INT_PICKS else pick(rows[0])
+        return np.array([pick(r) for r in rows])
+
+
+_INT_PICKS = (_KERNEL_STATS[np.argmin], _KERNEL_STATS[np.argmax])
 
 
 def _to_numpy(t):
@@ -131,18 +183,22 @@ class MultiStatistics(dict):
 
 # ---------------------------------------------------------------------------
 # Logbook (deap/tools/support.py:261-487): chronological list of dict records
-# with chapters (dict-valued fields) and an incremental text stream.
+# with chapters (dict-valued fields) and an incremental text stream whose
+# layout is the reference's character for character (pinned by
+# tests/golden/support.npz, generated by the reference itself).
 # ---------------------------------------------------------------------------
 class Logbook(list):
     def __init__(self):
         super().__init__()
         self.buffindex = 0
         self.chapters = defaultdict(Logbook)
+        self.columns_len = None
         self.header = None
         self.log_header = True
-        self._widths = {}
 
     def record(self, **infos):
+        """Append one record; dict-valued fields go to the chapter of that
+        name together with every non-dict field (support.py:335-349)."""
         shared = {k: v for k, v in infos.items() if not isinstance(v, dict)}
         flat = {}
         for key, value in infos.items():
@@ -163,50 +219,76 @@ class Logbook(list):
         start, self.buffindex = self.buffindex, len(self)
         return self.__str__(start)
 
+    def __delitem__(self, key):
+        idx = range(*key.indices(len(self))) if isinstance(key, slice) else [key]
+        for i in sorted(idx, reverse=True):
+            self.pop(i)
+            for chapter in self.chapters.values():
+                chapter.pop(i)
+
     def pop(self, index=0):
         if index < self.buffindex:
             self.buffindex -= 1
         return super().pop(index)
 
-    def _columns(self):
-        if self.header:
-            return list(self.header)
-        keys = sorted(self[0].keys()) if self else []
-        return keys + sorted(self.chapters.keys())
-
     @staticmethod
-    def _fmt(value):
-        return "{0:n}".format(value) if isinstance(value, float) else str(value)
+    def _cell(value):
+        # floats (numpy float64 included) use the locale-aware general format
+        return "{0:n}".format(value) if isinstance(value, float) else "{0}".format(value)
 
-    def _cells(self, row, cols):
-        out = []
-        for name in cols:
-            if name in self.chapters:
-                chap = self.chapters[name]
-                ccols = chap._columns()
-                crow = chap[row] if row < len(chap) else {}
-                out.append(" ".join(self._fmt(crow.get(c, "")) for c in ccols))
-            else:
-                out.append(self._fmt(self[row].get(name, "")))
-        return out
+    def _lines(self, start):
+        """Text lines from record ``start`` on (with the header block when
+        ``start == 0``); column widths only ever grow (columns_len)."""
+        cols = list(self.header) if self.header else \
+            sorted(self[0].keys()) + sorted(self.chapters.keys())
+        if not self.columns_len or len(self.columns_len) != len(cols):
+            self.columns_len = [len(c) for c in cols]
+        chap = {name: ch._lines(start) for name, ch in self.chapters.items()}
+        # a chapter's lines start with its own header block at start == 0
+        skip = {name: (len(t) - len(self) if start == 0 else 0) for name, t in chap.items()}
+        rows = []
+        for i, entry in enumerate(self[start:]):
+            row = []
+            for j, name in enumerate(cols):
+                cell = chap[name][i + skip[name]] if name in chap else \
+                    self._cell(entry.get(name, ""))
+                self.columns_len[j] = max(self.columns_len[j], len(cell))
+                row.append(cell)
+            rows.append(row)
+        if start == 0 and self.log_header:
+            depth = 1
+            if self.chapters:
+                depth += max(len(t) for t in chap.values()) - len(self) + 1
+            head = [[] for _ in range(depth)]
+            for j, name in enumerate(cols):
+                if name in chap:
+                    width = max(len(line.expandtabs()) for line in chap[name])
+                    pad = depth - 2 - skip[name]
+                    for i in range(pad):
+                        head[i].append(" " * width)
+                    head[pad].append(name.center(width))
+                    head[pad + 1].append("-" * width)
+                    for i in range(skip[name]):
+                        head[pad + 2 + i].append(chap[name][i])
+                else:
+                    width = max(len(r[j].expandtabs()) for r in rows)
+                    for line in head[:-1]:
+                        line.append(" " * width)
+                    head[-1].append(name)
+            rows = head + rows
+        fmt = "\t".join("{%d:<%d}" % (i, w) for i, w in enumerate(self.columns_len))
+        return [fmt.format(*r) for r in rows]
 
     def __str__(self, startindex=0):
-        cols = self._columns()
-        rows = [self._cells(i, cols) for i in range(startindex, len(self))]
-        for j, name in enumerate(cols):
-            w = max([len(name)] + [len(r[j]) for r in rows])
-            self._widths[name] = max(self._widths.get(name, 0), w)
-        lines = []
-        if startindex == 0 and self.log_header:
-            lines.append("\t".join(n.ljust(self._widths[n]) for n in cols))
-        for r in rows:
-            lines.append("\t".join(c.ljust(self._widths[n]) for c, n in zip(r, cols)))
-        return "\n".join(lines)
+        return "\n".join(self._lines(startindex))
 
 
 # ---------------------------------------------------------------------------
 # HallOfFame (deap/tools/support.py:490-588)
 # ---------------------------------------------------------------------------
+_VALUE_SIMILAR = (operator.eq, np.array_equal)
+
+
 class HallOfFame:
     def __init__(self, maxsize, similar=operator.eq):
         self.maxsize = maxsize
@@ -234,15 +316,23 @@ class HallOfFame:
         n = len(pop)
         if n == 0 or self.maxsize == 0:
             return
-        # maxsize 1 too: a first-argmax shortcut is wrong when the argmax is
-        # similar to the hofer but a lesser non-similar row beats the hofer
-        self._update_candidates(pop)
+        if self.similar in _VALUE_SIMILAR:
+            # maxsize 1 too: a first-argmax shortcut is wrong when the argmax is
+            # similar to the hofer but a lesser non-similar row beats the hofer
+            self._update_candidates(pop)
+            return
+        # a user `similar` may match rows of different fitness; the candidate
+        # argument below does not hold then, so walk the whole population
+        rows = list(range(n))
+        self._loop(rows, dict(zip(rows, pop.to_individuals())))
 
     def _update_candidates(self, pop):
         """HallOfFame.update for any maxsize / similar without copying the
         population: the reference loop (support.py:528-548) runs on host over a
         candidate set C = the K best rows (device selBest: wvalues desc, index
-        asc) in population order.  With t the fitness of the K-th row, the loop
+        asc) in population order.  Used only when ``similar`` is value equality
+        (``operator.eq`` / ``numpy.array_equal``), which matches rows of equal
+        genome and therefore equal fitness.  With t the fitness of the K-th row, the loop
         is accepted once it leaves a full hall whose every entry is strictly
         better than t (else K grows): a row outside C (fitness <= t) is then
         never in the final hall — it would be the worst entry when a better

@@ -301,10 +301,74 @@ int64_t dm_pack_bytes(const dm_pop* pop, int64_t k);
 int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
                  const void* emigrant_block, int64_t k, int32_t* out_slots);
 
+/* random.sample(population, k) as migRing's `replacement`
+ * (examples/ga/onemax_multidemic.py:46-47, migration.py:42-44): out_idx[k]
+ * (device) = k distinct row indices of [0, n) in draw order, from the
+ * counter-based RNG (stage SAMPLE).  k > n is DM_ERR_INVALID (the reference's
+ * "Sample larger than population" ValueError). */
+int dm_sel_sample(dm_ctx* ctx, int64_t n, int64_t k, dm_rng rng, int32_t* out_idx);
+
+/* The hops of one migRing (migration.py:34,48-51: from_deme ->
+ * migarray[from_deme], in from_deme order) as seen by rank `me`, given
+ * owner[d] = rank holding deme d.  Host-only (no device work): hops[i] =
+ * {kind, from, to, peer} with kind DM_HOP_LOCAL (both demes on `me`),
+ * DM_HOP_SEND (from on `me`, to on peer) or DM_HOP_RECV (to on `me`, from on
+ * peer); hops involving neither side are skipped.  flags & DM_MIG_FORCE_P2P
+ * turns every local hop between two different demes into a send/recv pair
+ * to `me` itself (exercises the RCCL data path on one GPU). */
+enum dm_hop_kind { DM_HOP_LOCAL = 0, DM_HOP_SEND = 1, DM_HOP_RECV = 2 };
+enum dm_mig_flags { DM_MIG_FORCE_P2P = 1 };
+typedef struct dm_mig_hop {
+    int32_t kind, from, to, peer;
+} dm_mig_hop;
+int dm_mig_plan(int32_t n_demes, const int32_t* migarray, const int32_t* owner, int32_t me,
+                int32_t flags, dm_mig_hop* hops, int32_t cap, int32_t* nhops);
+
+/* migRing(populations, k, selection, replacement, migarray) over the demes
+ * held by this process (migration.py:4-51), whole migration in one call:
+ * every local deme's emigrants (rows emig_idx[i][0..k), the result of
+ * `selection`) and immigrants (rows immig_idx[i][0..k) = `replacement`, or
+ * the emigrants when immig_idx or immig_idx[i] is NULL) are packed first;
+ * then the blocks move along migarray (NULL = ring d -> d+1) and each
+ * receiving deme applies the sequential list.index placement (dm_mig_place)
+ * in from_deme order.  Host arrays: demes[n_local], deme_ids[n_local] (global
+ * ids), emig_idx/immig_idx/out_slots[n_local] of device pointers (out_slots
+ * may be NULL; else out_slots[i] receives the k slots written into local deme
+ * i by its last incoming hop).  dm_mig_ring: every deme is local
+ * (deme_ids = 0..n_demes-1).  Host-synchronising. */
+int dm_mig_ring(dm_ctx* ctx, int32_t n_demes, dm_pop* demes, const int32_t* migarray,
+                int64_t k, int32_t* const* emig_idx, int32_t* const* immig_idx,
+                int32_t* const* out_slots);
+
+/* ---- RCCL communicator for islands across GPUs -------- */
+/* One process per GPU; rank 0 creates the unique id and shares its
+ * DM_COMM_ID_BYTES bytes out of band (the Python layer broadcasts them over
+ * torch.distributed); every rank then calls dm_comm_init collectively. */
+#define DM_COMM_ID_BYTES 128
+typedef struct dm_comm dm_comm;
+int dm_comm_get_unique_id(uint8_t* id_out);
+int dm_comm_init(dm_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id, dm_comm** out);
+int dm_comm_destroy(dm_comm* comm);
+/* dm_mig_ring across ranks: owner[n_demes] (host) gives each deme's rank;
+ * this rank holds demes[n_local] with global ids deme_ids[n_local].  Cross-
+ * rank hops are grouped ncclSend / ncclRecv of the packed emigrant blocks
+ * (ncclGroupStart/End, RCCL point-to-point over xGMI) on the ctx stream;
+ * placement is local to the receiver.  Must be called by every rank with the
+ * same n_demes / migarray / owner / k.  flags: DM_MIG_FORCE_P2P. */
+int dm_mig_ring_rccl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
+                     const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
+                     const int32_t* owner, int64_t k, int32_t* const* emig_idx,
+                     int32_t* const* immig_idx, int32_t* const* out_slots, int32_t flags);
+
 /* ---- statistics (tools.Statistics / Logbook helpers) --------------------- */
-/* Per objective j: out[j*6 + {0..5}] = {min, max, sum, sumsq, argmin, argmax}
- * of fitness.values (= wvalues / weights) over valid rows (device doubles).
- * weights: host [nobj]. */
+/* tools.Statistics(key=lambda ind: ind.fitness.values) reductions
+ * (support.py:199-210) in one pass: per objective j, out[j*8 + {0..7}] =
+ * {min, max, mean, m2, sum, argmin, argmax, count} of fitness.values
+ * (= wvalues / weights, base.py:184-185) over valid rows, device doubles;
+ * m2 = sum of squared deviations from the mean (np.var = m2 / count,
+ * np.std = sqrt(np.var)), combined pairwise (Chan et al.); argmin / argmax
+ * are first occurrences; a NaN value makes min / max / mean / m2 / sum NaN
+ * as numpy's reducers do.  weights: host [nobj].  Asynchronous. */
 int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                      double* out);
 

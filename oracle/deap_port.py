@@ -178,9 +178,16 @@ def ea_simple_generations(pop, evaluate, mate, mutate, select, cxpb, mutpb, ngen
     return pop
 
 
-def run(problem="rastrigin", n=4096, dim=1000, ngen=2, workers=None, seed=1):
-    """Time ``ngen`` eaSimple generations (cxpb 0.5, mutpb 0.2, tournsize 3)
-    of the reference's CPU path.  Returns (ind-gen/s, seconds, workers)."""
+def evolve(problem="rastrigin", n=4096, dim=1000, ngen=2, workers=None, seed=1,
+           time_gen0=False):
+    """Seed the stdlib ``random``, build the population as the reference's
+    ``toolbox.population`` would (initRepeat of ``random.uniform`` /
+    ``random.randint`` per gene), evaluate it and run ``ngen`` eaSimple
+    generations (cxpb 0.5, mutpb 0.2, tournsize 3; algorithms.py:149-181).
+    Returns (population, seconds of the timed generations, workers); with
+    ``time_gen0`` the timed region also covers the generation-0 evaluation,
+    as timing a whole ``eaSimple`` call does (calibration against the
+    reference)."""
     random.seed(seed)
     if problem == "onemax":
         pop = [IndBits(random.randint(0, 1) for _ in range(dim)) for _ in range(n)]
@@ -200,13 +207,22 @@ def run(problem="rastrigin", n=4096, dim=1000, ngen=2, workers=None, seed=1):
         pool = multiprocessing.Pool(workers)
         mapper = pool.map
     try:
+        t0 = time.perf_counter()
         for ind, fit in zip(pop, mapper(evaluate, pop)):
             ind.fitness.values = fit
-        t0 = time.perf_counter()
+        if not time_gen0:
+            t0 = time.perf_counter()
         ea_simple_generations(pop, evaluate, mate, mutate, select, 0.5, 0.2, ngen, mapper)
         dt = time.perf_counter() - t0
     finally:
         if pool is not None:
             pool.close()
             pool.join()
-    return n * ngen / dt, dt, (workers or 1)
+    return pop, dt, (workers or 1)
+
+
+def run(problem="rastrigin", n=4096, dim=1000, ngen=2, workers=None, seed=1):
+    """Time ``ngen`` eaSimple generations of the reference's CPU path.
+    Returns (ind-gen/s, seconds, workers)."""
+    _pop, dt, used = evolve(problem, n, dim, ngen, workers, seed)
+    return n * ngen / dt, dt, used

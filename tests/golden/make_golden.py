@@ -669,6 +669,246 @@ def gen_c1_trajectory(D):
     return out
 
 
+def gen_selrandom(D, rng):
+    """selRandom (selection.py:12-24) with replayed random.choice draws, and one
+    eaSimple generation with toolbox.select = selRandom (the fused
+    DM_SEL_RANDOM path of dm_generation)."""
+    tools = D["deap.tools"]
+    algorithms = D["deap.algorithms"]
+    base = D["deap.base"]
+    bm = D["deap.benchmarks"]
+    out = {}
+    for j, (n, k) in enumerate([(50, 50), (17, 40), (1000, 7)]):
+        Ind = make_types(D, "d", (1.0,))
+        pop = to_inds(Ind, rng.uniform(0, 1, size=(n, 3)), rng.uniform(0, 1, size=(n, 1)))
+        idx = rng.integers(0, n, size=k)
+        with Replay(choices=[int(a) for a in idx]):
+            chosen = tools.selRandom(pop, k)
+        out["sr%d_n" % j] = np.array(n)
+        out["sr%d_choice" % j] = idx
+        out["sr%d_out" % j] = np.array([next(i for i, p in enumerate(pop) if p is c)
+                                        for c in chosen])
+    cases = [("f64", "d", 200, 24, "blend", "gaussian", "rastrigin", (-1.0,)),
+             ("bits", "b", 300, 31, "twopoint", "flipbit", "onemax", (1.0,))]
+    for j, (gt, tc, dim, n, cx, mut, objective, weights) in enumerate(cases):
+        Ind = make_types(D, tc, weights)
+        genes = (rng.integers(0, 2, size=(n, dim)).astype(np.uint8) if gt == "bits"
+                 else rng.uniform(-5.12, 5.12, size=(n, dim)))
+        evalf = (lambda ind: (sum(ind),)) if objective == "onemax" else getattr(bm, objective)
+        pop = to_inds(Ind, genes)
+        for ind in pop:
+            ind.fitness.values = evalf(ind)
+        genes0, wv0, valid0 = from_inds(pop, genes.dtype, 1)
+        cxpb, mutpb, indpb, alpha = 0.5, 0.2, 0.05, 0.5
+        asp = rng.integers(0, n, size=(n, 1))
+        npairs = n // 2
+        cx_flag = rng.random(npairs) < cxpb
+        cx_raw = np.stack([rng.integers(1, dim + 1, npairs), rng.integers(1, dim, npairs)], 1)
+        blend_u = rng.random((npairs, dim))
+        mut_flag = rng.random(n) < mutpb
+        mask = rng.random((n, dim)) < indpb
+        gauss = rng.normal(0.0, 1.0, size=(n, dim))
+        floats, ints, gausses = [], [], []
+        for p in range(npairs):
+            floats.append(flag(cx_flag[p]))
+            if cx_flag[p]:
+                if cx == "twopoint":
+                    ints.extend(int(v) for v in cx_raw[p])
+                else:
+                    floats.extend(float(v) for v in blend_u[p])
+        for i in range(n):
+            floats.append(flag(mut_flag[i]))
+            if mut_flag[i]:
+                for g in range(dim):
+                    floats.append(flag(mask[i, g]))
+                    if mut == "gaussian" and mask[i, g]:
+                        gausses.append(float(gauss[i, g]))
+        tb = base.Toolbox()
+        tb.register("evaluate", evalf)
+        tb.register("select", tools.selRandom)
+        if cx == "twopoint":
+            tb.register("mate", tools.cxTwoPoint)
+        else:
+            tb.register("mate", tools.cxBlend, alpha=alpha)
+        if mut == "flipbit":
+            tb.register("mutate", tools.mutFlipBit, indpb=indpb)
+        else:
+            tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=indpb)
+        with Replay(floats=floats, ints=ints, gausses=gausses,
+                    choices=[int(a) for a in asp.ravel()]):
+            pop2, log = algorithms.eaSimple(pop, tb, cxpb, mutpb, 1, verbose=False)
+        og, owv, ovalid = from_inds(pop2, genes.dtype, 1)
+        key = "srea%d_" % j
+        out.update({key + "genes": genes0, key + "wv": wv0, key + "valid": valid0,
+                    key + "asp": asp, key + "cx_flag": cx_flag, key + "cx_raw": cx_raw,
+                    key + "blend_u": blend_u, key + "mut_flag": mut_flag, key + "mask": mask,
+                    key + "gauss": gauss, key + "out_genes": og, key + "out_wv": owv,
+                    key + "nevals": np.array(log.select("nevals")),
+                    key + "meta": np.array([gt, tc, cx, mut, objective, str(weights[0])])})
+    return out
+
+
+PORT_CASES = [("rastrigin", "d", 1000, 256), ("onemax", "b", 4096, 128),
+              ("rosenbrock", "d", 300, 200)]
+
+
+def _reference_ea(D, problem, tc, dim, n, ngen, seed, mapper=None):
+    """The reference's own eaSimple run a user writes (README.md:72-103 /
+    examples/ga/onemax_mp.py) with the real Mersenne Twister; returns
+    (population, logbook, seconds of eaSimple)."""
+    import time
+    tools = D["deap.tools"]
+    algorithms = D["deap.algorithms"]
+    base = D["deap.base"]
+    bm = D["deap.benchmarks"]
+    weights = (1.0,) if problem == "onemax" else (-1.0,)
+    Ind = make_types(D, tc, weights)
+    random.seed(seed)
+    if problem == "onemax":
+        pop = [Ind(random.randint(0, 1) for _ in range(dim)) for _ in range(n)]
+    else:
+        lo, hi = (-5.12, 5.12) if problem == "rastrigin" else (-2.048, 2.048)
+        pop = [Ind(random.uniform(lo, hi) for _ in range(dim)) for _ in range(n)]
+    tb = base.Toolbox()
+    if mapper is not None:
+        tb.register("map", mapper)
+    if problem == "onemax":
+        tb.register("evaluate", _onemax_eval)
+        tb.register("mate", tools.cxTwoPoint)
+        tb.register("mutate", tools.mutFlipBit, indpb=0.05)
+    else:
+        tb.register("evaluate", getattr(bm, problem))
+        tb.register("mate", tools.cxBlend, alpha=0.5)
+        tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+    tb.register("select", tools.selTournament, tournsize=3)
+    t0 = time.perf_counter()
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, ngen, verbose=False)
+    return pop, log, time.perf_counter() - t0
+
+
+def _onemax_eval(ind):
+    return (sum(ind),)  # README.md:85-86
+
+
+def gen_port(D):
+    """Calibration of oracle/deap_port.py (the CPU baseline bench.py times):
+    the reference's seeded eaSimple outputs (bit-exact target) and, in
+    port_calibration.json, the reference-vs-port wall time on the same
+    configuration in this container (within +-20 %)."""
+    import json
+    import multiprocessing
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import deap_port
+    out = {}
+    for j, (problem, tc, dim, n) in enumerate(PORT_CASES):
+        pop, log, _ = _reference_ea(D, problem, tc, dim, n, 2, 1)
+        m = 1
+        g, wv, ok = from_inds(pop, np.uint8 if tc == "b" else np.float64, m)
+        key = "port%d_" % j
+        out.update({key + "genes": g, key + "wv": wv, key + "nevals": np.array(log.select("nevals")),
+                    key + "meta": np.array([problem, tc, str(dim), str(n)])})
+    cal = {"note": "seconds of eaSimple(ngen=2) including its generation-0 evaluation, same "
+                   "seed, this build container; median of 3 (reference = 2to3 copy of "
+                   "/root/reference/deap, oracle/deap_port.evolve(time_gen0=True))",
+           "cpu_count": os.cpu_count(), "cases": []}
+    for problem, tc, dim, n, workers in [("rastrigin", "d", 1000, 2048, 1),
+                                         ("onemax", "b", 4096, 2048, 1),
+                                         ("rastrigin", "d", 1000, 4096, 8)]:
+        ref_t, port_t = [], []
+        for _ in range(3):
+            if workers > 1:
+                pool = multiprocessing.Pool(workers)
+                try:
+                    ref_t.append(_reference_ea(D, problem, tc, dim, n, 2, 1, pool.map)[2])
+                finally:
+                    pool.close()
+                    pool.join()
+            else:
+                ref_t.append(_reference_ea(D, problem, tc, dim, n, 2, 1)[2])
+            port_t.append(deap_port.evolve(problem, n, dim, 2, workers if workers > 1 else None,
+                                           1, time_gen0=True)[1])
+        r, p = sorted(ref_t)[1], sorted(port_t)[1]
+        cal["cases"].append({"problem": problem, "genome": "array('%s')" % tc, "dim": dim,
+                             "pop": n, "workers": workers, "reference_s": round(r, 4),
+                             "port_s": round(p, 4), "port_over_reference": round(p / r, 4)})
+        print(cal["cases"][-1])
+    with open(os.path.join(HERE, "port_calibration.json"), "w") as f:
+        json.dump(cal, f, indent=1)
+    return out
+
+
+def gen_support(D, rng):
+    """HallOfFame.update (support.py:490-588) over a sequence of populations
+    with duplicates and fitness ties, and the text of Logbook streams
+    (support.py:261-487) fed by Statistics / MultiStatistics compiles."""
+    import operator
+    tools = D["deap.tools"]
+    out = {}
+    hof_cases = [(1, (1.0,), "eq"), (5, (1.0,), "eq"), (12, (1.0, -1.0), "eq"),
+                 (40, (-1.0,), "eq"), (3, (1.0,), "array_equal"), (7, (1.0,), "first_gene")]
+    for j, (maxsize, weights, sim) in enumerate(hof_cases):
+        similar = {"eq": operator.eq, "array_equal": np.array_equal,
+                   "first_gene": lambda a, b: a[0] == b[0]}[sim]
+        Ind = make_types(D, "d", weights)
+        hof = tools.HallOfFame(maxsize, similar=similar)
+        key = "hof%d_" % j
+        for gen in range(4):
+            n = 300
+            genes = rng.integers(0, 4, size=(n, 6)).astype(np.float64)
+            genes[rng.integers(0, n, 30)] = genes[rng.integers(0, n, 30)]  # duplicates
+            wv = np.stack([genes.sum(1) // 2 + gen * 0.5] +
+                          ([-genes[:, 0]] if len(weights) > 1 else []), 1) * np.array(weights)
+            pop = to_inds(Ind, genes, wv)
+            hof.update(pop)
+            out[key + "genes%d" % gen] = genes
+            out[key + "wv%d" % gen] = wv
+            out[key + "hof_genes%d" % gen] = np.array([list(h) for h in hof])
+            out[key + "hof_wv%d" % gen] = np.array([h.fitness.wvalues for h in hof])
+        out[key + "meta"] = np.array([str(maxsize), sim] + [str(w) for w in weights])
+    # Logbook text: Statistics on fitness values, a header, one stream per gen
+    Ind = make_types(D, "d", (-1.0,))
+    stats = tools.Statistics(key=lambda ind: ind.fitness.values)
+    stats.register("avg", np.mean)
+    stats.register("std", np.std)
+    stats.register("min", np.min)
+    stats.register("max", np.max)
+    log = tools.Logbook()
+    log.header = ["gen", "nevals"] + stats.fields
+    streams = []
+    for gen in range(5):
+        n = 64 + 7 * gen
+        wv = -np.round(rng.uniform(0, 10 ** gen, size=(n, 1)), 3)
+        pop = to_inds(Ind, np.zeros((n, 2)), wv)
+        out["log_wv%d" % gen] = wv
+        log.record(gen=gen, nevals=n - gen, **stats.compile(pop))
+        streams.append(log.stream)
+    out["log_streams"] = np.array(streams)
+    out["log_str"] = np.array(str(log))
+    # MultiStatistics -> chapters (examples/gp/symbreg.py:76-84 layout)
+    stats_fit = tools.Statistics(lambda ind: ind.fitness.values)
+    stats_size = tools.Statistics(len)
+    mstats = tools.MultiStatistics(fitness=stats_fit, size=stats_size)
+    mstats.register("avg", np.mean)
+    mstats.register("max", np.max)
+    log2 = tools.Logbook()
+    log2.header = "gen", "evals", "fitness", "size"
+    log2.chapters["fitness"].header = "min", "avg", "max"
+    log2.chapters["size"].header = "avg", "max"
+    mstats.register("min", np.min)
+    streams = []
+    for gen in range(4):
+        n = 40 + gen
+        wv = -np.round(rng.uniform(0, 5, size=(n, 1)), 2)
+        pop = to_inds(Ind, np.zeros((n, 3 + gen)), wv)
+        out["mlog_wv%d" % gen] = wv
+        log2.record(gen=gen, evals=n, **mstats.compile(pop))
+        streams.append(log2.stream)
+    out["mlog_streams"] = np.array(streams)
+    out["mlog_str"] = np.array(str(log2))
+    return out
+
+
 def main():
     D = load_reference()
     if sys.argv[1:] == ["log"]:
@@ -678,6 +918,13 @@ def main():
     if sys.argv[1:] == ["sbx"]:
         np.savez_compressed(os.path.join(HERE, "sbx.npz"),
                             **gen_sbx(D, np.random.default_rng(91)))
+        return
+    if sys.argv[1:] == ["round2"]:  # fixtures added in round 2 (existing ones untouched)
+        np.savez_compressed(os.path.join(HERE, "selrandom.npz"),
+                            **gen_selrandom(D, np.random.default_rng(5)))
+        np.savez_compressed(os.path.join(HERE, "support.npz"),
+                            **gen_support(D, np.random.default_rng(17)))
+        np.savez_compressed(os.path.join(HERE, "port.npz"), **gen_port(D))
         return
     if sys.argv[1:] == ["dcd"]:  # regenerate one fixture without touching the rest
         np.savez_compressed(os.path.join(HERE, "dcd.npz"),

@@ -1,0 +1,200 @@
+"""GPU: selRandom (selection.py:12-24) against the reference's own outputs,
+the per-generation bookkeeping of eaSimple on device — Statistics through the
+one-pass dm_fitness_stats kernel, HallOfFame candidate sets, the Logbook text
+— against fixtures the reference produced (tests/golden/support.npz,
+selrandom.npz), and its cost at 2^20."""
+import ctypes
+import time
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_close(a, b, tol):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
+
+
+def _dp():
+    from deap_amd.device import DevicePopulation
+    return DevicePopulation
+
+
+def test_sel_random_matches_reference(gpu):
+    import torch
+    from deap_amd import tools
+    from deap_amd.decisions import Decisions
+    d = golden("selrandom.npz")
+    for j in range(3):
+        n = int(d["sr%d_n" % j])
+        ch = d["sr%d_choice" % j]
+        pop = _dp().from_numpy(np.zeros((n, 2)), weights=(1.0,), wvalues=np.zeros((n, 1)),
+                               valid=np.ones(n))
+        dec = Decisions.from_numpy(gpu, aspirants=ch.reshape(-1, 1))
+        got = tools.selRandom(pop, len(ch), mode="inject", decisions=dec)
+        assert got.cpu().numpy().tolist() == d["sr%d_out" % j].tolist(), j
+    del torch
+
+
+def test_ea_generation_with_sel_random_matches_reference(gpu):
+    """eaSimple with toolbox.select = selRandom: the fused DM_SEL_RANDOM path."""
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.decisions import Decisions
+    d = golden("selrandom.npz")
+    for j in range(2):
+        k = "srea%d_" % j
+        gt, tc, cx, mut, objective, w0 = d[k + "meta"]
+        pop = _dp().from_numpy(d[k + "genes"], weights=(float(w0),), gtype=gt,
+                               wvalues=d[k + "wv"], valid=d[k + "valid"])
+        tb = base.Toolbox()
+        tb.register("evaluate", getattr(benchmarks, objective))
+        tb.register("select", tools.selRandom)
+        if cx == "twopoint":
+            tb.register("mate", tools.cxTwoPoint)
+            tb.register("mutate", tools.mutFlipBit, indpb=0.05)
+        else:
+            tb.register("mate", tools.cxBlend, alpha=0.5)
+            tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+        dec = Decisions.from_numpy(gpu, aspirants=d[k + "asp"], cx_flag=d[k + "cx_flag"],
+                                   cx_raw=d[k + "cx_raw"], blend_u=d[k + "blend_u"],
+                                   mut_flag=d[k + "mut_flag"], mut_mask=d[k + "mask"],
+                                   gauss=d[k + "gauss"])
+        pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 1, verbose=False, decisions=[dec],
+                                       mode="inject")
+        g, wv, ok = pop.to_numpy()
+        assert np.array_equal(g, d[k + "out_genes"]), j
+        assert ok.all()
+        assert _rel_close(wv, d[k + "out_wv"], 0 if gt == "bits" else 1e-12), j
+        assert log.select("nevals") == d[k + "nevals"].tolist()
+
+
+@pytest.mark.parametrize("nobj,n", [(1, 1 << 20), (3, 100003), (2, 1)])
+def test_fitness_stats_kernel_matches_numpy(gpu, nobj, n):
+    """dm_fitness_stats at 2^20 against numpy on the same values (mean / std /
+    var 1e-12 relative, min / max / argmin / argmax exact), invalid rows
+    skipped, NaN propagated."""
+    import torch
+    from deap_amd import _lib
+    rng = np.random.default_rng(nobj)
+    weights = (-1.0, 1.0, 0.5)[:nobj]
+    wv = rng.normal(1e4, 3.0, size=(n, nobj)) * np.array(weights)
+    wv[rng.integers(0, n, min(n, 50))] = wv[0]  # ties with row 0
+    valid = np.ones(n, np.uint8)
+    if n > 10:
+        valid[rng.integers(0, n, 100)] = 0
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=weights, wvalues=wv, valid=valid)
+    out = torch.empty(nobj * 8, dtype=torch.float64, device=gpu)
+    _lib.call("dm_fitness_stats", pop.ctx.bind(), ctypes.byref(pop.c_pop()),
+              (ctypes.c_double * nobj)(*weights), ctypes.c_void_p(out.data_ptr()))
+    r = out.cpu().numpy().reshape(nobj, 8)
+    vals = (wv / np.array(weights))[valid.astype(bool)]
+    rows = np.nonzero(valid)[0]
+    for o in range(nobj):
+        v = vals[:, o]
+        assert r[o, 0] == v.min() and r[o, 1] == v.max()
+        assert int(r[o, 5]) == rows[np.argmin(v)]
+        assert int(r[o, 6]) == rows[np.argmax(v)]
+        assert int(r[o, 7]) == len(v)
+        assert _rel_close(r[o, 2], v.mean(), 1e-12)
+        assert _rel_close(r[o, 4], v.sum(), 1e-12)
+        assert _rel_close(np.sqrt(r[o, 3] / r[o, 7]), v.std(), 1e-10)
+    wv[n // 2, 0] = np.nan
+    pop2 = _dp().from_numpy(np.zeros((n, 1)), weights=weights, wvalues=wv, valid=np.ones(n))
+    _lib.call("dm_fitness_stats", pop2.ctx.bind(), ctypes.byref(pop2.c_pop()),
+              (ctypes.c_double * nobj)(*weights), ctypes.c_void_p(out.data_ptr()))
+    r = out.cpu().numpy().reshape(nobj, 8)
+    assert np.isnan(r[0, [0, 1, 2, 3, 4]]).all()
+
+
+def _stats_registered():
+    from deap_amd import tools
+    stats = tools.Statistics(key=lambda ind: ind.fitness.values)
+    stats.register("avg", np.mean)
+    stats.register("std", np.std)
+    stats.register("min", np.min)
+    stats.register("max", np.max)
+    return stats
+
+
+def test_logbook_from_device_statistics_matches_reference_text(gpu):
+    """Statistics.compile on DevicePopulations (dm_fitness_stats) recorded in
+    a Logbook prints the reference's stream text (support.npz)."""
+    from deap_amd import tools
+    d = golden("support.npz")
+    stats = _stats_registered()
+    log = tools.Logbook()
+    log.header = ["gen", "nevals"] + stats.fields
+    for gen in range(5):
+        wv = d["log_wv%d" % gen]
+        pop = _dp().from_numpy(np.zeros((len(wv), 2)), weights=(-1.0,), wvalues=wv,
+                               valid=np.ones(len(wv)))
+        rec = {k: v() if callable(v) else v for k, v in stats.compile(pop).items()}
+        log.record(gen=gen, nevals=len(wv) - gen, **rec)
+        assert log.stream == str(d["log_streams"][gen]), gen
+
+
+def test_hall_of_fame_device_matches_reference(gpu):
+    """HallOfFame.update on DevicePopulations (candidate sets via selBest for
+    value-equality `similar`, host walk otherwise) against the reference's
+    own halls after each of four updates."""
+    import operator
+    from deap_amd import tools
+    d = golden("support.npz")
+    sims = {"eq": operator.eq, "array_equal": np.array_equal,
+            "first_gene": lambda a, b: a[0] == b[0]}
+    j = 0
+    while "hof%d_meta" % j in d:
+        meta = d["hof%d_meta" % j]
+        maxsize, sim, weights = int(meta[0]), str(meta[1]), tuple(float(w) for w in meta[2:])
+        hof = tools.HallOfFame(maxsize, similar=sims[sim])
+        for gen in range(4):
+            genes, wv = d["hof%d_genes%d" % (j, gen)], d["hof%d_wv%d" % (j, gen)]
+            pop = _dp().from_numpy(genes, weights=weights, gtype="f64", wvalues=wv,
+                                   valid=np.ones(len(genes)))
+            hof.update(pop)
+            assert [list(h) for h in hof] == d["hof%d_hof_genes%d" % (j, gen)].tolist(), (j, gen)
+            assert [list(h.fitness.wvalues) for h in hof] == \
+                d["hof%d_hof_wv%d" % (j, gen)].tolist(), (j, gen)
+        j += 1
+
+
+def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
+    """eaSimple(..., stats, halloffame) at 2^20 Rastrigin-1000D: the bookkeeping
+    (one dm_fitness_stats pass + the HallOfFame candidate selBest per
+    generation) stays a small fraction of the generation.
+    Prints ms/gen with and without it."""
+    import torch
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim = 1 << 20, 1000
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.rastrigin)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+    res = {}
+    for label in ("plain", "stats+hof"):
+        st = RandomStream(5)
+        pop = tools.initPopulation(n=n, dim=dim, low=-5.12, high=5.12, gtype="f64",
+                                   weights=(-1.0,), stream=st)
+        kw = {}
+        if label != "plain":
+            kw = {"stats": _stats_registered(), "halloffame": tools.HallOfFame(10)}
+        algorithms.eaSimple(pop, tb, 0.5, 0.2, 2, verbose=False, stream=st, **kw)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 10, verbose=False, stream=st, **kw)
+        torch.cuda.synchronize()
+        res[label] = (time.perf_counter() - t0) / 10 * 1e3
+        if label != "plain":
+            mins = log.select("min")
+            assert all(np.isfinite(m) for m in mins) and len(kw["halloffame"]) == 10
+            best = kw["halloffame"][0].fitness.values[0]
+            assert best <= min(mins) + 1e-9
+    print("eaSimple ms/gen at 2^20: plain %.3f, with stats+hof %.3f" % (res["plain"],
+                                                                        res["stats+hof"]))
+    assert res["stats+hof"] < 1.5 * res["plain"] + 2.0

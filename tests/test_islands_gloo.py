@@ -115,3 +115,83 @@ def test_mig_ring_distributed_matches_single_process(migarray):
 def test_owner_map_single_rank_owns_all():
     from deap_amd import islands
     assert islands.owner_map([0, 1, 2], 3, 1, None) == {0: 0, 1: 0, 2: 0}
+
+
+def _worker_split(rank, world, port, seed, ids_by_rank, migarray, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from deap_amd import islands
+        islands.pack, islands.place, islands._select = _pack, _place, _select
+        demes = _demes(seed)
+        ids = ids_by_rank[rank]
+        mine = [HostDeme(demes[i]) for i in ids]
+        islands.migRingDistributed(mine, ids, N_DEMES, K, selection=None, migarray=migarray,
+                                   stream=object())
+        q.put((rank, {i: (m.d["genes"].copy(), m.d["wvalues"].copy()) for i, m in zip(ids, mine)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ids_by_rank,migarray", [
+    ([[0, 3], [1, 2]], None),             # interleaved ownership
+    ([[2], [0, 1, 3]], [3, 2, 0, 1]),      # uneven split
+    ([[1, 2, 3], [0]], [0, 2, 1, 3]),      # self hops (deme migrates into itself)
+])
+def test_mig_ring_distributed_any_split(ids_by_rank, migarray):
+    """owner_map accepts any split agreed through all_gather_object."""
+    from oracle import ops
+    seed = 23
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_split, args=(r, 2, port, seed, ids_by_rank, migarray, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        _, part = q.get(timeout=120)
+        got.update(part)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _demes(seed)
+    em = [ops.sel_best(d["wvalues"], K) for d in ref]
+    ops.mig_ring(ref, em, None, migarray)
+    for d in range(N_DEMES):
+        assert np.array_equal(got[d][0], ref[d]["genes"]), "deme %d genomes" % d
+        assert np.array_equal(got[d][1], ref[d]["wvalues"]), "deme %d fitness" % d
+
+
+@pytest.mark.parametrize("migarray", [None, [2, 3, 1, 0], [0, 2, 1, 3], [1, 1, 3, 2]])
+@pytest.mark.parametrize("owner", [[0, 0, 0, 0], [0, 1, 0, 1], [1, 1, 0, 0], [0, 0, 1, 2]])
+def test_c_mig_plan_matches_python_routing(migarray, owner):
+    """dm_mig_plan (the C ABI's routing, host-only) gives, for every rank,
+    exactly the hops route_blocks performs: local references, sends and
+    receives, in from_deme order."""
+    from deap_amd import _lib, islands
+    if not __import__("os").path.exists(_lib.LIB_PATH):
+        pytest.skip("libdeapmi.so not built")
+    n = len(owner)
+    mig = migarray if migarray is not None else list(range(1, n)) + [0]
+    for me in sorted(set(owner)):
+        want = []
+        for frm, to in enumerate(mig):
+            s, d = owner[frm], owner[to]
+            if s == me and d == me:
+                want.append(("local", frm, to, me))
+            elif s == me:
+                want.append(("send", frm, to, d))
+            elif d == me:
+                want.append(("recv", frm, to, s))
+        assert islands.mig_plan(n, migarray, dict(enumerate(owner)), me) == want
+    # the single-GPU RCCL test hook: local hops between different demes
+    # become a send/recv pair to the rank itself
+    hops = islands.mig_plan(n, migarray, {d: 0 for d in range(n)}, 0, force_p2p=True)
+    for frm, to in enumerate(mig):
+        if frm == to:
+            assert ("local", frm, to, 0) in hops
+        else:
+            i = hops.index(("send", frm, to, 0))
+            assert hops[i + 1] == ("recv", frm, to, 0)
