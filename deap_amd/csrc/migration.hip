@@ -212,27 +212,23 @@ extern "C" int dm_pack_rows(dm_ctx* ctx, const dm_pop* pop, const int32_t* idx, 
     return DM_OK;
 }
 
-extern "C" int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
-                            const void* emigrant_block, int64_t k, int32_t* out_slots) {
-    DM_CHECK_ARG(ctx && pop && immigrant_block && emigrant_block && out_slots, "null argument");
-    int rc = validate_pop(pop, "pop");
-    if (rc) return rc;
-    DM_CHECK_ARG(k >= 0 && k <= 4096, "k must be in [0, 4096]");
-    if (k == 0) return DM_OK;
+namespace dm {
+// Placement for one receiving deme, asynchronous: *err (device int32) gets
+// j + 1 when immigrant j is not found (list.index ValueError), else stays 0.
+static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
+                           const void* emigrant_block, int64_t k, int32_t* out_slots,
+                           int32_t* err) {
     const int64_t n = pop->n;
     const int64_t words = (n + 63) / 64;
     const size_t bm = align_up((size_t)k * words * 8, 256);
     char* base = (char*)scratch_slot(ctx, 3, bm + align_up((size_t)k * k, 256) +
-                                                 align_up((size_t)std::max<int64_t>(n, 1) * 4, 256) + 256);
+                                                 align_up((size_t)std::max<int64_t>(n, 1) * 4, 256));
     if (!base) return DM_ERR_NOMEM;
     unsigned long long* bitmap = (unsigned long long*)base;
     uint8_t* E = (uint8_t*)(base + bm);
     int32_t* content = (int32_t*)(base + bm + align_up((size_t)k * k, 256));
-    int32_t* err = (int32_t*)(base + bm + align_up((size_t)k * k, 256) +
-                              align_up((size_t)std::max<int64_t>(n, 1) * 4, 256));
     hipStream_t s = ctx->stream;
     DM_HIP(hipMemsetAsync(bitmap, 0, (size_t)k * words * 8, s));
-    DM_HIP(hipMemsetAsync(err, 0, 4, s));
     DM_HIP(hipMemsetAsync(content, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
     match_kernel<<<grid, 256, 0, s>>>((const char*)pop->genes, pop->wvalues, pop->valid, n,
@@ -244,9 +240,25 @@ extern "C" int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_bloc
                                      pop->nobj, emigrant_block, k, words, bitmap, E, out_slots,
                                      content, err);
     DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+}  // namespace dm
+
+extern "C" int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
+                            const void* emigrant_block, int64_t k, int32_t* out_slots) {
+    DM_CHECK_ARG(ctx && pop && immigrant_block && emigrant_block && out_slots, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0 && k <= 4096, "k must be in [0, 4096]");
+    if (k == 0) return DM_OK;
+    int32_t* err = (int32_t*)scratch_slot(ctx, 4, 256);
+    if (!err) return DM_ERR_NOMEM;
+    DM_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+    if ((rc = mig_place_async(ctx, pop, immigrant_block, emigrant_block, k, out_slots, err)))
+        return rc;
     int32_t herr = 0;
-    DM_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
-    DM_HIP(hipStreamSynchronize(s));
+    DM_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    DM_HIP(hipStreamSynchronize(ctx->stream));
     DM_CHECK_ARG(herr == 0, "migRing: immigrant %d is not in the receiving population", herr - 1);
     return DM_OK;
 }
@@ -417,7 +429,9 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
     int nrecv = 0;
     for (const dm_mig_hop& h : hops) nrecv += h.kind == DM_HOP_RECV;
     // [emigrant block | immigrant block] per local deme, then one per receive
-    char* base = (char*)scratch_slot(ctx, 4, bb * (2 * (size_t)n_local + nrecv));
+    char* base = (char*)scratch_slot(ctx, 4, bb * (2 * (size_t)n_local + nrecv) +
+                                                 align_up((size_t)k * 4, 256) +
+                                                 align_up(hops.size() * 4, 256));
     if (!base) return DM_ERR_NOMEM;
     hipStream_t s = ctx->stream;
     std::vector<char*> emig(n_local), immig(n_local);
@@ -455,17 +469,24 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
     }
     for (size_t h = 0; h < hops.size(); ++h)
         if (hops[h].kind == DM_HOP_LOCAL) incoming[h] = emig[local_of[hops[h].from]];
-    // migration.py:48-51: placements in from_deme order
+    // migration.py:48-51: placements in from_deme order, asynchronous; one
+    // status word per hop, copied back and checked once at the end
+    int32_t* slot_scratch = (int32_t*)(base + 2 * (size_t)n_local * bb + (size_t)nrecv * bb);
+    int32_t* errs = slot_scratch + align_up((size_t)k, 64);
+    DM_HIP(hipMemsetAsync(errs, 0, hops.size() * 4, s));
     for (size_t h = 0; h < hops.size(); ++h) {
         if (!incoming[h]) continue;
         const int32_t t = local_of[hops[h].to];
-        int32_t* slots = out_slots && out_slots[t] ? out_slots[t] : nullptr;
-        if (!slots) {
-            slots = (int32_t*)scratch(ctx, (size_t)k * 4);
-            if (!slots) return DM_ERR_NOMEM;
-        }
-        if ((rc = dm_mig_place(ctx, &demes[t], immig[t], incoming[h], k, slots))) return rc;
+        int32_t* slots = out_slots && out_slots[t] ? out_slots[t] : slot_scratch;
+        if ((rc = mig_place_async(ctx, &demes[t], immig[t], incoming[h], k, slots, errs + h)))
+            return rc;
     }
+    std::vector<int32_t> herr(hops.size(), 0);
+    DM_HIP(hipMemcpyAsync(herr.data(), errs, hops.size() * 4, hipMemcpyDeviceToHost, s));
+    DM_HIP(hipStreamSynchronize(s));
+    for (size_t h = 0; h < hops.size(); ++h)
+        DM_CHECK_ARG(herr[h] == 0, "migRing: immigrant %d of deme %d is not in the receiving "
+                     "population", herr[h] - 1, hops[h].to);
     return DM_OK;
 }
 

@@ -268,6 +268,101 @@ int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool des
                          vals_out, (int32_t*)(s + 2 * kb), s + 2 * kb + vb);
 }
 
+
+// Top-k of a single-objective population (k <= TOPK_MAX): the order of the
+// first k entries of the stable sort, from two launches instead of a full
+// 8-pass radix sort of n keys — each block bitonic-sorts its slice of
+// (key, index) pairs in LDS and keeps its first k; one block then sorts the
+// blocks' candidates.  Pairs are distinct (the index breaks ties), so the
+// result is exactly the stable order: ties by ascending index.
+constexpr int TOPK_MAX = 32;
+
+template <int ITEMS>
+__device__ void bitonic_lds(uint64_t* key, int32_t* idx) {
+    for (int size = 2; size <= ITEMS; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < ITEMS / 2; t += blockDim.x) {
+                const int lo = 2 * t - (t & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint64_t ka = key[lo], kb = key[hi];
+                const int32_t ia = idx[lo], ib = idx[hi];
+                const bool gt = ka > kb || (ka == kb && ia > ib);
+                if (gt == up) {
+                    key[lo] = kb;
+                    key[hi] = ka;
+                    idx[lo] = ib;
+                    idx[hi] = ia;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(256) void topk_block_kernel(const double* wv, int64_t n, bool desc,
+                                                         int k, uint64_t* ckey, int32_t* cidx) {
+    __shared__ uint64_t key[ITEMS];
+    __shared__ int32_t idx[ITEMS];
+    const int64_t base = (int64_t)blockIdx.x * ITEMS;
+    for (int i = threadIdx.x; i < ITEMS; i += blockDim.x) {
+        const int64_t r = base + i;
+        if (r < n) {
+            const uint64_t q = ordered_key(wv[r]);
+            key[i] = desc ? ~q : q;
+            idx[i] = (int32_t)r;
+        } else {
+            key[i] = ~0ull;
+            idx[i] = INT32_MAX;
+        }
+    }
+    __syncthreads();
+    bitonic_lds<ITEMS>(key, idx);
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+        ckey[(int64_t)blockIdx.x * k + i] = key[i];
+        cidx[(int64_t)blockIdx.x * k + i] = idx[i];
+    }
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(1024) void topk_merge_kernel(const uint64_t* ckey, const int32_t* cidx,
+                                                          int ncand, int k, int32_t* out) {
+    __shared__ uint64_t key[ITEMS];
+    __shared__ int32_t idx[ITEMS];
+    for (int i = threadIdx.x; i < ITEMS; i += blockDim.x) {
+        key[i] = i < ncand ? ckey[i] : ~0ull;
+        idx[i] = i < ncand ? cidx[i] : INT32_MAX;
+    }
+    __syncthreads();
+    bitonic_lds<ITEMS>(key, idx);
+    for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = idx[i];
+}
+
+static int sel_topk(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx, bool best) {
+    const int64_t n = pop->n;
+    const int items = n <= (1ll << 18) ? 1024 : n <= (1ll << 20) ? 4096 : 8192;
+    const int64_t blocks = (n + items - 1) / items;
+    const int64_t ncand = blocks * k;
+    char* w = (char*)scratch_slot(ctx, 3, align_up((size_t)ncand * 8, 256) + (size_t)ncand * 4);
+    if (!w) return DM_ERR_NOMEM;
+    uint64_t* ckey = (uint64_t*)w;
+    int32_t* cidx = (int32_t*)(w + align_up((size_t)ncand * 8, 256));
+    hipStream_t s = ctx->stream;
+    if (items == 1024)
+        topk_block_kernel<1024><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
+    else if (items == 4096)
+        topk_block_kernel<4096><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
+    else
+        topk_block_kernel<8192><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
+    if (ncand <= 1024)
+        topk_merge_kernel<1024><<<1, 1024, 0, s>>>(ckey, cidx, (int)ncand, (int)k, out_idx);
+    else
+        topk_merge_kernel<8192><<<1, 1024, 0, s>>>(ckey, cidx, (int)ncand, (int)k, out_idx);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
 }  // namespace dm
 
 using namespace dm;
@@ -280,6 +375,10 @@ static int sel_sorted(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_id
     k = std::min(k, pop->n);
     if (k == 0) return DM_OK;
     DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    // small k of a single objective (migRing emigrants, HallOfFame candidates)
+    if (pop->nobj == 1 && k <= TOPK_MAX && pop->n > 4 * k && pop->n <= 256ll * 8192 &&
+        !std::getenv("DM_SELBEST_FULLSORT"))
+        return sel_topk(ctx, pop, k, out_idx, best);
     int32_t* full = out_idx;
     if (k < pop->n) {
         full = (int32_t*)scratch_slot(ctx, 3, (size_t)pop->n * 4);

@@ -80,11 +80,20 @@ def _replay(gt, dim, n_demes, ngen, k, init, decs, record, w):
             nevals[d].append(nev)
         if gen % 5 == 0:
             rec = next(mig)
-            em = [ops.sel_best(state[d]["wvalues"], k) for d in range(n_demes)]
             for d in range(n_demes):
-                assert rec["emigrants"][d].tolist() == em[d].tolist(), (gen, d)
+                em = ops.sel_best(state[d]["wvalues"], k)
+                got = rec["emigrants"][d]
+                if gt == "bits":
+                    assert got.tolist() == em.tolist(), (gen, d)
+                else:
+                    # fp64 fitness agrees to 1e-12 relative, so two rows whose
+                    # fitnesses are that close may swap ranks: the device's
+                    # choice must be a selBest under the oracle's values up to
+                    # that tolerance, and its rows are then replayed
+                    assert _rel_close(state[d]["wvalues"][got], state[d]["wvalues"][em], 1e-12), \
+                        (gen, d, got, em)
             im = None if rec["immigrants"][0] is None else rec["immigrants"]
-            ops.mig_ring(state, em, im)
+            ops.mig_ring(state, rec["emigrants"], im)
     return state, nevals
 
 

@@ -198,3 +198,22 @@ def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
     print("eaSimple ms/gen at 2^20: plain %.3f, with stats+hof %.3f" % (res["plain"],
                                                                         res["stats+hof"]))
     assert res["stats+hof"] < 1.5 * res["plain"] + 2.0
+
+
+@pytest.mark.parametrize("n,k", [(200, 1), (4097, 15), (100000, 32), (1 << 20, 15),
+                                 ((1 << 21) - 3, 7)])
+def test_sel_best_topk_path_matches_stable_sort(gpu, n, k):
+    """selBest / selWorst of a single objective with small k take the
+    two-launch top-k path; the result is the reference's stable order
+    (sorted(..., reverse=True)[:k], selection.py:27-48): ties by index."""
+    from deap_amd import tools
+    from oracle import ops
+    rng = np.random.default_rng(n)
+    wv = rng.integers(0, 40, size=(n, 1)).astype(np.float64)  # heavy ties
+    wv[rng.integers(0, n, 10)] = -0.0
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0,), wvalues=wv, valid=np.ones(n))
+    assert tools.selBest(pop, k).cpu().numpy().tolist() == ops.sel_best(wv, k).tolist()
+    assert tools.selWorst(pop, k).cpu().numpy().tolist() == ops.sel_worst(wv, k).tolist()
+    wv2 = rng.normal(size=(n, 1))
+    pop2 = _dp().from_numpy(np.zeros((n, 1)), weights=(-1.0,), wvalues=wv2, valid=np.ones(n))
+    assert tools.selBest(pop2, k).cpu().numpy().tolist() == ops.sel_best(wv2, k).tolist()
