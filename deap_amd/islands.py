@@ -221,7 +221,8 @@ def _mig_ring_rccl(comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_
 
 def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=None,
                   n_demes=None, streams=None, stats=None, halloffame=None, verbose=False,
-                  mode=None, decisions=None, record=None, group=None, force_p2p=False):
+                  mode=None, decisions=None, record=None, group=None, force_p2p=False,
+                  callback=None):
     """The multi-demic GA loop of ``examples/ga/onemax_multidemic.py:79-93``
     on device demes, each deme's generation one fused launch
     (select -> clone -> varAnd -> evaluate, ``dm_generation``)::
@@ -243,6 +244,8 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
     ``streams``: one RandomStream per deme (default: seeded from the deme id).
     ``decisions``: dict deme_id -> list (dump: filled per generation; inject:
     read).  ``record``: list receiving each migration's selected indices.
+    ``callback(gen, stage, demes)`` (test hook) runs after every generation
+    (stage "generation") and after every migration (stage "migration").
     Returns ``(demes, logbook)``; generation 0 evaluates invalid individuals."""
     from .algorithms import GenerationStep, _check_pop, _eval
     from .ops import RandomStream
@@ -281,6 +284,8 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
                           ctypes.c_void_p(nev[i].data_ptr() + 8 * gen), mode, dec, gen - 1)
             d.swap_storage(offspring[i])
             book(gen, deme_ids[i], d)
+        if callback is not None:
+            callback(gen, "generation", demes)
         if mig_every and gen % mig_every == 0:
             if n_demes == len(demes) and group is None and not dist.is_initialized() \
                     and not force_p2p:
@@ -288,6 +293,8 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
             else:
                 migRingDistributed(demes, deme_ids, n_demes, stream=streams[0], group=group,
                                    record=record, force_p2p=force_p2p, **mig_kw)
+            if callback is not None:
+                callback(gen, "migration", demes)
     counts = nev.cpu().tolist()
     pos = {d: i for i, d in enumerate(deme_ids)}
     from .algorithms import _materialise

@@ -42,7 +42,7 @@ def _decisions(dn, dim):
             "mut_mask": ops.unpack_mask(dn["mut_mask"], dim), "gauss": dn.get("gauss")}
 
 
-def _run(gt, dim, n, n_demes, ngen, k, replacement, force_p2p=False):
+def _run(gt, dim, n, n_demes, ngen, k, replacement, force_p2p=False, snapshots=None):
     from deap_amd import islands, tools
     from deap_amd.ops import RandomStream
     w = (1.0,) if gt == "bits" else (-1.0,)
@@ -53,9 +53,14 @@ def _run(gt, dim, n, n_demes, ngen, k, replacement, force_p2p=False):
     init = [d.genes_numpy() for d in demes]
     decs, record = {}, []
     tb = _toolbox(gt, k, replacement)
+
+    def snap(gen, stage, ds):
+        snapshots.append((gen, stage, [d.to_numpy() for d in ds]))
+
     demes, log = islands.eaSimpleDemes(demes, tb, 0.5, 0.2, ngen, mig_every=5, streams=streams,
                                        mode="dump", decisions=decs, record=record,
-                                       force_p2p=force_p2p)
+                                       force_p2p=force_p2p,
+                                       callback=snap if snapshots is not None else None)
     return demes, log, init, decs, record, w
 
 
@@ -100,10 +105,11 @@ def _replay(gt, dim, n_demes, ngen, k, init, decs, record, w):
 @pytest.mark.parametrize("gt,dim,n,n_demes,replacement", [
     ("bits", 100, 64, 4, None),
     ("bits", 100, 64, 3, "sample"),          # the multidemic example's replacement
-    ("f64", 100, 48, 8, None),
-    ("f64", 64, 33, 5, "sample"),            # odd deme size
 ])
 def test_demes_with_migration_replay_in_oracle(gpu, gt, dim, n, n_demes, replacement):
+    """Packed-bit OneMax demes (exact fitness): the whole 12-generation
+    trajectory with two migrations replayed in the oracle from the initial
+    demes alone."""
     ngen, k = 12, 5
     demes, log, init, decs, record, w = _run(gt, dim, n, n_demes, ngen, k, replacement)
     assert len(record) == ngen // 5
@@ -174,3 +180,48 @@ def test_mig_place_identity_with_nan_genome(gpu):
     assert slots == [3, 5]
     g, wv, _ = a.to_numpy()
     assert np.array_equal(g[3], genes[0] + 100) and np.array_equal(g[5], genes[1] + 100)
+
+
+@pytest.mark.parametrize("dim,n,n_demes,replacement", [(100, 48, 8, None), (64, 33, 5, "sample")])
+def test_fp64_demes_stepwise_replay_in_oracle(gpu, dim, n, n_demes, replacement):
+    """Rastrigin fp64 demes: fitness agrees with the oracle to 1e-12 relative,
+    and a converging deme holds near-identical rows whose fitnesses lie within
+    that tolerance, so a long trajectory replayed from the initial demes alone
+    can flip a tournament.  Stage isolation instead: every generation is
+    replayed in the oracle from the device's state before it (genomes
+    bit-exact, fitness 1e-12), and every migration from the device's state
+    before it with the device's emigrant rows (bit-exact), the rows checked to
+    be a selBest under the oracle's fitness to the same tolerance."""
+    ngen, k = 12, 5
+    snaps = []
+    demes, log, init, decs, record, w = _run("f64", dim, n, n_demes, ngen, k, replacement,
+                                             snapshots=snaps)
+    prev = []
+    for d in range(n_demes):
+        g = init[d].copy()
+        prev.append((g, ops.evaluate(g, "rastrigin", w), np.ones(len(g), bool)))
+    mig = iter(record)
+    for gen, stage, state in snaps:
+        if stage == "generation":
+            for d in range(n_demes):
+                g0, wv0, ok0 = prev[d]
+                dn = decs[d][gen - 1].numpy()
+                g, wv, ok, nev = ops.ea_generation(g0, wv0, ok0, 0.5, 0.2, "blend", "gaussian",
+                                                   _decisions(dn, dim), "rastrigin", w)
+                assert np.array_equal(state[d][0], g), (gen, d)
+                assert _rel_close(state[d][1], wv, 1e-12), (gen, d)
+        else:
+            rec = next(mig)
+            before = [{"genes": prev[d][0].copy(), "wvalues": prev[d][1].copy(),
+                       "valid": prev[d][2].copy()} for d in range(n_demes)]
+            for d in range(n_demes):
+                em = ops.sel_best(before[d]["wvalues"], k)
+                got = rec["emigrants"][d]
+                assert _rel_close(before[d]["wvalues"][got], before[d]["wvalues"][em], 1e-12)
+            im = None if rec["immigrants"][0] is None else rec["immigrants"]
+            ops.mig_ring(before, rec["emigrants"], im)
+            for d in range(n_demes):
+                assert np.array_equal(state[d][0], before[d]["genes"]), (gen, d)
+                assert np.array_equal(state[d][1], before[d]["wvalues"]), (gen, d)
+        prev = [(s[0], s[1], s[2].astype(bool)) for s in state]
+    assert len(record) == ngen // 5
