@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r02a}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} -s > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v -rf --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} -s > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|Error|error" $OUT/pytest_gpu.log | tail -15
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after crash-like exit"; exit $rc; fi
