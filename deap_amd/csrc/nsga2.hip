@@ -26,6 +26,17 @@ namespace dm {
 int validate_pop(const dm_pop* p, const char* what);
 int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool desc,
                     int32_t* vals_out);
+// dominance.hip: integer-rank symmetric dominance + device-driven peeling
+size_t fast_dom_ranks_bytes(int64_t U);
+int fast_dom_ranks(hipStream_t s, const double* ufit, int m, int64_t U, int4* R4, char* work);
+int64_t fast_dom_words(int64_t U);
+size_t fast_dom_partial_bytes(int64_t U);
+int fast_dom_matrix(hipStream_t s, const int4* R4, int m, int64_t U, uint64_t* D, char* partials,
+                    int32_t* count);
+size_t fast_fronts_bytes(int64_t U);
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t sorted0, int64_t N,
+                const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
+                int32_t* fstarts, char* work, std::vector<int32_t>& ufront, int64_t* sorted);
 
 // ---------------------------------------------------------------------------
 // Workspace bump allocator over the context scratch
@@ -65,6 +76,9 @@ __global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, in
         segstart_in[j] = start ? (int32_t)j : 0;
         if (start) isrep[perm[j]] = 1;
     }
+}
+__global__ void nan_any_kernel(const double* wv, int64_t cnt, int32_t* flag) {
+    GRID_LOOP(i, cnt) if (wv[i] != wv[i]) *flag = 1;
 }
 __global__ void zero_i32_kernel(int32_t* p, int64_t n) {
     GRID_LOOP(i, n) p[i] = 0;
@@ -433,6 +447,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     void* rtemp = bp.take<char>(radix_sort_temp_bytes(n));
     void* stemp = bp.take<char>(scan_temp_bytes(n));
     int32_t* utotal = small;
+    int32_t* nanflag = small + 2;
     int32_t* ftotal = small + 4;
     int64_t* dtotal = (int64_t*)(small + 8);
     // lexicographic ascending sort of wvalues (ties by index: stable)
@@ -442,9 +457,16 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
     if ((rc = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return rc;
     if ((rc = exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp))) return rc;
-    DM_HIP(hipMemcpyAsync(hostv, utotal, 4, hipMemcpyDeviceToHost, s));
+    DM_HIP(hipMemsetAsync(nanflag, 0, 4, s));
+    nan_any_kernel<<<g1(n * m), 256, 0, s>>>(wv, n * m, nanflag);
+    DM_HIP(hipMemcpyAsync(hostv, utotal, 12, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
     const int64_t U = hostv[0];
+    const bool has_nan = hostv[2] != 0;
+    // integer ranks + symmetric tiles + device-driven peel (dominance.hip);
+    // DM_DOM_LDS / DM_DOM_BALLOT select the fp64 kernels (cross-checks)
+    const bool fast = m >= 2 && m <= 4 && !has_nan && !std::getenv("DM_DOM_LDS") &&
+                      !std::getenv("DM_DOM_BALLOT");
     const int64_t W = (U + 63) / 64;
     const int64_t tiles = (W + PEEL_WORDS - 1) / PEEL_WORDS;
     const double dbytes = (double)U * (double)W * 8.0;
@@ -471,14 +493,29 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         set_error("internal workspace overflow");
         return DM_ERR_INVALID;
     }
-    uint64_t* D = (uint64_t*)scratch_slot(ctx, 1, (size_t)U * W * 8);
+    uint64_t* D = (uint64_t*)scratch_slot(
+        ctx, 1, fast ? (size_t)fast_dom_words(U) * 8 : (size_t)U * W * 8);
     if (!D) return DM_ERR_NOMEM;
+    char* fwork = nullptr;  // fast path: partials | R4 | ranks / fronts work
+    if (fast) {
+        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
+        const size_t rb = align_up((size_t)U * 16, 256);
+        fwork = (char*)scratch_slot(ctx, 4, pb + rb + std::max(fast_dom_ranks_bytes(U),
+                                                               fast_fronts_bytes(U)));
+        if (!fwork) return DM_ERR_NOMEM;
+    }
 
     zero_i32_kernel<<<g1(U), 256, 0, s>>>(gsize, U);
     zero_i32_kernel<<<g1(U), 256, 0, s>>>(count, U);
     fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
     unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
-    if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
+    if (fast) {
+        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
+        int4* R4 = (int4*)(fwork + pb);
+        char* rwork = fwork + pb + align_up((size_t)U * 16, 256);
+        if ((rc = fast_dom_ranks(s, ufit, m, U, R4, rwork))) return rc;
+        if ((rc = fast_dom_matrix(s, R4, m, U, D, fwork, count))) return rc;
+    } else if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
         const int64_t ngroups = (W + DB_WPW - 1) / DB_WPW;
         int32_t* cpart = (int32_t*)scratch_slot(ctx, 4, (size_t)ngroups * U * 4);
         if (!cpart) return DM_ERR_NOMEM;
@@ -513,7 +550,17 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     ufront.push_back((int32_t)F);
     const int64_t N = std::min<int64_t>(n, k);
     int32_t rnk = 0;
-    while (!first_only && sorted_inds < N && ustart + F < U && F > 0) {
+    if (fast && !first_only && sorted_inds < N && F < U && F > 0) {
+        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
+        char* frwork = fwork + pb + align_up((size_t)U * 16, 256);
+        int64_t total = 0;
+        // ufs doubles as the device front-start array
+        if ((rc = fast_fronts(ctx, D, U, (int32_t)F, sorted_inds, N, gsize, ulist, rankU, count,
+                              ufs, frwork, ufront, &total)))
+            return rc;
+        sorted_inds = total;
+    }
+    while (!fast && !first_only && sorted_inds < N && ustart + F < U && F > 0) {
         // peel front `rnk` (ulist[ustart, ustart+F)) -> front rnk+1
         const int64_t waves_target = 8192;
         int64_t nchunks = std::max<int64_t>(1, std::min<int64_t>(max_chunks, waves_target / tiles));

@@ -381,24 +381,50 @@ def test_sort_nondominated_with_nan_fitness(gpu, m):
     assert [f.cpu().numpy().tolist() for f in fronts] == want
 
 
-def test_dominance_ballot_equals_lds_kernel_large(gpu, monkeypatch):
-    """At sizes the oracle cannot finish: the ballot dominance kernel and the
-    LDS-tiled one (DM_DOM_LDS) give identical fronts and selNSGA2 choices."""
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_dominance_paths_agree_large(gpu, monkeypatch, m):
+    """At sizes the oracle cannot finish: the integer-rank symmetric dominance
+    with the device-driven peel (default), the fp64 ballot kernel
+    (DM_DOM_BALLOT) and the LDS-tiled kernel (DM_DOM_LDS) give identical
+    fronts and selNSGA2 choices."""
     from deap_amd import tools
-    rng = np.random.default_rng(31)
+    rng = np.random.default_rng(31 + m)
     n = 30011
-    wv = np.round(rng.uniform(0, 1, size=(n, 3)), 2)  # many equal fitnesses
-    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0, -1.0, 1.0), gtype="f64",
-                           wvalues=wv, valid=np.ones(n))
+    wv = np.round(rng.uniform(0, 1, size=(n, m)), 2)  # many equal fitnesses
+    w = (1.0, -1.0, 1.0, -1.0)[:m]
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
+                           valid=np.ones(n))
     got = []
-    for lds in (False, True):
-        if lds:
-            monkeypatch.setenv("DM_DOM_LDS", "1")
+    for env in (None, "DM_DOM_BALLOT", "DM_DOM_LDS"):
+        monkeypatch.delenv("DM_DOM_BALLOT", raising=False)
+        monkeypatch.delenv("DM_DOM_LDS", raising=False)
+        if env:
+            monkeypatch.setenv(env, "1")
         fronts = tools.sortNondominated(pop, n)
         got.append(([f.cpu().numpy().tolist() for f in fronts],
-                    tools.selNSGA2(pop, n // 2).cpu().numpy().tolist()))
-    assert got[0] == got[1]
+                    tools.selNSGA2(pop, n // 2).cpu().numpy().tolist(),
+                    [len(f) for f in tools.sortNondominated(pop, n // 3)]))
+    assert got[0] == got[1] == got[2]
     assert sum(len(f) for f in got[0][0]) == n
+
+
+def test_front_larger_than_the_lds_sort(gpu, monkeypatch):
+    """A second front of 20,000 unique fitnesses (beyond the 16,384 the
+    one-workgroup LDS sort orders) goes through the host's radix-sort
+    fallback; fronts equal the fp64 LDS path."""
+    from deap_amd import tools
+    k = 20000
+    i = np.arange(k, dtype=np.float64)
+    front0 = np.stack([i, k - i], 1)
+    front1 = np.stack([i - 0.5, k - i - 0.5], 1)  # each dominated by its front-0 twin
+    wv = np.concatenate([front1, front0, front1[:7]])[np.random.default_rng(2).permutation(2 * k + 7)]
+    pop = _dp().from_numpy(np.zeros((len(wv), 1)), weights=(1.0, 1.0), gtype="f64",
+                           wvalues=wv, valid=np.ones(len(wv)))
+    fast = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, len(wv))]
+    monkeypatch.setenv("DM_DOM_LDS", "1")
+    ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, len(wv))]
+    assert [len(f) for f in fast] == [k, k + 7]
+    assert fast == ref
 
 
 def test_sel_best_large_ties(gpu):
