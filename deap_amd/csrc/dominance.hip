@@ -88,6 +88,92 @@ int64_t sd_task_count(int64_t ngroups) {
 
 typedef __attribute__((address_space(4))) const int32_t c4_i32;
 
+// min / max over the M rank differences d_o = y_o - x_o: some x_o > y_o iff
+// min < 0, some x_o < y_o iff max > 0 (ranks < 2^31: no overflow)
+template <int M>
+__device__ __forceinline__ void diff_minmax(const int32_t (&x)[M], const int32_t (&y)[M],
+                                            int32_t& mn, int32_t& mx) {
+    int32_t d[M];
+#pragma unroll
+    for (int o = 0; o < M; ++o) d[o] = y[o] - x[o];
+    mn = d[0];
+    mx = d[0];
+#pragma unroll
+    for (int o = 1; o < M; ++o) {
+        mn = min(mn, d[o]);
+        mx = max(mx, d[o]);
+    }
+}
+
+// t + t + (bit `lane` of mask): one v_addc_co_u32 with the wave mask as the
+// carry-in (lane-local "shift in the bit of this lane" / "count this lane").
+__device__ __forceinline__ uint32_t add2_carry(uint32_t t, uint32_t a, uint64_t mask) {
+    uint32_t out;
+    uint64_t cout;
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %3, %4"
+                 : "=v"(out), "=s"(cout)
+                 : "v"(t), "v"(a), "s"(mask));
+    return out;
+}
+
+// One u-block I (64 rows, nb valid) against the wave's SD_WPW v-blocks.
+// FULL: every v-block J is above I (J > I) — both directions are recorded;
+// otherwise the diagonal band: J < I skipped, J == I direct only.  Rows are
+// walked in descending order so the transposed words build up by doubling
+// (t = 2t + bit): bit j of the word <-> row 64I + j; rows 63..32 feed the
+// high half, 31..0 the low half.
+template <int M, bool FULL, bool HI>
+__device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, int64_t J0,
+                                        const int32_t (&y)[SD_WPW][M], int lane,
+                                        uint32_t (&acc_lo)[SD_WPW], uint32_t (&acc_hi)[SD_WPW],
+                                        uint32_t (&tw)[SD_WPW], int32_t (&vcnt)[SD_WPW],
+                                        int32_t& cpark) {
+    const int jtop = HI ? 63 : 31, jbot = HI ? 32 : 0;
+    for (int j = jtop; j >= jbot; --j) {
+        if (j >= nb) {
+            if (FULL) {
+#pragma unroll
+                for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
+            }
+            continue;
+        }
+        int32_t x[M];
+        const int64_t ub = (I * 64 + j) * 4;
+#pragma unroll
+        for (int o = 0; o < M; ++o) x[o] = Rs[ub + o];
+        int32_t ucnt = 0;
+        const bool me = lane == j;
+#pragma unroll
+        for (int k = 0; k < SD_WPW; ++k) {
+            if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
+            int32_t mn, mx;
+            diff_minmax<M>(x, y[k], mn, mx);
+            const uint64_t gm = __ballot(mn < 0);  // some x > y
+            const uint64_t lm = __ballot(mx > 0);  // some x < y
+            const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
+            const uint64_t dvu = lm & ~gm;         // v dominates u
+            acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
+            acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
+            ucnt += __popcll(dvu);
+            if (FULL) {
+                tw[k] = add2_carry(tw[k], tw[k], dvu);
+                vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
+            }
+        }
+        cpark = me ? ucnt : cpark;
+    }
+}
+
+template <int M, bool FULL>
+__device__ __forceinline__ void sd_block(const int32_t* Rs, int64_t I, int nb, int64_t J0,
+                                         const int32_t (&y)[SD_WPW][M], int lane,
+                                         uint32_t (&acc_lo)[SD_WPW], uint32_t (&acc_hi)[SD_WPW],
+                                         uint32_t (&t_lo)[SD_WPW], uint32_t (&t_hi)[SD_WPW],
+                                         int32_t (&vcnt)[SD_WPW], int32_t& cpark) {
+    sd_rows<M, FULL, true>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, t_hi, vcnt, cpark);
+    sd_rows<M, FULL, false>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, t_lo, vcnt, cpark);
+}
+
 template <int M>
 __global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R4, int64_t U,
                                                       int64_t NB, int64_t NG, int64_t ngroups,
@@ -95,9 +181,11 @@ __global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R
                                                       int16_t* __restrict__ crow,
                                                       int16_t* __restrict__ ccol) {
     const int lane = threadIdx.x & 63;
-    const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform task index (SGPR): everything derived from it is scalar
+    const int64_t t = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     if (t >= ntasks) return;
-    // decode (h, c, g) from the task index (wave-uniform binary search)
+    // decode (h, c, g) from the task index
     const int64_t pair = t >> 1;
     int64_t lo = 0, hi = (ngroups + 1) / 2;  // largest h with S(h) <= pair
     while (hi - lo > 1) {
@@ -132,52 +220,30 @@ __global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R
     int32_t vcnt[SD_WPW] = {0, 0, 0, 0};
     const int64_t I_begin = c * SD_CHUNK;
     const int64_t I_end = std::min<int64_t>(std::min<int64_t>(I_begin + SD_CHUNK, J0 + SD_WPW), NB);
-    const c4_i32* R4s = (const c4_i32*)(const void*)R4;
+    const int32_t* Rs = (const int32_t*)(const void*)R4;
     for (int64_t IG = I_begin; IG < I_end; IG += SD_TG) {
-        uint64_t tacc[SD_WPW][SD_TG];
+        uint32_t t_lo[SD_WPW][SD_TG], t_hi[SD_WPW][SD_TG];
 #pragma unroll
         for (int k = 0; k < SD_WPW; ++k)
 #pragma unroll
-            for (int ii = 0; ii < SD_TG; ++ii) tacc[k][ii] = 0;
+            for (int ii = 0; ii < SD_TG; ++ii) t_lo[k][ii] = t_hi[k][ii] = 0;
 #pragma unroll
         for (int ii = 0; ii < SD_TG; ++ii) {
             const int64_t I = IG + ii;
             if (I >= I_end) break;
             const int nb = (int)std::min<int64_t>(64, U - I * 64);
-            uint32_t acc_lo[SD_WPW], acc_hi[SD_WPW];
+            uint32_t acc_lo[SD_WPW], acc_hi[SD_WPW], tl[SD_WPW], th[SD_WPW];
 #pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) acc_lo[k] = acc_hi[k] = 0;
+            for (int k = 0; k < SD_WPW; ++k) acc_lo[k] = acc_hi[k] = tl[k] = th[k] = 0;
             int32_t cpark = 0;
-            for (int j = 0; j < nb; ++j) {
-                const int64_t ub = (I * 64 + j) * 4;  // scalar loads, u wave-uniform
-                int32_t x[M];
+            if (I < J0)
+                sd_block<M, true>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, tl, th, vcnt, cpark);
+            else
+                sd_block<M, false>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, tl, th, vcnt, cpark);
 #pragma unroll
-                for (int o = 0; o < M; ++o) x[o] = R4s[ub + o];
-                int32_t ucnt = 0;
-#pragma unroll
-                for (int k = 0; k < SD_WPW; ++k) {
-                    const int64_t J = J0 + k;
-                    if (J < I) continue;  // pair handled with the roles swapped
-                    bool gl = false, ll = false;
-#pragma unroll
-                    for (int o = 0; o < M; ++o) {
-                        gl |= x[o] > y[k][o];
-                        ll |= x[o] < y[k][o];
-                    }
-                    const uint64_t gm = __ballot(gl), lm = __ballot(ll);
-                    const uint64_t duv = gm & ~lm;  // u dominates v (v = lane)
-                    const uint64_t dvu = lm & ~gm;  // v dominates u
-                    // park the (wave-uniform) word in lane j: one v_cndmask per half
-                    acc_lo[k] = lane == j ? (uint32_t)duv : acc_lo[k];
-                    acc_hi[k] = lane == j ? (uint32_t)(duv >> 32) : acc_hi[k];
-                    ucnt += __popcll(dvu);
-                    if (J > I) {
-                        const bool vd = ll && !gl, ud = gl && !ll;
-                        tacc[k][ii] |= (uint64_t)vd << j;
-                        vcnt[k] += ud ? 1 : 0;
-                    }
-                }
-                cpark = lane == j ? ucnt : cpark;
+            for (int k = 0; k < SD_WPW; ++k) {
+                t_lo[k][ii] = tl[k];
+                t_hi[k][ii] = th[k];
             }
             // direct words: row 64I + lane, words J >= I of this v-group
             const int64_t u = I * 64 + lane;
@@ -201,13 +267,13 @@ __global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R
                 uint4* q = reinterpret_cast<uint4*>(seg);
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
-                    q[p] = make_uint4((uint32_t)tacc[k][2 * p], (uint32_t)(tacc[k][2 * p] >> 32),
-                                      (uint32_t)tacc[k][2 * p + 1],
-                                      (uint32_t)(tacc[k][2 * p + 1] >> 32));
+                    q[p] = make_uint4(t_lo[k][2 * p], t_hi[k][2 * p], t_lo[k][2 * p + 1],
+                                      t_hi[k][2 * p + 1]);
             } else {
 #pragma unroll
                 for (int ii = 0; ii < SD_TG; ++ii)
-                    if (IG + ii < J && IG + ii < I_end) seg[ii] = tacc[k][ii];
+                    if (IG + ii < J && IG + ii < I_end)
+                        seg[ii] = ((uint64_t)t_hi[k][ii] << 32) | t_lo[k][ii];
             }
         }
     }
