@@ -131,10 +131,8 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
     const int jtop = HI ? 63 : 31, jbot = HI ? 32 : 0;
     for (int j = jtop; j >= jbot; --j) {
         if (j >= nb) {
-            if (FULL) {
 #pragma unroll
-                for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
-            }
+            for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
             continue;
         }
         int32_t x[M];
@@ -155,7 +153,7 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
             acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
             acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
             ucnt += __popcll(dvu);
-            if (FULL) {
+            if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
                 tw[k] = add2_carry(tw[k], tw[k], dvu);
                 vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
             }
