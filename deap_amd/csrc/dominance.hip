@@ -303,11 +303,12 @@ __global__ void sym_count_reduce_kernel(const int16_t* __restrict__ crow,
 struct FrontState {
     int32_t F;         // size of the current front (ulist[ustart, ustart + F))
     int32_t ustart;
-    int32_t nfronts;   // fronts emitted
+    int32_t nfronts;   // fronts emitted after front 0
     int32_t done;
     int32_t overflow;  // candidates exceed the LDS sort: the host orders them
     int32_t ncand;     // candidates of the next front appended by the peel
     int64_t sorted;    // individuals in the emitted fronts
+    int64_t pending;   // individuals of the released candidates (gsize sums)
     int64_t N;         // min(n, k)
     int64_t U;
 };
@@ -336,13 +337,23 @@ __device__ __forceinline__ uint64_t transpose64_w(uint64_t x, int lane) {
     return x;
 }
 
-constexpr int PEEL_GRID_WAVES = 8192;
+constexpr int PEEL_WAVES = 16;  // waves of a peel workgroup (they split the front's members)
 
-__global__ __launch_bounds__(256) void peel_tiled_kernel(const uint64_t* __restrict__ D, int64_t NG,
-                                                         const int32_t* __restrict__ ulist,
-                                                         FrontState* st, int32_t* count,
-                                                         unsigned long long* lastpos,
-                                                         int32_t* cand) {
+// One workgroup owns one 8-word row segment s (v in [512 s, 512 s + 512)):
+// its waves take interleaved 64-member slices of the front, transpose the
+// members' row segments, and the per-wave (dominators, last position) of each
+// v are reduced in LDS.  v is written by this workgroup only, so count and
+// lastpos need no atomics; a v whose count reaches zero is released: its
+// rank, its sort key (last releasing position, U index) and its individual
+// count are recorded here, so the ordering kernel only sorts.
+__global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __restrict__ D,
+                                                          int64_t NG,
+                                                          const int32_t* __restrict__ ulist,
+                                                          const int32_t* __restrict__ gsize,
+                                                          FrontState* st, int32_t* count,
+                                                          uint64_t* ckey, int32_t* rankU) {
+    __shared__ int32_t sdec[PEEL_WAVES][512];
+    __shared__ int32_t slast[PEEL_WAVES][512];
     __shared__ int32_t sF, sust, sstop, snf;
     if (threadIdx.x == 0) {
         sF = st->F;
@@ -352,88 +363,169 @@ __global__ __launch_bounds__(256) void peel_tiled_kernel(const uint64_t* __restr
     }
     __syncthreads();
     if (sstop) return;
-    const int64_t F = sF, U = st->U;
+    const int64_t F = sF, U = st->U, s = blockIdx.x;
     const int32_t* members = ulist + sust;
-    const uint64_t rtag = (uint64_t)(snf) << 32;  // peeled front index, above the position
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    int64_t nch = std::max<int64_t>(1, nwaves / NG);
-    nch = std::min<int64_t>(nch, (F + 63) / 64);
-    int64_t chunk = (F + nch - 1) / nch;
-    chunk = (chunk + 63) / 64 * 64;
-    nch = (F + chunk - 1) / chunk;
-    const int64_t items = NG * nch;
-    for (int64_t it = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; it < items;
-         it += nwaves) {
-        const int64_t s = it % NG, ch = it / NG;
-        int32_t dec[8], last[8];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int32_t dec[8], last[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        dec[w] = 0;
+        last[w] = -1;
+    }
+    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += PEEL_WAVES * 64) {
+        const int64_t j = j0 + lane;
+        const bool ok = j < F;
+        uint64_t seg[8];
+        if (ok) {
+            const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const uint4 v = q[p];
+                seg[2 * p] = ((uint64_t)v.y << 32) | v.x;
+                seg[2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) seg[w] = 0;
+        }
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
-            dec[w] = 0;
-            last[w] = -1;
+            const uint64_t tcol = transpose64_w(seg[w], lane);  // bit i: member j0+i dominates v
+            dec[w] += __popcll(tcol);
+            if (tcol) last[w] = (int32_t)(j0 + 63 - __clzll(tcol));
         }
-        const int64_t jb = ch * chunk, je = std::min<int64_t>(F, jb + chunk);
-        for (int64_t j0 = jb; j0 < je; j0 += 64) {
-            const int64_t j = j0 + lane;
-            const bool ok = j < je;
-            uint64_t seg[8];
-            if (ok) {
-                const int64_t u = members[j];
-                const uint4* q = reinterpret_cast<const uint4*>(D + tword(u, s * 8, NG));
+    }
 #pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const uint4 v = q[p];
-                    seg[2 * p] = ((uint64_t)v.y << 32) | v.x;
-                    seg[2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
+    for (int w = 0; w < 8; ++w) {
+        sdec[wave][w * 64 + lane] = dec[w];
+        slast[wave][w * 64 + lane] = last[w];
+    }
+    __syncthreads();
+    if (threadIdx.x >= 512) return;
+    const int t = threadIdx.x;
+    int32_t d = 0, l = -1;
+#pragma unroll
+    for (int wv = 0; wv < PEEL_WAVES; ++wv) {
+        d += sdec[wv][t];
+        l = max(l, slast[wv][t]);
+    }
+    const int64_t v = s * 512 + t;
+    bool fresh = false;
+    if (v < U && d > 0) {
+        const int32_t left = count[v] - d;
+        count[v] = left;
+        fresh = left == 0;
+    }
+    const unsigned long long fm = __ballot(fresh);
+    if (fm) {
+        const int first = __ffsll(fm) - 1;
+        int32_t base = 0;
+        if (lane == first) base = atomicAdd(&st->ncand, __popcll(fm));
+        base = __shfl(base, first, 64);
+        int64_t gs = 0;
+        if (fresh) {
+            ckey[base + __popcll(fm & ((1ull << lane) - 1))] =
+                ((uint64_t)(uint32_t)l << 32) | (uint32_t)v;
+            rankU[v] = snf + 1;
+            gs = gsize[v];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
+        if (lane == first) atomicAdd((unsigned long long*)&st->pending, (unsigned long long)gs);
+    }
+}
+
+constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
+
+// Bitonic sort of P = 1024 * E keys held E per thread (element i = tid*E + e),
+// ascending: compare-exchanges of stride < E stay in registers, strides below
+// 64 E go through lane shuffles, only the longer ones through LDS (one
+// barrier per stage), so a 2,048-key sort needs 18 barriers instead of 66.
+template <int E>
+__device__ void block_bitonic(uint64_t (&k)[E], uint64_t* lds) {
+    constexpr int P = 1024 * E;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int size = 2; size <= P; size <<= 1) {
+        int stride = size >> 1;
+        if (stride >= 64 * E) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) lds[tid * E + e] = k[e];
+            __syncthreads();
+            for (; stride >= 64 * E; stride >>= 1) {
+                for (int q = tid; q < P / 2; q += 1024) {
+                    const int a = 2 * q - (q & (stride - 1));
+                    const int b = a + stride;
+                    const bool up = (a & size) == 0;
+                    const uint64_t ka = lds[a], kb = lds[b];
+                    if ((ka > kb) == up) {
+                        lds[a] = kb;
+                        lds[b] = ka;
+                    }
                 }
-            } else {
-#pragma unroll
-                for (int w = 0; w < 8; ++w) seg[w] = 0;
+                __syncthreads();
             }
 #pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t tcol = transpose64_w(seg[w], lane);  // bit i: member j0+i dominates v
-                dec[w] += __popcll(tcol);
-                if (tcol) last[w] = (int32_t)(j0 + 63 - __clzll(tcol));
+            for (int e = 0; e < E; ++e) k[e] = lds[tid * E + e];
+            __syncthreads();
+        }
+        for (; stride >= E; stride >>= 1) {
+            const int ls = stride / E;
+            const bool lower = (lane & ls) == 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t p = shfl_xor_u64(k[e], ls);
+                const bool up = ((tid * E + e) & size) == 0;
+                const bool take_min = lower == up;
+                k[e] = take_min ? (p < k[e] ? p : k[e]) : (p > k[e] ? p : k[e]);
             }
         }
+        // strides below E: registers of this thread (compile-time indices)
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const int64_t v = (s * 8 + w) * 64 + lane;
-            bool fresh = false;
-            if (v < U && dec[w] > 0) {
-                atomicMax(&lastpos[v], rtag | (uint32_t)last[w]);
-                fresh = atomicSub(&count[v], dec[w]) == dec[w];
-            }
-            // one append slot per wave for the v released here
-            const unsigned long long fm = __ballot(fresh);
-            if (fm) {
-                const int first = __ffsll(fm) - 1;
-                int32_t base = 0;
-                if (lane == first) base = atomicAdd(&st->ncand, __popcll(fm));
-                base = __shfl(base, first, 64);
-                if (fresh) cand[base + __popcll(fm & ((1ull << lane) - 1))] = (int32_t)v;
+        for (int st2 = E / 2; st2 > 0; st2 >>= 1) {
+            if (st2 >= size) continue;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                if (e & st2) continue;
+                const int f = e | st2;
+                const bool up = ((tid * E + e) & size) == 0;
+                const uint64_t a = k[e], b = k[f];
+                const bool sw = (a > b) == up;
+                k[e] = sw ? b : a;
+                k[f] = sw ? a : b;
             }
         }
     }
 }
 
-constexpr int ORDER_CAP = 16384;  // candidates sorted in LDS by one workgroup
+template <int E>
+__device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, uint64_t* lds) {
+    uint64_t k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = threadIdx.x * E + e;
+        k[e] = i < n ? ckey[i] : ~0ull;
+    }
+    block_bitonic<E>(k, lds);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = threadIdx.x * E + e;
+        if (i < n) out[i] = (int32_t)(uint32_t)k[e];
+    }
+}
 
-// Orders the candidates by (last releasing position, U index), appends the
-// front to ulist and updates the state.  presorted: cand already ordered (the
-// host's fallback for fronts larger than ORDER_CAP).
-__global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, int32_t* cand,
-                                                           const unsigned long long* lastpos,
-                                                           const int32_t* gsize, int32_t* ulist,
-                                                           int32_t* rankU, int32_t* fstarts,
+// Orders the released candidates by (last releasing position, U index),
+// appends them to ulist as the next front and updates the state.
+// presorted: ckey already ordered (the host's radix-sort fallback for fronts
+// larger than ORDER_CAP).
+__global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const uint64_t* ckey,
+                                                           int32_t* ulist, int32_t* fstarts,
                                                            int presorted) {
-    __shared__ uint64_t key[ORDER_CAP];
-    __shared__ int64_t red[1024];
-    __shared__ int32_t sn, sgo;
+    __shared__ uint64_t lds[ORDER_CAP];
+    __shared__ int32_t sn, sgo, snstart;
     if (threadIdx.x == 0) {
         sgo = !(st->done || (st->overflow && !presorted));
         sn = st->ncand;
+        snstart = st->ustart + st->F;
     }
     __syncthreads();
     if (!sgo) return;
@@ -446,59 +538,25 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, int32
         if (threadIdx.x == 0) st->overflow = 1;
         return;
     }
-    const int32_t F = st->F, ust = st->ustart, r = st->nfronts;
-    const int32_t nstart = ust + F;
-    int64_t gsum = 0;
-    if (!presorted) {
-        int P = 1;
-        while (P < n) P <<= 1;
-        for (int i = threadIdx.x; i < P; i += blockDim.x) {
-            if (i < n) {
-                const int32_t v = cand[i];
-                key[i] = ((uint64_t)(uint32_t)lastpos[v] << 32) | (uint32_t)v;
-            } else {
-                key[i] = ~0ull;
-            }
-        }
-        __syncthreads();
-        for (int size = 2; size <= P; size <<= 1) {
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                for (int q = threadIdx.x; q < P / 2; q += blockDim.x) {
-                    const int a = 2 * q - (q & (stride - 1));
-                    const int b = a + stride;
-                    const bool up = (a & size) == 0;
-                    const uint64_t ka = key[a], kb = key[b];
-                    if ((ka > kb) == up) {
-                        key[a] = kb;
-                        key[b] = ka;
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int32_t v = (int32_t)(uint32_t)key[i];
-            ulist[nstart + i] = v;
-            rankU[v] = r + 1;
-            gsum += gsize[v];
-        }
+    int32_t* out = ulist + snstart;
+    if (presorted) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = (int32_t)(uint32_t)ckey[i];
+    } else if (n <= 1024) {
+        order_sorted<1>(ckey, n, out, lds);
+    } else if (n <= 2048) {
+        order_sorted<2>(ckey, n, out, lds);
+    } else if (n <= 4096) {
+        order_sorted<4>(ckey, n, out, lds);
+    } else if (n <= 8192) {
+        order_sorted<8>(ckey, n, out, lds);
     } else {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int32_t v = cand[i];
-            ulist[nstart + i] = v;
-            rankU[v] = r + 1;
-            gsum += gsize[v];
-        }
-    }
-    red[threadIdx.x] = gsum;
-    __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
+        order_sorted<16>(ckey, n, out, lds);
     }
     if (threadIdx.x == 0) {
-        const int64_t sorted = st->sorted + red[0];
+        const int32_t nstart = snstart, r = st->nfronts;
+        const int64_t sorted = st->sorted + st->pending;
         st->sorted = sorted;
+        st->pending = 0;
         st->ustart = nstart;
         st->F = n;
         st->nfronts = r + 1;
@@ -507,16 +565,6 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, int32
         fstarts[r + 2] = nstart + n;
         // emo.py:109: continue while pareto_sorted < N (and fronts remain)
         if (sorted >= st->N || nstart + n >= st->U) st->done = 1;
-    }
-}
-
-// fallback keys for fronts larger than ORDER_CAP
-__global__ void cand_key_kernel(const int32_t* cand, int32_t n, const unsigned long long* lastpos,
-                                uint64_t* keys, int32_t* vals) {
-    DGRID_LOOP(i, n) {
-        const int32_t v = cand[i];
-        keys[i] = ((uint64_t)(uint32_t)lastpos[v] << 32) | (uint32_t)v;
-        vals[i] = v;
     }
 }
 
@@ -529,6 +577,7 @@ __global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, i
     st->overflow = 0;
     st->ncand = 0;
     st->sorted = sorted0;
+    st->pending = 0;
     st->N = N;
     st->U = U;
     fstarts[0] = 0;
@@ -599,14 +648,14 @@ int fast_dom_matrix(hipStream_t s, const int4* R4, int m, int64_t U, uint64_t* D
 }
 
 size_t fast_fronts_bytes(int64_t U) {
-    return align_up(sizeof(FrontState), 256) + align_up((size_t)U * 8, 256) +
-           align_up((size_t)U * 4, 256) + 2 * align_up((size_t)U * 8, 256) +
-           align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
+    return align_up(sizeof(FrontState), 256) + 2 * align_up((size_t)U * 8, 256) +
+           align_up((size_t)U * 8, 256) + 2 * align_up((size_t)U * 4, 256) +
+           radix_sort_temp_bytes(U);
 }
 
 // Fronts 1.. after front 0 (ulist[0, F0), rankU set): peel on the device,
-// checking the status every `batch` fronts.  Fills ufront (front starts in
-// ulist, host) and *sorted (individuals).  `work`: fast_fronts_bytes(U).
+// checking the status every few fronts.  Fills ufront (front starts in ulist,
+// host) and *sorted (individuals).  `work`: fast_fronts_bytes(U).
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t sorted0, int64_t N,
                 const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* work, std::vector<int32_t>& ufront, int64_t* sorted) {
@@ -615,38 +664,39 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t s
     char* p = work;
     FrontState* st = (FrontState*)p;
     p += align_up(sizeof(FrontState), 256);
-    unsigned long long* lastpos = (unsigned long long*)p;
+    uint64_t* ckey = (uint64_t*)p;
     p += align_up((size_t)U * 8, 256);
-    int32_t* cand = (int32_t*)p;
+    uint64_t* ktmp = (uint64_t*)p;
+    p += align_up((size_t)U * 8, 256);
+    uint64_t* kspare = (uint64_t*)p;  // keep the layout of fast_fronts_bytes
+    p += align_up((size_t)U * 8, 256);
+    int32_t* vals = (int32_t*)p;
     p += align_up((size_t)U * 4, 256);
-    uint64_t* keys = (uint64_t*)p;
-    uint64_t* ktmp = (uint64_t*)(p + align_up((size_t)U * 8, 256));
-    p += 2 * align_up((size_t)U * 8, 256);
     int32_t* vtmp = (int32_t*)p;
     p += align_up((size_t)U * 4, 256);
     void* rtemp = p;
-    DM_HIP(hipMemsetAsync(lastpos, 0, (size_t)U * 8, s));
+    (void)kspare;
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     FrontState* hst = (FrontState*)pinned(ctx, sizeof(FrontState));
     if (!hst) return DM_ERR_NOMEM;
-    const unsigned pblocks = PEEL_GRID_WAVES / 4;
     int batch = 4;
     for (;;) {
         for (int b = 0; b < batch; ++b) {
-            peel_tiled_kernel<<<pblocks, 256, 0, s>>>(D, NG, ulist, st, count, lastpos, cand);
-            front_order_kernel<<<1, 1024, 0, s>>>(st, cand, lastpos, gsize, ulist, rankU, fstarts, 0);
+            peel_owned_kernel<<<(unsigned)NG, 1024, 0, s>>>(D, NG, ulist, gsize, st, count, ckey,
+                                                            rankU);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, ulist, fstarts, 0);
         }
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
         DM_HIP(hipStreamSynchronize(s));
         if (hst->done) break;
         if (hst->overflow) {
-            // a front too large for the LDS sort: order it with the radix sort
+            // a front too large for the LDS sort: the radix sort orders its keys
             const int32_t n = hst->ncand;
-            cand_key_kernel<<<dg1(n), 256, 0, s>>>(cand, n, lastpos, keys, cand);
-            int rc = radix_sort_pairs(s, keys, cand, ktmp, vtmp, n, 0, 64, rtemp);
+            DM_HIP(hipMemsetAsync(vals, 0, (size_t)n * 4, s));
+            int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, n, 0, 64, rtemp);
             if (rc) return rc;
-            front_order_kernel<<<1, 1024, 0, s>>>(st, cand, lastpos, gsize, ulist, rankU, fstarts, 1);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, ulist, fstarts, 1);
             DM_LAUNCH_CHECK();
         }
         batch = std::min(batch * 2, 32);
