@@ -68,6 +68,9 @@ __global__ void rank_scatter_kernel(const int32_t* vals, const int32_t* excl, co
 constexpr int SD_WPW = 4;     // 64-v blocks per wave (a v-group)
 constexpr int SD_CHUNK = 16;  // u-blocks per task
 constexpr int SD_TG = 8;      // u-blocks per transposed store (one 64-B row segment)
+#ifndef DM_SD_BATCH
+#define DM_SD_BATCH 4  // rows per scalar rank load (A/B knob: 1 or 4)
+#endif
 
 // word w of row u in the tiled layout (NG = 8-word groups per row)
 __host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NG) {
@@ -129,36 +132,46 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
                                         uint32_t (&tw)[SD_WPW], int32_t (&vcnt)[SD_WPW],
                                         int32_t& cpark) {
     const int jtop = HI ? 63 : 31, jbot = HI ? 32 : 0;
-    for (int j = jtop; j >= jbot; --j) {
-        if (j >= nb) {
+    // four rows per step: their ranks arrive with one 64-B scalar load, so a
+    // wave waits on the scalar cache once per four rows
+    constexpr int B = DM_SD_BATCH;
+    for (int jj = jtop; jj >= jbot; jj -= B) {
+        const c4_i32* xp = (const c4_i32*)(const void*)(Rs + (I * 64 + jj - (B - 1)) * 4);
+        int32_t xs[4 * B];
 #pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
-            continue;
-        }
-        int32_t x[M];
-        const int64_t ub = (I * 64 + j) * 4;
+        for (int q = 0; q < 4 * B; ++q) xs[q] = xp[q];
 #pragma unroll
-        for (int o = 0; o < M; ++o) x[o] = Rs[ub + o];
-        int32_t ucnt = 0;
-        const bool me = lane == j;
+        for (int q = 0; q < B; ++q) {
+            const int j = jj - q;
+            if (j >= nb) {  // rows past the end of the population: shift in zeros
 #pragma unroll
-        for (int k = 0; k < SD_WPW; ++k) {
-            if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
-            int32_t mn, mx;
-            diff_minmax<M>(x, y[k], mn, mx);
-            const uint64_t gm = __ballot(mn < 0);  // some x > y
-            const uint64_t lm = __ballot(mx > 0);  // some x < y
-            const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
-            const uint64_t dvu = lm & ~gm;         // v dominates u
-            acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
-            acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
-            ucnt += __popcll(dvu);
-            if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
-                tw[k] = add2_carry(tw[k], tw[k], dvu);
-                vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
+                for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
+                continue;
             }
+            int32_t x[M];
+#pragma unroll
+            for (int o = 0; o < M; ++o) x[o] = xs[(B - 1 - q) * 4 + o];
+            int32_t ucnt = 0;
+            const bool me = lane == j;
+#pragma unroll
+            for (int k = 0; k < SD_WPW; ++k) {
+                if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
+                int32_t mn, mx;
+                diff_minmax<M>(x, y[k], mn, mx);
+                const uint64_t gm = __ballot(mn < 0);  // some x > y
+                const uint64_t lm = __ballot(mx > 0);  // some x < y
+                const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
+                const uint64_t dvu = lm & ~gm;         // v dominates u
+                acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
+                acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
+                ucnt += __popcll(dvu);
+                if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
+                    tw[k] = add2_carry(tw[k], tw[k], dvu);
+                    vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
+                }
+            }
+            cpark = me ? ucnt : cpark;
         }
-        cpark = me ? ucnt : cpark;
     }
 }
 
@@ -372,27 +385,34 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
         dec[w] = 0;
         last[w] = -1;
     }
-    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += PEEL_WAVES * 64) {
-        const int64_t j = j0 + lane;
-        const bool ok = j < F;
-        uint64_t seg[8];
-        if (ok) {
-            const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
+    // two 64-member slices per step: 8 row-segment loads per lane in flight
+    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += 2 * PEEL_WAVES * 64) {
+        uint64_t seg[2][8];
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const uint4 v = q[p];
-                seg[2 * p] = ((uint64_t)v.y << 32) | v.x;
-                seg[2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
+        for (int h = 0; h < 2; ++h) {
+            const int64_t j = j0 + h * PEEL_WAVES * 64 + lane;
+            if (j < F) {
+                const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const uint4 v = q[p];
+                    seg[h][2 * p] = ((uint64_t)v.y << 32) | v.x;
+                    seg[h][2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) seg[h][w] = 0;
             }
-        } else {
-#pragma unroll
-            for (int w = 0; w < 8; ++w) seg[w] = 0;
         }
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint64_t tcol = transpose64_w(seg[w], lane);  // bit i: member j0+i dominates v
-            dec[w] += __popcll(tcol);
-            if (tcol) last[w] = (int32_t)(j0 + 63 - __clzll(tcol));
+        for (int h = 0; h < 2; ++h) {
+            const int64_t jb = j0 + h * PEEL_WAVES * 64;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const uint64_t tcol = transpose64_w(seg[h][w], lane);  // bit i: member jb+i dominates v
+                dec[w] += __popcll(tcol);
+                if (tcol) last[w] = (int32_t)(jb + 63 - __clzll(tcol));
+            }
         }
     }
 #pragma unroll
@@ -588,7 +608,7 @@ __global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, i
 // host drivers (called from nsga2.hip)
 // ---------------------------------------------------------------------------
 size_t fast_dom_ranks_bytes(int64_t U) {
-    return align_up((size_t)U * 16, 256) + 2 * align_up((size_t)U * 8, 256) +
+    return 2 * align_up((size_t)U * 8, 256) +
            3 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U) + scan_temp_bytes(U);
 }
 

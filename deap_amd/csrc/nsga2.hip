@@ -499,7 +499,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     char* fwork = nullptr;  // fast path: partials | R4 | ranks / fronts work
     if (fast) {
         const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
-        const size_t rb = align_up((size_t)U * 16, 256);
+        const size_t rb = align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
         fwork = (char*)scratch_slot(ctx, 4, pb + rb + std::max(fast_dom_ranks_bytes(U),
                                                                fast_fronts_bytes(U)));
         if (!fwork) return DM_ERR_NOMEM;
@@ -512,7 +512,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     if (fast) {
         const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
         int4* R4 = (int4*)(fwork + pb);
-        char* rwork = fwork + pb + align_up((size_t)U * 16, 256);
+        char* rwork = fwork + pb + align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
         if ((rc = fast_dom_ranks(s, ufit, m, U, R4, rwork))) return rc;
         if ((rc = fast_dom_matrix(s, R4, m, U, D, fwork, count))) return rc;
     } else if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
@@ -552,7 +552,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     int32_t rnk = 0;
     if (fast && !first_only && sorted_inds < N && F < U && F > 0) {
         const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
-        char* frwork = fwork + pb + align_up((size_t)U * 16, 256);
+        char* frwork = fwork + pb + align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
         int64_t total = 0;
         // ufs doubles as the device front-start array
         if ((rc = fast_fronts(ctx, D, U, (int32_t)F, sorted_inds, N, gsize, ulist, rankU, count,
