@@ -67,10 +67,12 @@ __global__ void rank_scatter_kernel(const int32_t* vals, const int32_t* excl, co
 // ---------------------------------------------------------------------------
 constexpr int SD_WPW = 4;     // 64-v blocks per wave (a v-group)
 constexpr int SD_CHUNK = 16;  // u-blocks per task
-constexpr int SD_TG = 8;      // u-blocks per transposed store (one 64-B row segment)
-#ifndef DM_SD_BATCH
-#define DM_SD_BATCH 4  // rows per scalar rank load (A/B knob: 1 or 4)
+#ifndef DM_SD_TG
+#define DM_SD_TG 8
 #endif
+constexpr int SD_TG = DM_SD_TG;  // u-blocks per transposed store (8: one 64-B row segment)
+static_assert(SD_TG == 4 || SD_TG == 8, "transposed store group");
+
 
 // word w of row u in the tiled layout (NG = 8-word groups per row)
 __host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NG) {
@@ -134,44 +136,45 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
     const int jtop = HI ? 63 : 31, jbot = HI ? 32 : 0;
     // four rows per step: their ranks arrive with one 64-B scalar load, so a
     // wave waits on the scalar cache once per four rows
-    constexpr int B = DM_SD_BATCH;
-    for (int jj = jtop; jj >= jbot; jj -= B) {
-        const c4_i32* xp = (const c4_i32*)(const void*)(Rs + (I * 64 + jj - (B - 1)) * 4);
-        int32_t xs[4 * B];
+    // the next row's ranks are loaded (scalar) before this row is compared,
+    // so the scalar-cache latency overlaps a row's worth of compares
+    const c4_i32* xrow = (const c4_i32*)(const void*)Rs;
+    int32_t xn[M];
 #pragma unroll
-        for (int q = 0; q < 4 * B; ++q) xs[q] = xp[q];
+    for (int o = 0; o < M; ++o) xn[o] = xrow[(I * 64 + jtop) * 4 + o];
+    for (int j = jtop; j >= jbot; --j) {
+        int32_t x[M];
 #pragma unroll
-        for (int q = 0; q < B; ++q) {
-            const int j = jj - q;
-            if (j >= nb) {  // rows past the end of the population: shift in zeros
+        for (int o = 0; o < M; ++o) x[o] = xn[o];
+        if (j > jbot) {
 #pragma unroll
-                for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
-                continue;
-            }
-            int32_t x[M];
-#pragma unroll
-            for (int o = 0; o < M; ++o) x[o] = xs[(B - 1 - q) * 4 + o];
-            int32_t ucnt = 0;
-            const bool me = lane == j;
-#pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) {
-                if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
-                int32_t mn, mx;
-                diff_minmax<M>(x, y[k], mn, mx);
-                const uint64_t gm = __ballot(mn < 0);  // some x > y
-                const uint64_t lm = __ballot(mx > 0);  // some x < y
-                const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
-                const uint64_t dvu = lm & ~gm;         // v dominates u
-                acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
-                acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
-                ucnt += __popcll(dvu);
-                if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
-                    tw[k] = add2_carry(tw[k], tw[k], dvu);
-                    vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
-                }
-            }
-            cpark = me ? ucnt : cpark;
+            for (int o = 0; o < M; ++o) xn[o] = xrow[(I * 64 + j - 1) * 4 + o];
         }
+        if (j >= nb) {  // rows past the end of the population: shift in zeros
+#pragma unroll
+            for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
+            continue;
+        }
+        int32_t ucnt = 0;
+        const bool me = lane == j;
+#pragma unroll
+        for (int k = 0; k < SD_WPW; ++k) {
+            if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
+            int32_t mn, mx;
+            diff_minmax<M>(x, y[k], mn, mx);
+            const uint64_t gm = __ballot(mn < 0);  // some x > y
+            const uint64_t lm = __ballot(mx > 0);  // some x < y
+            const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
+            const uint64_t dvu = lm & ~gm;         // v dominates u
+            acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];
+            acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
+            ucnt += __popcll(dvu);
+            if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
+                tw[k] = add2_carry(tw[k], tw[k], dvu);
+                vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
+            }
+        }
+        cpark = me ? ucnt : cpark;
     }
 }
 
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R
             if (IG + SD_TG <= J && IG + SD_TG <= I_end) {
                 uint4* q = reinterpret_cast<uint4*>(seg);
 #pragma unroll
-                for (int p = 0; p < 4; ++p)
+                for (int p = 0; p < SD_TG / 2; ++p)
                     q[p] = make_uint4(t_lo[k][2 * p], t_hi[k][2 * p], t_lo[k][2 * p + 1],
                                       t_hi[k][2 * p + 1]);
             } else {
@@ -385,34 +388,26 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
         dec[w] = 0;
         last[w] = -1;
     }
-    // two 64-member slices per step: 8 row-segment loads per lane in flight
-    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += 2 * PEEL_WAVES * 64) {
-        uint64_t seg[2][8];
+    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += PEEL_WAVES * 64) {
+        const int64_t j = j0 + lane;
+        uint64_t seg[8];
+        if (j < F) {
+            const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int64_t j = j0 + h * PEEL_WAVES * 64 + lane;
-            if (j < F) {
-                const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const uint4 v = q[p];
-                    seg[h][2 * p] = ((uint64_t)v.y << 32) | v.x;
-                    seg[h][2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
-                }
-            } else {
-#pragma unroll
-                for (int w = 0; w < 8; ++w) seg[h][w] = 0;
+            for (int p = 0; p < 4; ++p) {
+                const uint4 v = q[p];
+                seg[2 * p] = ((uint64_t)v.y << 32) | v.x;
+                seg[2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
             }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) seg[w] = 0;
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int64_t jb = j0 + h * PEEL_WAVES * 64;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t tcol = transpose64_w(seg[h][w], lane);  // bit i: member jb+i dominates v
-                dec[w] += __popcll(tcol);
-                if (tcol) last[w] = (int32_t)(jb + 63 - __clzll(tcol));
-            }
+        for (int w = 0; w < 8; ++w) {
+            const uint64_t tcol = transpose64_w(seg[w], lane);  // bit i: member j0+i dominates v
+            dec[w] += __popcll(tcol);
+            if (tcol) last[w] = (int32_t)(j0 + 63 - __clzll(tcol));
         }
     }
 #pragma unroll
