@@ -157,10 +157,8 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
         }
         int32_t ucnt = 0;
         const bool me = lane == j;
-        uint64_t dw[SD_WPW];
 #pragma unroll
         for (int k = 0; k < SD_WPW; ++k) {
-            dw[k] = 0;
             if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
             int32_t mn, mx;
             diff_minmax<M>(x, y[k], mn, mx);
@@ -168,18 +166,13 @@ __device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, in
             const uint64_t lm = __ballot(mx > 0);  // some x < y
             const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
             const uint64_t dvu = lm & ~gm;         // v dominates u
-            dw[k] = duv;
+            acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];  // park the direct word in lane j
+            acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
             ucnt += __popcll(dvu);
             if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
                 tw[k] = add2_carry(tw[k], tw[k], dvu);
                 vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
             }
-        }
-#pragma unroll
-        for (int k = 0; k < SD_WPW; ++k) {  // park the direct words in lane j
-            if (!FULL && J0 + k < I) continue;
-            acc_lo[k] = me ? (uint32_t)dw[k] : acc_lo[k];
-            acc_hi[k] = me ? (uint32_t)(dw[k] >> 32) : acc_hi[k];
         }
         cpark = me ? ucnt : cpark;
     }
