@@ -45,8 +45,31 @@ static dim3 dg1(int64_t n) {
 }
 
 // ---------------------------------------------------------------------------
-// 1. dense ranks per objective: R[u] = int4 {rank_0, .., rank_{m-1}, pad}
+// 1. ranks in objective-0 order
 // ---------------------------------------------------------------------------
+// Unique fitness u gets the position q = pos[u] of its group in the
+// population's lexicographic order (sigma[q] = u), so objective 0 ascends
+// with q.  S[q] = int4 {rank_1, .., rank_{m-1}, rank_0, pad}: objective 0's
+// dense rank is component m-1.
+__global__ void lex_flags_kernel(const double* wv, int m, const int32_t* perm,
+                                 const int32_t* segin, int64_t n, int32_t* fst, int32_t* f0) {
+    DGRID_LOOP(j, n) {
+        fst[j] = (j == 0 || segin[j] != 0) ? 1 : 0;
+        f0[j] = (j == 0 || !(wv[(int64_t)perm[j] * m] == wv[(int64_t)perm[j - 1] * m])) ? 1 : 0;
+    }
+}
+__global__ void lex_sigma_kernel(const int32_t* perm, const int32_t* uidx, const int32_t* fst,
+                                 const int32_t* qex, const int32_t* f0, const int32_t* rex,
+                                 int64_t n, int m, int32_t* sigma, int32_t* pos, int32_t* S) {
+    DGRID_LOOP(j, n) {
+        if (fst[j]) {
+            const int32_t q = qex[j], u = uidx[perm[j]];
+            sigma[q] = u;
+            pos[u] = q;
+            S[(int64_t)q * 4 + (m - 1)] = rex[j] + f0[j] - 1;
+        }
+    }
+}
 __global__ void rank_key_kernel(const double* ufit, int m, int o, int64_t U, uint64_t* keys,
                                 int32_t* vals) {
     DGRID_LOOP(u, U) {
@@ -58,60 +81,95 @@ __global__ void rank_flag_kernel(const uint64_t* keys, int64_t U, int32_t* flag)
     DGRID_LOOP(j, U) flag[j] = (j > 0 && keys[j] != keys[j - 1]) ? 1 : 0;
 }
 __global__ void rank_scatter_kernel(const int32_t* vals, const int32_t* excl, const int32_t* flag,
-                                    int64_t U, int o, int32_t* R4) {
-    DGRID_LOOP(j, U) R4[(int64_t)vals[j] * 4 + o] = excl[j] + flag[j];
+                                    const int32_t* pos, int64_t U, int c, int32_t* S) {
+    DGRID_LOOP(j, U) S[(int64_t)pos[vals[j]] * 4 + c] = excl[j] + flag[j];
 }
 
 // ---------------------------------------------------------------------------
-// 2. symmetric dominance over ranks
+// 2. dominance below the objective-0 diagonal
 // ---------------------------------------------------------------------------
-constexpr int SD_WPW = 4;     // 64-v blocks per wave (a v-group)
-constexpr int SD_CHUNK = 16;  // u-blocks per task
-#ifndef DM_SD_TG
-#define DM_SD_TG 4
+// a can dominate b only if rank_0(a) >= rank_0(b), i.e. (with ties aside)
+// only for b before a in q order.  A wave owns an A-group of TD_WPW 64-row
+// blocks (dominators a in the lanes, ranks in VGPRs) and sweeps the 64-v
+// blocks B that the group's largest rank_0 can reach (v wave-uniform, ranks
+// by scalar loads).  When every rank_0 of B is below every rank_0 of the
+// group ("strict" block pair) objective 0 is decided, and a dominates b iff
+// its other m-1 ranks are >= b's: m-1 compares whose wave masks are ANDed by
+// the SALU.  Otherwise (the group's own blocks, rank_0 ties across blocks)
+// the full test: min(x - y) >= 0 and max(x - y) > 0 over all m ranks.  The
+// mask bit of lane a is shifted into a's word D[a][B] lane-locally
+// (t = 2t + bit, one v_addc); the mask's popcount is b's dominator count
+// contribution, parked in lane b%64 and stored as an int16 partial per
+// (A-group, b).  Words above the reach of a group are never written (the
+// peel skips them), so the matrix costs about half the bytes and compares of
+// the symmetric pass and the strict inner step is m-1 compares + 1 add.
+#ifndef DM_TD_WPW
+#define DM_TD_WPW 4
 #endif
-constexpr int SD_TG = DM_SD_TG;  // u-blocks per transposed store (8: one 64-B row segment)
-static_assert(SD_TG == 4 || SD_TG == 8, "transposed store group");
+constexpr int TD_WPW = DM_TD_WPW;  // 64-row blocks per A-group
+constexpr int TD_SEGS = 2;  // 8-block row segments (512 v) per task
 
-
-// word w of row u in the tiled layout (NG = 8-word groups per row)
-__host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NG) {
-    return ((((u >> 6) * NG + (w >> 3)) << 6) + (u & 63)) * 8 + (w & 7);
+__host__ __device__ __forceinline__ int32_t icomp(const int4& r, int c) {
+    return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w;
 }
 
-// tasks are (h, c, g%2) with v-groups g = 2h, 2h+1 and u-chunks c <= h/2:
-// S(h) = sum_{h' < h} (h'/2 + 1) = (q + r)(q + 1) for h = 2q + r
-__device__ __forceinline__ int64_t sd_tasks_before(int64_t h) {
-    const int64_t q = h >> 1, r = h & 1;
-    return (q + r) * (q + 1);
-}
-int64_t sd_task_count(int64_t ngroups) {
-    const int64_t nh = (ngroups + 1) / 2;
-    const int64_t q = nh >> 1, r = nh & 1;
-    return 2 * (q + r) * (q + 1);
+// word w of row u in the tiled layout: tiles of 64 rows x 4 words (2 KB),
+// NQ = 4-word groups per row.  A wave's store of 4 words of its 64 rows is one
+// contiguous 2 KB; a peel read of 4 words of one row is 32 contiguous bytes.
+__host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NQ) {
+    return ((((u >> 6) * NQ + (w >> 2)) << 6) + (u & 63)) * 4 + (w & 3);
 }
 
-typedef __attribute__((address_space(4))) const int32_t c4_i32;
-
-// min / max over the M rank differences d_o = y_o - x_o: some x_o > y_o iff
-// min < 0, some x_o < y_o iff max > 0 (ranks < 2^31: no overflow)
-template <int M>
-__device__ __forceinline__ void diff_minmax(const int32_t (&x)[M], const int32_t (&y)[M],
-                                            int32_t& mn, int32_t& mx) {
-    int32_t d[M];
-#pragma unroll
-    for (int o = 0; o < M; ++o) d[o] = y[o] - x[o];
-    mn = d[0];
-    mx = d[0];
-#pragma unroll
-    for (int o = 1; o < M; ++o) {
-        mn = min(mn, d[o]);
-        mx = max(mx, d[o]);
+// nseg[g]: 8-block segments of v the rows of A-group g reach (every v whose
+// rank_0 <= the group's largest); toff[g]: first task of g (TD_SEGS segments
+// per task), toff[ngroups] = tasks.  One workgroup; nseg is nondecreasing.
+__global__ __launch_bounds__(1024) void tri_plan_kernel(const int4* S, int m, int64_t U,
+                                                        int64_t NG, int64_t ngroups,
+                                                        int32_t* nseg, int32_t* toff,
+                                                        int32_t* counter) {
+    __shared__ int32_t sh[1024];
+    __shared__ int32_t carry;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        carry = 0;
+        *counter = 0;
     }
+    __syncthreads();
+    for (int64_t base = 0; base < ngroups; base += 1024) {
+        const int64_t g = base + tid;
+        int32_t nt = 0;
+        if (g < ngroups) {
+            const int64_t last = std::min<int64_t>((g + 1) * TD_WPW * 64, U) - 1;
+            const int32_t rmax = icomp(S[last], m - 1);
+            int64_t lo = last, hi = U - 1;  // last q with rank_0 <= rmax
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (icomp(S[mid], m - 1) <= rmax) lo = mid;
+                else hi = mid - 1;
+            }
+            const int32_t ns = (int32_t)std::min<int64_t>(NG, (lo >> 9) + 1);
+            nseg[g] = ns;
+            nt = (ns + TD_SEGS - 1) / TD_SEGS;
+        }
+        sh[tid] = nt;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int32_t add = tid >= off ? sh[tid - off] : 0;
+            __syncthreads();
+            sh[tid] += add;
+            __syncthreads();
+        }
+        const int32_t c0 = carry;
+        if (g < ngroups) toff[g] = c0 + sh[tid] - nt;
+        __syncthreads();
+        if (tid == 1023) carry = c0 + sh[1023];
+        __syncthreads();
+    }
+    if (tid == 0) toff[ngroups] = carry;
 }
 
 // t + t + (bit `lane` of mask): one v_addc_co_u32 with the wave mask as the
-// carry-in (lane-local "shift in the bit of this lane" / "count this lane").
+// carry-in (lane-local "shift in the bit of this lane").
 __device__ __forceinline__ uint32_t add2_carry(uint32_t t, uint32_t a, uint64_t mask) {
     uint32_t out;
     uint64_t cout;
@@ -121,195 +179,206 @@ __device__ __forceinline__ uint32_t add2_carry(uint32_t t, uint32_t a, uint64_t 
     return out;
 }
 
-// One u-block I (64 rows, nb valid) against the wave's SD_WPW v-blocks.
-// FULL: every v-block J is above I (J > I) — both directions are recorded;
-// otherwise the diagonal band: J < I skipped, J == I direct only.  Rows are
-// walked in descending order so the transposed words build up by doubling
-// (t = 2t + bit): bit j of the word <-> row 64I + j; rows 63..32 feed the
-// high half, 31..0 the low half.
-template <int M, bool FULL, bool HI>
-__device__ __forceinline__ void sd_rows(const int32_t* Rs, int64_t I, int nb, int64_t J0,
-                                        const int32_t (&y)[SD_WPW][M], int lane,
-                                        uint32_t (&acc_lo)[SD_WPW], uint32_t (&acc_hi)[SD_WPW],
-                                        uint32_t (&tw)[SD_WPW], int32_t (&vcnt)[SD_WPW],
-                                        int32_t& cpark) {
-    const int jtop = HI ? 63 : 31, jbot = HI ? 32 : 0;
-    // four rows per step: their ranks arrive with one 64-B scalar load, so a
-    // wave waits on the scalar cache once per four rows
-    // the next row's ranks are loaded (scalar) before this row is compared,
-    // so the scalar-cache latency overlaps a row's worth of compares
-    const c4_i32* xrow = (const c4_i32*)(const void*)Rs;
-    int32_t xn[M];
+// v_writelane_b32 with an immediate lane: lane L of old <- the wave-uniform val
+template <int L>
+__device__ __forceinline__ int32_t writelane(int32_t old, int32_t val) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(val), "i"(L));
+    return old;
+}
+
+// one row b (ranks y) against the group's lanes: shift the dominance bits
+// into tw, return b's dominator count over the group
+template <int M, bool STRICT>
+__device__ __forceinline__ int32_t td_row(const int4 y4, const int32_t (&x)[TD_WPW][M],
+                                          uint32_t (&tw)[TD_WPW]) {
+    int32_t y[M];
+    y[0] = y4.x;
+    y[1] = y4.y;
+    if constexpr (M > 2) y[2] = y4.z;
+    if constexpr (M > 3) y[3] = y4.w;
+    int32_t cnt = 0;
 #pragma unroll
-    for (int o = 0; o < M; ++o) xn[o] = xrow[(I * 64 + jtop) * 4 + o];
-    for (int j = jtop; j >= jbot; --j) {
-        int32_t x[M];
+    for (int k = 0; k < TD_WPW; ++k) {
+        uint64_t msk;
+        if constexpr (STRICT) {
+            msk = __ballot(x[k][0] >= y[0]);
 #pragma unroll
-        for (int o = 0; o < M; ++o) x[o] = xn[o];
-        if (j > jbot) {
+            for (int o = 1; o < M - 1; ++o) msk &= __ballot(x[k][o] >= y[o]);
+        } else {
+            int32_t mn = x[k][0] - y[0], mx = mn;
 #pragma unroll
-            for (int o = 0; o < M; ++o) xn[o] = xrow[(I * 64 + j - 1) * 4 + o];
+            for (int o = 1; o < M; ++o) {
+                const int32_t d = x[k][o] - y[o];
+                mn = min(mn, d);
+                mx = max(mx, d);
+            }
+            msk = __ballot(mn >= 0) & __ballot(mx > 0);
         }
-        if (j >= nb) {  // rows past the end of the population: shift in zeros
+        tw[k] = add2_carry(tw[k], tw[k], msk);
+#ifndef DM_TD_NOCOUNT
+        cnt += __popcll(msk);
+#endif
+    }
+    return cnt;
+}
+
+// rows JTOP..JTOP-31 of a full block (descending: bit j of the word <-> row
+// j); the block's ranks are in the wave's LDS buffer (broadcast reads), the
+// next four rows read ahead
+template <int M, bool STRICT, int JTOP, int J4 = 0>
+__device__ __forceinline__ void td_half(const int4* L, const int32_t (&x)[TD_WPW][M],
+                                        uint32_t (&tw)[TD_WPW], int32_t& cpark, const int4 (&cur)[4]) {
+    int4 nxt[4];
+    if constexpr (J4 + 4 < 32) {
 #pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) tw[k] += tw[k];
+        for (int i = 0; i < 4; ++i) nxt[i] = L[JTOP - J4 - 4 - i];
+    }
+    cpark = writelane<JTOP - J4>(cpark, td_row<M, STRICT>(cur[0], x, tw));
+    cpark = writelane<JTOP - J4 - 1>(cpark, td_row<M, STRICT>(cur[1], x, tw));
+    cpark = writelane<JTOP - J4 - 2>(cpark, td_row<M, STRICT>(cur[2], x, tw));
+    cpark = writelane<JTOP - J4 - 3>(cpark, td_row<M, STRICT>(cur[3], x, tw));
+    if constexpr (J4 + 4 < 32) td_half<M, STRICT, JTOP, J4 + 4>(L, x, tw, cpark, nxt);
+}
+template <int M, bool STRICT, int JTOP>
+__device__ __forceinline__ void td_half(const int4* L, const int32_t (&x)[TD_WPW][M],
+                                        uint32_t (&tw)[TD_WPW], int32_t& cpark) {
+    int4 cur[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cur[i] = L[JTOP - i];
+    td_half<M, STRICT, JTOP, 0>(L, x, tw, cpark, cur);
+}
+
+// the last, partial block (nb < 64 rows): rows past the end shift in zeros
+template <int M, bool STRICT>
+__device__ void td_partial_half(const int4* L, int jtop, int nb,
+                                const int32_t (&x)[TD_WPW][M], uint32_t (&tw)[TD_WPW],
+                                int32_t& cpark) {
+    for (int j = jtop; j > jtop - 32; --j) {
+        if (j >= nb) {
+#pragma unroll
+            for (int k = 0; k < TD_WPW; ++k) tw[k] += tw[k];
             continue;
         }
-        int32_t ucnt = 0;
-        const bool me = lane == j;
-#pragma unroll
-        for (int k = 0; k < SD_WPW; ++k) {
-            if (!FULL && J0 + k < I) continue;  // pair handled with the roles swapped
-            int32_t mn, mx;
-            diff_minmax<M>(x, y[k], mn, mx);
-            const uint64_t gm = __ballot(mn < 0);  // some x > y
-            const uint64_t lm = __ballot(mx > 0);  // some x < y
-            const uint64_t duv = gm & ~lm;         // u dominates v (v = lane)
-            const uint64_t dvu = lm & ~gm;         // v dominates u
-            acc_lo[k] = me ? (uint32_t)duv : acc_lo[k];  // park the direct word in lane j
-            acc_hi[k] = me ? (uint32_t)(duv >> 32) : acc_hi[k];
-            ucnt += __popcll(dvu);
-            if (FULL || J0 + k > I) {  // off-diagonal: the transposed word and v's count too
-                tw[k] = add2_carry(tw[k], tw[k], dvu);
-                vcnt[k] = (int32_t)add2_carry((uint32_t)vcnt[k], 0u, duv);
-            }
-        }
-        cpark = me ? ucnt : cpark;
+        const int32_t cnt = td_row<M, STRICT>(L[j], x, tw);
+        cpark = (int)(threadIdx.x & 63) == j ? cnt : cpark;
     }
 }
 
-template <int M, bool FULL>
-__device__ __forceinline__ void sd_block(const int32_t* Rs, int64_t I, int nb, int64_t J0,
-                                         const int32_t (&y)[SD_WPW][M], int lane,
-                                         uint32_t (&acc_lo)[SD_WPW], uint32_t (&acc_hi)[SD_WPW],
-                                         uint32_t (&t_lo)[SD_WPW], uint32_t (&t_hi)[SD_WPW],
-                                         int32_t (&vcnt)[SD_WPW], int32_t& cpark) {
-    sd_rows<M, FULL, true>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, t_hi, vcnt, cpark);
-    sd_rows<M, FULL, false>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, t_lo, vcnt, cpark);
-}
-
+// Persistent: each wave takes tasks (A-group g, TD_SEGS segments of B) from
+// an atomic counter until toff[ngroups] are done.
 template <int M>
-__global__ __launch_bounds__(256) void sym_dom_kernel(const int4* __restrict__ R4, int64_t U,
-                                                      int64_t NB, int64_t NG, int64_t ngroups,
-                                                      int64_t ntasks, uint64_t* __restrict__ D,
-                                                      int16_t* __restrict__ crow,
-                                                      int16_t* __restrict__ ccol) {
+__global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S, int64_t U,
+                                                      int64_t NB, int64_t NQ, int64_t ngroups,
+                                                      const int32_t* __restrict__ nseg,
+                                                      const int32_t* __restrict__ toff,
+                                                      int32_t* counter, uint64_t* __restrict__ D,
+                                                      int16_t* __restrict__ part) {
+    __shared__ int4 sbuf[4][64];  // per wave: the ranks of the current v block
     const int lane = threadIdx.x & 63;
-    // wave-uniform task index (SGPR): everything derived from it is scalar
-    const int64_t t = __builtin_amdgcn_readfirstlane(
-        (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-    if (t >= ntasks) return;
-    // decode (h, c, g) from the task index
-    const int64_t pair = t >> 1;
-    int64_t lo = 0, hi = (ngroups + 1) / 2;  // largest h with S(h) <= pair
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (sd_tasks_before(mid) <= pair) lo = mid;
-        else hi = mid;
-    }
-    const int64_t h = lo;
-    const int64_t c = pair - sd_tasks_before(h);
-    const int64_t g = 2 * h + (t & 1);
-    if (g >= ngroups) return;
-    const int64_t J0 = g * SD_WPW;
-    int32_t y[SD_WPW][M];
-#pragma unroll
-    for (int k = 0; k < SD_WPW; ++k) {
-        const int64_t v = (J0 + k) * 64 + lane;
-        if (v < U) {
-            const int4 r = R4[v];
-            y[k][0] = r.x;
-            y[k][1] = r.y;
-            if constexpr (M > 2) y[k][2] = r.z;
-            if constexpr (M > 3) y[k][3] = r.w;
-        } else {
-            // a lane past the end: x > y in objective 0 and x < y in
-            // objective 1 for every u, so neither side dominates
-            y[k][0] = -1;
-            y[k][1] = INT32_MAX;
-            if constexpr (M > 2) y[k][2] = 0;
-            if constexpr (M > 3) y[k][3] = 0;
+    int4* L = sbuf[threadIdx.x >> 6];
+    const int64_t Upad = NB * 64;
+    const int32_t total = toff[ngroups];
+    for (;;) {
+        int32_t t = 0;
+        if (lane == 0) t = atomicAdd(counter, 1);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= total) break;
+        int64_t lo = 0, hi = ngroups - 1;  // last g with toff[g] <= t
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (toff[mid] <= t) lo = mid;
+            else hi = mid - 1;
         }
-    }
-    int32_t vcnt[SD_WPW] = {0, 0, 0, 0};
-    const int64_t I_begin = c * SD_CHUNK;
-    const int64_t I_end = std::min<int64_t>(std::min<int64_t>(I_begin + SD_CHUNK, J0 + SD_WPW), NB);
-    const int32_t* Rs = (const int32_t*)(const void*)R4;
-    for (int64_t IG = I_begin; IG < I_end; IG += SD_TG) {
-        uint32_t t_lo[SD_WPW][SD_TG], t_hi[SD_WPW][SD_TG];
+        const int64_t g = lo, c = t - toff[g];
+        const int64_t A0 = g * TD_WPW;
+        int32_t x[TD_WPW][M];
 #pragma unroll
-        for (int k = 0; k < SD_WPW; ++k)
+        for (int k = 0; k < TD_WPW; ++k) {
+            const int64_t r = (A0 + k) * 64 + lane;
+            const int4 xr = r < U ? S[r] : make_int4(-1, -1, -1, -1);  // past the end: no bits
+            x[k][0] = xr.x;
+            x[k][1] = xr.y;
+            if constexpr (M > 2) x[k][2] = xr.z;
+            if constexpr (M > 3) x[k][3] = xr.w;
+        }
+        const int32_t rmin = __builtin_amdgcn_readfirstlane(icomp(S[A0 * 64], M - 1));
+        const int64_t B0 = c * TD_SEGS * 8;
+        const int64_t B1 = std::min<int64_t>(std::min<int64_t>((int64_t)nseg[g], (c + 1) * TD_SEGS) * 8, NB);
+        int4 nxt = B0 < B1 ? S[B0 * 64 + lane] : make_int4(0, 0, 0, 0);
+        // words of 4 consecutive v blocks, stored together (whole 2 KB tiles)
+        uint64_t wq[TD_WPW][4];
 #pragma unroll
-            for (int ii = 0; ii < SD_TG; ++ii) t_lo[k][ii] = t_hi[k][ii] = 0;
+        for (int k = 0; k < TD_WPW; ++k)
 #pragma unroll
-        for (int ii = 0; ii < SD_TG; ++ii) {
-            const int64_t I = IG + ii;
-            if (I >= I_end) break;
-            const int nb = (int)std::min<int64_t>(64, U - I * 64);
-            uint32_t acc_lo[SD_WPW], acc_hi[SD_WPW], tl[SD_WPW], th[SD_WPW];
+            for (int i = 0; i < 4; ++i) wq[k][i] = 0;
+        for (int64_t B = B0; B < B1; ++B) {
+            const int nb = (int)std::min<int64_t>(64, U - B * 64);
+            L[lane] = nxt;  // the previous block's reads were issued before (in-order LDS)
+            if (B + 1 < B1) nxt = S[(B + 1) * 64 + lane];
+            const bool strict = __builtin_amdgcn_readfirstlane(icomp(L[nb - 1], M - 1)) < rmin;
+            uint32_t th[TD_WPW], tl[TD_WPW];
 #pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) acc_lo[k] = acc_hi[k] = tl[k] = th[k] = 0;
+            for (int k = 0; k < TD_WPW; ++k) th[k] = tl[k] = 0;
             int32_t cpark = 0;
-            if (I < J0)
-                sd_block<M, true>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, tl, th, vcnt, cpark);
-            else
-                sd_block<M, false>(Rs, I, nb, J0, y, lane, acc_lo, acc_hi, tl, th, vcnt, cpark);
-#pragma unroll
-            for (int k = 0; k < SD_WPW; ++k) {
-                t_lo[k][ii] = tl[k];
-                t_hi[k][ii] = th[k];
-            }
-            // direct words: row 64I + lane, words J >= I of this v-group
-            const int64_t u = I * 64 + lane;
-            if (u < U) {
-#pragma unroll
-                for (int k = 0; k < SD_WPW; ++k) {
-                    const int64_t J = J0 + k;
-                    if (J >= I && J < NB) D[tword(u, J, NG)] = ((uint64_t)acc_hi[k] << 32) | acc_lo[k];
+            if (nb == 64) {
+                if (strict) {
+                    td_half<M, true, 63>(L, x, th, cpark);
+                    td_half<M, true, 31>(L, x, tl, cpark);
+                } else {
+                    td_half<M, false, 63>(L, x, th, cpark);
+                    td_half<M, false, 31>(L, x, tl, cpark);
                 }
-                crow[g * U + u] = (int16_t)cpark;
-            }
-        }
-        // transposed words: row 64J + lane, words I (< J) of this 8-block group
-#pragma unroll
-        for (int k = 0; k < SD_WPW; ++k) {
-            const int64_t J = J0 + k;
-            const int64_t v = J * 64 + lane;
-            if (J >= NB || v >= U || IG >= J) continue;
-            uint64_t* seg = D + tword(v, IG, NG);  // 64-B aligned row segment
-            if (IG + SD_TG <= J && IG + SD_TG <= I_end) {
-                uint4* q = reinterpret_cast<uint4*>(seg);
-#pragma unroll
-                for (int p = 0; p < SD_TG / 2; ++p)
-                    q[p] = make_uint4(t_lo[k][2 * p], t_hi[k][2 * p], t_lo[k][2 * p + 1],
-                                      t_hi[k][2 * p + 1]);
+            } else if (strict) {
+                td_partial_half<M, true>(L, 63, nb, x, th, cpark);
+                td_partial_half<M, true>(L, 31, nb, x, tl, cpark);
             } else {
+                td_partial_half<M, false>(L, 63, nb, x, th, cpark);
+                td_partial_half<M, false>(L, 31, nb, x, tl, cpark);
+            }
+            part[g * Upad + B * 64 + lane] = (int16_t)cpark;
+            const int bq = (int)(B & 3);
 #pragma unroll
-                for (int ii = 0; ii < SD_TG; ++ii)
-                    if (IG + ii < J && IG + ii < I_end)
-                        seg[ii] = ((uint64_t)t_hi[k][ii] << 32) | t_lo[k][ii];
+            for (int k = 0; k < TD_WPW; ++k) {
+                const uint64_t w = ((uint64_t)th[k] << 32) | tl[k];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wq[k][i] = bq == i ? w : wq[k][i];
+            }
+            if (bq == 3 || B + 1 == B1) {
+#pragma unroll
+                for (int k = 0; k < TD_WPW; ++k) {
+                    if (A0 + k < NB) {
+                        uint4* q = reinterpret_cast<uint4*>(D + tword((A0 + k) * 64 + lane, B & ~3ll, NQ));
+                        q[0] = make_uint4((uint32_t)wq[k][0], (uint32_t)(wq[k][0] >> 32),
+                                          (uint32_t)wq[k][1], (uint32_t)(wq[k][1] >> 32));
+                        q[1] = make_uint4((uint32_t)wq[k][2], (uint32_t)(wq[k][2] >> 32),
+                                          (uint32_t)wq[k][3], (uint32_t)(wq[k][3] >> 32));
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) wq[k][i] = 0;
+                }
             }
         }
-    }
-#pragma unroll
-    for (int k = 0; k < SD_WPW; ++k) {
-        const int64_t v = (J0 + k) * 64 + lane;
-        if (v < U) ccol[c * U + v] = (int16_t)vcnt[k];
     }
 }
 
-// count[x] = sum over the v-groups g >= I(x)/4 of crow[g][x] + sum over the
-// u-chunks c <= (I(x)/4)/4 of ccol[c][x]
-__global__ void sym_count_reduce_kernel(const int16_t* __restrict__ crow,
-                                        const int16_t* __restrict__ ccol, int64_t U,
-                                        int64_t ngroups, int32_t* __restrict__ count) {
-    DGRID_LOOP(x, U) {
-        const int64_t g0 = (x >> 6) / SD_WPW;
+// count[sigma[q]] (U order, front 0) = countq[q] (q order, the peel) = sum
+// over the A-groups reaching q's segment of part[g][q]
+__global__ void tri_count_kernel(const int16_t* __restrict__ part, const int32_t* __restrict__ nseg,
+                                 const int32_t* __restrict__ sigma, int64_t U, int64_t Upad,
+                                 int64_t ngroups, int32_t* __restrict__ count,
+                                 int32_t* __restrict__ countq) {
+    DGRID_LOOP(q, U) {
+        const int32_t sq = (int32_t)(q >> 9);
+        int64_t lo = 0, hi = ngroups;  // first g with nseg[g] > sq
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (nseg[mid] > sq) hi = mid;
+            else lo = mid + 1;
+        }
         int32_t cnt = 0;
-        for (int64_t g = g0; g < ngroups; ++g) cnt += crow[g * U + x];
-        const int64_t cmax = g0 / 4;  // chunks of the tasks of v-group g0
-        for (int64_t c = 0; c <= cmax; ++c) cnt += ccol[c * U + x];
-        count[x] = cnt;
+        for (int64_t g = lo; g < ngroups; ++g) cnt += part[g * Upad + q];
+        count[sigma[q]] = cnt;
+        countq[q] = cnt;
     }
 }
 
@@ -334,40 +403,98 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
     const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), m, 64);
     return ((uint64_t)hi << 32) | lo;
 }
-// 64x64 bit transpose across the wave: in lane i bit j = A[i][j]; out lane j
-// bit i = A[i][j].
-__device__ __forceinline__ uint64_t transpose64_w(uint64_t x, int lane) {
-    const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull,
-                               0x00FF00FF00FF00FFull, 0x0F0F0F0F0F0F0F0Full,
-                               0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-    for (int st = 0; st < 6; ++st) {
-        const int s = 32 >> st;
-        const uint64_t mlo = masks[st];
-        const uint64_t y = shfl_xor_u64(x, s);
-        if (lane & s)
-            x = (x & ~mlo) | ((y & ~mlo) >> s);
-        else
-            x = (x & mlo) | ((y & mlo) << s);
+// 64x64 bit transposes across the wave (in lane i bit j = A[i][j]; out lane j
+// bit i = A[i][j]) of N words at once, stage by stage so that the lane
+// exchanges of all N words are in flight together, without branches: the
+// stage of distance s swaps 2s-bit blocks between lanes i and i^s.  s = 32
+// moves whole 32-bit halves; s = 16 and 8 recombine bytes with one v_perm;
+// s = 4, 2, 1 rotate the partner's half and merge with one bit-field insert,
+// the per-lane selectors and masks computed once.
+struct Transposer {
+    uint32_t sel16, sel8, m4, m2, m1, r4, r2, r1;
+    bool low32;
+    __device__ explicit Transposer(int lane) {
+        sel16 = (lane & 16) ? 0x03020706u : 0x05040100u;
+        sel8 = (lane & 8) ? 0x03070105u : 0x06020400u;
+        m4 = (lane & 4) ? ~0x0F0F0F0Fu : 0x0F0F0F0Fu;
+        m2 = (lane & 2) ? ~0x33333333u : 0x33333333u;
+        m1 = (lane & 1) ? ~0x55555555u : 0x55555555u;
+        r4 = (lane & 4) ? 4u : 28u;
+        r2 = (lane & 2) ? 2u : 30u;
+        r1 = (lane & 1) ? 1u : 31u;
+        low32 = (lane & 32) == 0;
     }
-    return x;
-}
+    template <int N>
+    __device__ __forceinline__ void run(uint32_t (&lo)[N], uint32_t (&hi)[N]) const {
+        {  // s = 32: lanes < 32 take the partner's low half as their high half
+            uint32_t r[N];
+#pragma unroll
+            for (int w = 0; w < N; ++w) r[w] = __shfl_xor(low32 ? hi[w] : lo[w], 32, 64);
+#pragma unroll
+            for (int w = 0; w < N; ++w) {
+                hi[w] = low32 ? r[w] : hi[w];
+                lo[w] = low32 ? lo[w] : r[w];
+            }
+        }
+        bytes<N>(lo, hi, 16, sel16);
+        bytes<N>(lo, hi, 8, sel8);
+        bits<N>(lo, hi, 4, m4, r4);
+        bits<N>(lo, hi, 2, m2, r2);
+        bits<N>(lo, hi, 1, m1, r1);
+    }
+    template <int N>
+    __device__ __forceinline__ static void bytes(uint32_t (&lo)[N], uint32_t (&hi)[N], int s,
+                                                 uint32_t sel) {
+        uint32_t rl[N], rh[N];
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            rl[w] = __shfl_xor(lo[w], s, 64);
+            rh[w] = __shfl_xor(hi[w], s, 64);
+        }
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            lo[w] = __builtin_amdgcn_perm(rl[w], lo[w], sel);
+            hi[w] = __builtin_amdgcn_perm(rh[w], hi[w], sel);
+        }
+    }
+    template <int N>
+    __device__ __forceinline__ static void bits(uint32_t (&lo)[N], uint32_t (&hi)[N], int s,
+                                                uint32_t m, uint32_t rot) {
+        uint32_t rl[N], rh[N];
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            rl[w] = __shfl_xor(lo[w], s, 64);
+            rh[w] = __shfl_xor(hi[w], s, 64);
+        }
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            const uint32_t tl = __builtin_amdgcn_alignbit(rl[w], rl[w], rot);
+            const uint32_t th = __builtin_amdgcn_alignbit(rh[w], rh[w], rot);
+            lo[w] = (m & lo[w]) | (~m & tl);
+            hi[w] = (m & hi[w]) | (~m & th);
+        }
+    }
+};
 
-constexpr int PEEL_WAVES = 16;  // waves of a peel workgroup (they split the front's members)
+constexpr int PEEL_WAVES = 8;   // waves of a peel workgroup (they split the front's members)
+constexpr int PEEL_BATCH = 2;   // member chunks per wave in flight
 
-// One workgroup owns one 8-word row segment s (v in [512 s, 512 s + 512)):
-// its waves take interleaved 64-member slices of the front, transpose the
-// members' row segments, and the per-wave (dominators, last position) of each
-// v are reduced in LDS.  v is written by this workgroup only, so count and
-// lastpos need no atomics; a v whose count reaches zero is released: its
-// rank, its sort key (last releasing position, U index) and its individual
-// count are recorded here, so the ordering kernel only sorts.
-__global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __restrict__ D,
-                                                          int64_t NG,
-                                                          const int32_t* __restrict__ ulist,
-                                                          const int32_t* __restrict__ gsize,
-                                                          FrontState* st, int32_t* count,
-                                                          uint64_t* ckey, int32_t* rankU) {
+// One workgroup (8 waves, two per CU resident) owns one 8-word row segment s
+// (v in [512 s, 512 s + 512), q order): its waves take interleaved 64-member
+// slices of the front, transpose the members' row segments, and the per-wave
+// (dominators, last position) of each v are reduced in LDS.  v is written by
+// this workgroup only, so countq needs no atomics; a v whose count reaches
+// zero is released: its rank, its sort key (last releasing position, U index),
+// its row and its individual count are recorded here, so the ordering kernel
+// only sorts.
+__global__ __launch_bounds__(512) void peel_owned_kernel(const uint64_t* __restrict__ D,
+                                                         int64_t NQ,
+                                                         const int2* __restrict__ mrow,
+                                                         const int32_t* __restrict__ gsize,
+                                                         const int32_t* __restrict__ sigma,
+                                                         FrontState* st, int32_t* countq,
+                                                         uint64_t* ckey, int32_t* cq,
+                                                         int32_t* rankU) {
     __shared__ int32_t sdec[PEEL_WAVES][512];
     __shared__ int32_t slast[PEEL_WAVES][512];
     __shared__ int32_t sF, sust, sstop, snf;
@@ -380,34 +507,66 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
     __syncthreads();
     if (sstop) return;
     const int64_t F = sF, U = st->U, s = blockIdx.x;
-    const int32_t* members = ulist + sust;
+    const int2* members = mrow + sust;  // (row in q order, segments it reaches)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const Transposer tr(lane);
     int32_t dec[8], last[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
         dec[w] = 0;
         last[w] = -1;
     }
-    for (int64_t j0 = (int64_t)wave * 64; j0 < F; j0 += PEEL_WAVES * 64) {
-        const int64_t j = j0 + lane;
-        uint64_t seg[8];
-        if (j < F) {
-            const uint4* q = reinterpret_cast<const uint4*>(D + tword(members[j], s * 8, NG));
+    constexpr int64_t STEP = PEEL_WAVES * 64;
+    // member rows of the next batch are loaded one batch ahead
+    int2 mr[PEEL_BATCH];
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const uint4 v = q[p];
-                seg[2 * p] = ((uint64_t)v.y << 32) | v.x;
-                seg[2 * p + 1] = ((uint64_t)v.w << 32) | v.z;
+    for (int b = 0; b < PEEL_BATCH; ++b) {
+        const int64_t j = (int64_t)wave * 64 + b * STEP + lane;
+        mr[b] = j < F ? members[j] : make_int2(0, 0);
+    }
+    for (int64_t jb = (int64_t)wave * 64; jb < F; jb += STEP * PEEL_BATCH) {
+        uint64_t seg[PEEL_BATCH][8];
+        bool has[PEEL_BATCH];
+#pragma unroll
+        for (int b = 0; b < PEEL_BATCH; ++b) {
+            has[b] = s < mr[b].y;  // words past the reach of the row are not stored (zero)
+            if (has[b]) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint4* q = reinterpret_cast<const uint4*>(D + tword(mr[b].x, s * 8 + 4 * h, NQ));
+                    const uint4 x0 = q[0], x1 = q[1];
+                    seg[b][4 * h] = ((uint64_t)x0.y << 32) | x0.x;
+                    seg[b][4 * h + 1] = ((uint64_t)x0.w << 32) | x0.z;
+                    seg[b][4 * h + 2] = ((uint64_t)x1.y << 32) | x1.x;
+                    seg[b][4 * h + 3] = ((uint64_t)x1.w << 32) | x1.z;
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) seg[b][w] = 0;
             }
-        } else {
-#pragma unroll
-            for (int w = 0; w < 8; ++w) seg[w] = 0;
         }
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint64_t tcol = transpose64_w(seg[w], lane);  // bit i: member j0+i dominates v
-            dec[w] += __popcll(tcol);
-            if (tcol) last[w] = (int32_t)(j0 + 63 - __clzll(tcol));
+        for (int b = 0; b < PEEL_BATCH; ++b) {
+            const int64_t j = jb + (PEEL_BATCH + b) * STEP + lane;
+            mr[b] = j < F ? members[j] : make_int2(0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < PEEL_BATCH; ++b) {
+            const int64_t j0 = jb + b * STEP;
+            if (__ballot(has[b]) == 0) continue;
+            uint32_t lo[8], hi[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                lo[w] = (uint32_t)seg[b][w];
+                hi[w] = (uint32_t)(seg[b][w] >> 32);
+            }
+            tr.run<8>(lo, hi);  // lane v: bit i <-> member j0+i dominates v
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                dec[w] += __popc(lo[w]) + __popc(hi[w]);
+                const int32_t top = hi[w] ? 63 - __clz(hi[w]) : (lo[w] ? 31 - __clz(lo[w]) : -1);
+                if (top >= 0) last[w] = (int32_t)(j0 + top);
+            }
         }
     }
 #pragma unroll
@@ -416,7 +575,6 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
         slast[wave][w * 64 + lane] = last[w];
     }
     __syncthreads();
-    if (threadIdx.x >= 512) return;
     const int t = threadIdx.x;
     int32_t d = 0, l = -1;
 #pragma unroll
@@ -424,11 +582,11 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
         d += sdec[wv][t];
         l = max(l, slast[wv][t]);
     }
-    const int64_t v = s * 512 + t;
+    const int64_t v = s * 512 + t;  // q order
     bool fresh = false;
     if (v < U && d > 0) {
-        const int32_t left = count[v] - d;
-        count[v] = left;
+        const int32_t left = countq[v] - d;
+        countq[v] = left;
         fresh = left == 0;
     }
     const unsigned long long fm = __ballot(fresh);
@@ -439,10 +597,12 @@ __global__ __launch_bounds__(1024) void peel_owned_kernel(const uint64_t* __rest
         base = __shfl(base, first, 64);
         int64_t gs = 0;
         if (fresh) {
-            ckey[base + __popcll(fm & ((1ull << lane) - 1))] =
-                ((uint64_t)(uint32_t)l << 32) | (uint32_t)v;
-            rankU[v] = snf + 1;
-            gs = gsize[v];
+            const int32_t vu = sigma[v];
+            const int32_t slot = base + __popcll(fm & ((1ull << lane) - 1));
+            ckey[slot] = ((uint64_t)(uint32_t)l << 32) | (uint32_t)vu;
+            cq[slot] = (int32_t)v;
+            rankU[vu] = snf + 1;
+            gs = gsize[vu];
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
@@ -512,8 +672,15 @@ __device__ void block_bitonic(uint64_t (&k)[E], uint64_t* lds) {
     }
 }
 
+// member i of a front: (its row in q order, the row segments it reaches)
+__device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const int32_t* nseg) {
+    const int32_t r = pos[u];
+    return make_int2(r, nseg[r / (64 * TD_WPW)]);
+}
+
 template <int E>
-__device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, uint64_t* lds) {
+__device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2* mout,
+                             const int32_t* pos, const int32_t* nseg, uint64_t* lds) {
     uint64_t k[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -524,7 +691,11 @@ __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, uint
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = threadIdx.x * E + e;
-        if (i < n) out[i] = (int32_t)(uint32_t)k[e];
+        if (i < n) {
+            const int32_t u = (int32_t)(uint32_t)k[e];
+            out[i] = u;
+            mout[i] = member_row(u, pos, nseg);
+        }
     }
 }
 
@@ -532,42 +703,137 @@ __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, uint
 // appends them to ulist as the next front and updates the state.
 // presorted: ckey already ordered (the host's radix-sort fallback for fronts
 // larger than ORDER_CAP).
+// Orders the released candidates by (last releasing position l, U index) and
+// appends them to ulist / mrow as the next front.  Counting sort: l < F (the
+// current front's size), so the candidates are binned by l in LDS and ranked
+// inside their bin by U index; a bin of more than ORDER_BIN_MAX candidates
+// (or too many candidates) takes the bitonic sort of the whole key.
+// presorted: ckey already ordered (the host's radix-sort fallback).
+constexpr int ORDER_BIN_MAX = 64;
 __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const uint64_t* ckey,
-                                                           int32_t* ulist, int32_t* fstarts,
+                                                           const int32_t* cq, int32_t* ulist,
+                                                           int2* mrow, const int32_t* pos,
+                                                           const int32_t* nseg, int32_t* fstarts,
                                                            int presorted) {
-    __shared__ uint64_t lds[ORDER_CAP];
-    __shared__ int32_t sn, sgo, snstart;
-    if (threadIdx.x == 0) {
+    __shared__ union {
+        uint64_t keys[ORDER_CAP];
+        struct {
+            int32_t base[ORDER_CAP + 1];
+            int32_t tmp[ORDER_CAP];
+        } cs;
+    } lds;
+    __shared__ int32_t part[1024];
+    __shared__ int32_t sn, sgo, snstart, sF, smax;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
         sgo = !(st->done || (st->overflow && !presorted));
         sn = st->ncand;
         snstart = st->ustart + st->F;
+        sF = st->F;
+        smax = 0;
     }
     __syncthreads();
     if (!sgo) return;
     const int32_t n = sn;
     if (n == 0) {  // nothing released: the reference's `if F2 == 0: break`
-        if (threadIdx.x == 0) st->done = 1;
+        if (tid == 0) st->done = 1;
         return;
     }
     if (!presorted && n > ORDER_CAP) {
-        if (threadIdx.x == 0) st->overflow = 1;
+        if (tid == 0) st->overflow = 1;
         return;
     }
     int32_t* out = ulist + snstart;
+    int2* mout = mrow + snstart;
+    bool sorted_here = false;
     if (presorted) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = (int32_t)(uint32_t)ckey[i];
-    } else if (n <= 1024) {
-        order_sorted<1>(ckey, n, out, lds);
-    } else if (n <= 2048) {
-        order_sorted<2>(ckey, n, out, lds);
-    } else if (n <= 4096) {
-        order_sorted<4>(ckey, n, out, lds);
-    } else if (n <= 8192) {
-        order_sorted<8>(ckey, n, out, lds);
-    } else {
-        order_sorted<16>(ckey, n, out, lds);
+        for (int i = tid; i < n; i += blockDim.x) {
+            const int32_t u = (int32_t)(uint32_t)ckey[i];
+            out[i] = u;
+            mout[i] = member_row(u, pos, nseg);
+        }
+        sorted_here = true;
+    } else if (sF <= ORDER_CAP) {
+        constexpr int E = ORDER_CAP / 1024;
+        const int32_t Fr = sF;
+        for (int i = tid; i <= Fr; i += 1024) lds.cs.base[i] = 0;
+        __syncthreads();
+        uint64_t key[E];
+        int32_t qv[E], slot[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = tid + e * 1024;
+            if (i < n) {
+                key[e] = ckey[i];
+                qv[e] = cq[i];
+                slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
+            }
+        }
+        __syncthreads();
+        // exclusive prefix of the bin counts: thread t owns C consecutive bins
+        const int C = (Fr + 1023) / 1024;
+        const int b0 = tid * C, b1 = min(Fr, b0 + C);
+        int32_t sum = 0, mx = 0;
+        for (int b = b0; b < b1; ++b) {
+            const int32_t c = lds.cs.base[b];
+            sum += c;
+            mx = max(mx, c);
+        }
+        part[tid] = sum;
+        if (mx > ORDER_BIN_MAX) atomicMax(&smax, mx);
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int32_t y = tid >= o ? part[tid - o] : 0;
+            __syncthreads();
+            part[tid] += y;
+            __syncthreads();
+        }
+        int32_t run = part[tid] - sum;
+        for (int b = b0; b < b1; ++b) {
+            const int32_t c = lds.cs.base[b];
+            lds.cs.base[b] = run;
+            run += c;
+        }
+        if (tid == 0) lds.cs.base[Fr] = n;
+        __syncthreads();
+        if (smax == 0) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = tid + e * 1024;
+                if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = tid + e * 1024;
+                if (i < n) {
+                    const int32_t l = (int32_t)(key[e] >> 32), vu = (int32_t)(uint32_t)key[e];
+                    const int32_t beg = lds.cs.base[l], end = lds.cs.base[l + 1];
+                    int32_t r = beg;
+                    for (int32_t j = beg; j < end; ++j) r += lds.cs.tmp[j] < vu ? 1 : 0;
+                    out[r] = vu;
+                    mout[r] = make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]);
+                }
+            }
+            sorted_here = true;
+        }
+        __syncthreads();  // the bitonic fallback reuses the LDS
     }
-    if (threadIdx.x == 0) {
+    if (!sorted_here) {
+        uint64_t* keys = lds.keys;
+        if (n <= 1024) {
+            order_sorted<1>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 2048) {
+            order_sorted<2>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 4096) {
+            order_sorted<4>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 8192) {
+            order_sorted<8>(ckey, n, out, mout, pos, nseg, keys);
+        } else {
+            order_sorted<16>(ckey, n, out, mout, pos, nseg, keys);
+        }
+    }
+    if (tid == 0) {
         const int32_t nstart = snstart, r = st->nfronts;
         const int64_t sorted = st->sorted + st->pending;
         st->sorted = sorted;
@@ -581,6 +847,11 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
         // emo.py:109: continue while pareto_sorted < N (and fronts remain)
         if (sorted >= st->N || nstart + n >= st->U) st->done = 1;
     }
+}
+
+__global__ void member_rows_kernel(const int32_t* ulist, int64_t F, const int32_t* pos,
+                                   const int32_t* nseg, int2* mrow) {
+    DGRID_LOOP(j, F) mrow[j] = member_row(ulist[j], pos, nseg);
 }
 
 __global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, int64_t N, int64_t U,
@@ -602,104 +873,144 @@ __global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, i
 // ---------------------------------------------------------------------------
 // host drivers (called from nsga2.hip)
 // ---------------------------------------------------------------------------
-size_t fast_dom_ranks_bytes(int64_t U) {
-    return 2 * align_up((size_t)U * 8, 256) +
-           3 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U) + scan_temp_bytes(U);
+// Workspace of the fast path: the buffers that live from the ranks to the
+// last front, then the scratch shared by the rank sorts and the peel loop.
+struct FastLayout {
+    int64_t NB, NG, NQ, ngroups, Upad;
+    size_t part, S, sigma, pos, nseg, toff, counter, mrow, countq, cq, work, total;
+};
+static size_t ranks_work_bytes(int64_t n) {
+    return 2 * align_up((size_t)n * 8, 256) + 3 * align_up((size_t)n * 4, 256) +
+           radix_sort_temp_bytes(n) + scan_temp_bytes(n);
 }
-
-// Dense ranks of each objective; `work` holds fast_dom_ranks_bytes(U) bytes.
-int fast_dom_ranks(hipStream_t s, const double* ufit, int m, int64_t U, int4* R4, char* work) {
-    uint64_t* keys = (uint64_t*)work;
-    uint64_t* ktmp = (uint64_t*)(work + align_up((size_t)U * 8, 256));
-    char* p = work + 2 * align_up((size_t)U * 8, 256);
-    int32_t* vals = (int32_t*)p;
-    int32_t* vtmp = (int32_t*)(p + align_up((size_t)U * 4, 256));
-    int32_t* flag = (int32_t*)(p + 2 * align_up((size_t)U * 4, 256));
-    void* rtemp = p + 3 * align_up((size_t)U * 4, 256);
-    void* stemp = (char*)rtemp + radix_sort_temp_bytes(U);
-    DM_HIP(hipMemsetAsync(R4, 0, (size_t)U * 16, s));
-    for (int o = 0; o < m; ++o) {
-        rank_key_kernel<<<dg1(U), 256, 0, s>>>(ufit, m, o, U, keys, vals);
-        int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, U, 0, 64, rtemp);
-        if (rc) return rc;
-        rank_flag_kernel<<<dg1(U), 256, 0, s>>>(keys, U, flag);
-        // the scan may not alias its input: the exclusive prefix goes to vtmp
-        if ((rc = exclusive_scan_i32(s, flag, vtmp, U, nullptr, stemp))) return rc;
-        rank_scatter_kernel<<<dg1(U), 256, 0, s>>>(vals, vtmp, flag, U, o, (int32_t*)R4);
-    }
-    DM_LAUNCH_CHECK();
-    return DM_OK;
+static size_t fronts_work_bytes(int64_t U) {
+    return align_up(sizeof(FrontState), 256) + 2 * align_up((size_t)U * 8, 256) +
+           2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
 }
-
+static FastLayout fast_layout(int64_t n, int64_t U) {
+    FastLayout L;
+    L.NB = (U + 63) / 64;
+    L.NG = (L.NB + 7) / 8;
+    L.NQ = (L.NB + 3) / 4;
+    L.ngroups = (L.NB + TD_WPW - 1) / TD_WPW;
+    L.Upad = L.NB * 64;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(std::max<size_t>(bytes, 1), 256);
+        return o;
+    };
+    L.part = take((size_t)L.ngroups * L.Upad * 2);
+    L.S = take((size_t)L.Upad * 16);
+    L.sigma = take((size_t)U * 4);
+    L.pos = take((size_t)U * 4);
+    L.nseg = take((size_t)(L.ngroups + 1) * 4);
+    L.toff = take((size_t)(L.ngroups + 1) * 4);
+    L.counter = take(4);
+    L.mrow = take((size_t)U * 8);
+    L.countq = take((size_t)U * 4);
+    L.cq = take((size_t)U * 4);
+    L.work = take(std::max(ranks_work_bytes(n), fronts_work_bytes(U)));
+    L.total = off;
+    return L;
+}
+size_t fast_dom_bytes(int64_t n, int64_t U) { return fast_layout(n, U).total; }
 int64_t fast_dom_words(int64_t U) {
     const int64_t NB = (U + 63) / 64, NG = (NB + 7) / 8;
     return NB * 64 * NG * 8;
 }
-size_t fast_dom_partial_bytes(int64_t U) {
-    const int64_t NB = (U + 63) / 64;
-    const int64_t ngroups = (NB + SD_WPW - 1) / SD_WPW;
-    const int64_t nchunks = (NB + SD_CHUNK - 1) / SD_CHUNK;
-    return align_up((size_t)ngroups * U * 2, 256) + align_up((size_t)nchunks * U * 2, 256);
-}
 
-// D (tiled, fast_dom_words(U) words) and count[U] from the ranks.
-int fast_dom_matrix(hipStream_t s, const int4* R4, int m, int64_t U, uint64_t* D, char* partials,
-                    int32_t* count) {
-    const int64_t NB = (U + 63) / 64, NG = (NB + 7) / 8;
-    const int64_t ngroups = (NB + SD_WPW - 1) / SD_WPW;
-    int16_t* crow = (int16_t*)partials;
-    int16_t* ccol = (int16_t*)(partials + align_up((size_t)ngroups * U * 2, 256));
-    const int64_t ntasks = sd_task_count(ngroups);
-    const unsigned blocks = (unsigned)((ntasks + 3) / 4);
+// Ranks (objective 0 from the population's lexicographic order perm, whose
+// group starts segin marks; uidx: U index of each group's representative),
+// the dominance words D (fast_dom_words(U)) and count[U] (U order).
+int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t n,
+                   const int32_t* perm, const int32_t* segin, const int32_t* uidx,
+                   const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws) {
+    const FastLayout L = fast_layout(n, U);
+    int4* S = (int4*)(ws + L.S);
+    int32_t* sigma = (int32_t*)(ws + L.sigma);
+    int32_t* pos = (int32_t*)(ws + L.pos);
+    int32_t* nseg = (int32_t*)(ws + L.nseg);
+    int32_t* toff = (int32_t*)(ws + L.toff);
+    int32_t* counter = (int32_t*)(ws + L.counter);
+    int16_t* part = (int16_t*)(ws + L.part);
+    char* w = ws + L.work;
+    uint64_t* keys = (uint64_t*)w;
+    uint64_t* ktmp = (uint64_t*)(w + align_up((size_t)n * 8, 256));
+    char* p = w + 2 * align_up((size_t)n * 8, 256);
+    int32_t* vals = (int32_t*)p;
+    int32_t* vtmp = (int32_t*)(p + align_up((size_t)n * 4, 256));
+    int32_t* flag = (int32_t*)(p + 2 * align_up((size_t)n * 4, 256));
+    void* rtemp = p + 3 * align_up((size_t)n * 4, 256);
+    void* stemp = (char*)rtemp + radix_sort_temp_bytes(n);
+    DM_HIP(hipMemsetAsync(S, 0, (size_t)L.Upad * 16, s));
+    // objective 0 and the q order from the lexicographic order
+    lex_flags_kernel<<<dg1(n), 256, 0, s>>>(wv, m, perm, segin, n, vals, vtmp);
+    int rc;
+    if ((rc = exclusive_scan_i32(s, vals, flag, n, nullptr, stemp))) return rc;
+    if ((rc = exclusive_scan_i32(s, vtmp, (int32_t*)keys, n, nullptr, stemp))) return rc;
+    lex_sigma_kernel<<<dg1(n), 256, 0, s>>>(perm, uidx, vals, flag, vtmp, (int32_t*)keys, n, m,
+                                            sigma, pos, (int32_t*)S);
+    // objectives 1..m-1: dense ranks by a sort of the unique values
+    for (int o = 1; o < m; ++o) {
+        rank_key_kernel<<<dg1(U), 256, 0, s>>>(ufit, m, o, U, keys, vals);
+        if ((rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, U, 0, 64, rtemp))) return rc;
+        rank_flag_kernel<<<dg1(U), 256, 0, s>>>(keys, U, flag);
+        // the scan may not alias its input: the exclusive prefix goes to vtmp
+        if ((rc = exclusive_scan_i32(s, flag, vtmp, U, nullptr, stemp))) return rc;
+        rank_scatter_kernel<<<dg1(U), 256, 0, s>>>(vals, vtmp, flag, pos, U, o - 1, (int32_t*)S);
+    }
+    tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
+    const unsigned blocks = (unsigned)std::max(1, num_cus) * 8;
     switch (m) {
-        case 2: sym_dom_kernel<2><<<blocks, 256, 0, s>>>(R4, U, NB, NG, ngroups, ntasks, D, crow, ccol); break;
-        case 3: sym_dom_kernel<3><<<blocks, 256, 0, s>>>(R4, U, NB, NG, ngroups, ntasks, D, crow, ccol); break;
-        default: sym_dom_kernel<4><<<blocks, 256, 0, s>>>(R4, U, NB, NG, ngroups, ntasks, D, crow, ccol); break;
+        case 2: tri_dom_kernel<2><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
+        case 3: tri_dom_kernel<3><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
+        default: tri_dom_kernel<4><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
     }
     DM_LAUNCH_CHECK();
-    sym_count_reduce_kernel<<<dg1(U), 256, 0, s>>>(crow, ccol, U, ngroups, count);
+    tri_count_kernel<<<dg1(U), 256, 0, s>>>(part, nseg, sigma, U, L.Upad, L.ngroups, count,
+                                            (int32_t*)(ws + L.countq));
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
 
-size_t fast_fronts_bytes(int64_t U) {
-    return align_up(sizeof(FrontState), 256) + 2 * align_up((size_t)U * 8, 256) +
-           align_up((size_t)U * 8, 256) + 2 * align_up((size_t)U * 4, 256) +
-           radix_sort_temp_bytes(U);
-}
-
 // Fronts 1.. after front 0 (ulist[0, F0), rankU set): peel on the device,
 // checking the status every few fronts.  Fills ufront (front starts in ulist,
-// host) and *sorted (individuals).  `work`: fast_fronts_bytes(U).
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t sorted0, int64_t N,
-                const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
-                int32_t* fstarts, char* work, std::vector<int32_t>& ufront, int64_t* sorted) {
+// host) and *sorted (individuals).  ws: the fast_dom_build workspace.
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0, int64_t sorted0,
+                int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
+                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted) {
     hipStream_t s = ctx->stream;
-    const int64_t NB = (U + 63) / 64, NG = (NB + 7) / 8;
-    char* p = work;
+    const FastLayout L = fast_layout(n, U);
+    const int64_t NG = L.NG;
+    const int32_t* sigma = (const int32_t*)(ws + L.sigma);
+    const int32_t* pos = (const int32_t*)(ws + L.pos);
+    const int32_t* nseg = (const int32_t*)(ws + L.nseg);
+    int2* mrow = (int2*)(ws + L.mrow);
+    int32_t* countq = (int32_t*)(ws + L.countq);
+    int32_t* cq = (int32_t*)(ws + L.cq);
+    char* p = ws + L.work;
     FrontState* st = (FrontState*)p;
     p += align_up(sizeof(FrontState), 256);
     uint64_t* ckey = (uint64_t*)p;
     p += align_up((size_t)U * 8, 256);
     uint64_t* ktmp = (uint64_t*)p;
     p += align_up((size_t)U * 8, 256);
-    uint64_t* kspare = (uint64_t*)p;  // keep the layout of fast_fronts_bytes
-    p += align_up((size_t)U * 8, 256);
     int32_t* vals = (int32_t*)p;
     p += align_up((size_t)U * 4, 256);
     int32_t* vtmp = (int32_t*)p;
     p += align_up((size_t)U * 4, 256);
     void* rtemp = p;
-    (void)kspare;
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
+    member_rows_kernel<<<dg1(F0), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
     FrontState* hst = (FrontState*)pinned(ctx, sizeof(FrontState));
     if (!hst) return DM_ERR_NOMEM;
     int batch = 4;
     for (;;) {
         for (int b = 0; b < batch; ++b) {
-            peel_owned_kernel<<<(unsigned)NG, 1024, 0, s>>>(D, NG, ulist, gsize, st, count, ckey,
-                                                            rankU);
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, ulist, fstarts, 0);
+            peel_owned_kernel<<<(unsigned)NG, 512, 0, s>>>(D, L.NQ, mrow, gsize, sigma, st, countq,
+                                                           ckey, cq, rankU);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
         }
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
@@ -707,11 +1018,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t s
         if (hst->done) break;
         if (hst->overflow) {
             // a front too large for the LDS sort: the radix sort orders its keys
-            const int32_t n = hst->ncand;
-            DM_HIP(hipMemsetAsync(vals, 0, (size_t)n * 4, s));
-            int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, n, 0, 64, rtemp);
+            const int32_t nc = hst->ncand;
+            DM_HIP(hipMemsetAsync(vals, 0, (size_t)nc * 4, s));
+            int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, nc, 0, 64, rtemp);
             if (rc) return rc;
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, ulist, fstarts, 1);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
             DM_LAUNCH_CHECK();
         }
         batch = std::min(batch * 2, 32);

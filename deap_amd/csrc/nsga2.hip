@@ -26,17 +26,16 @@ namespace dm {
 int validate_pop(const dm_pop* p, const char* what);
 int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool desc,
                     int32_t* vals_out);
-// dominance.hip: integer-rank symmetric dominance + device-driven peeling
-size_t fast_dom_ranks_bytes(int64_t U);
-int fast_dom_ranks(hipStream_t s, const double* ufit, int m, int64_t U, int4* R4, char* work);
+// dominance.hip: integer ranks in objective-0 order, lower-triangle dominance,
+// device-driven peel
+size_t fast_dom_bytes(int64_t n, int64_t U);
 int64_t fast_dom_words(int64_t U);
-size_t fast_dom_partial_bytes(int64_t U);
-int fast_dom_matrix(hipStream_t s, const int4* R4, int m, int64_t U, uint64_t* D, char* partials,
-                    int32_t* count);
-size_t fast_fronts_bytes(int64_t U);
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t U, int32_t F0, int64_t sorted0, int64_t N,
-                const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
-                int32_t* fstarts, char* work, std::vector<int32_t>& ufront, int64_t* sorted);
+int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t n,
+                   const int32_t* perm, const int32_t* segin, const int32_t* uidx,
+                   const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0, int64_t sorted0,
+                int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
+                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted);
 
 // ---------------------------------------------------------------------------
 // Workspace bump allocator over the context scratch
@@ -496,12 +495,9 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     uint64_t* D = (uint64_t*)scratch_slot(
         ctx, 1, fast ? (size_t)fast_dom_words(U) * 8 : (size_t)U * W * 8);
     if (!D) return DM_ERR_NOMEM;
-    char* fwork = nullptr;  // fast path: partials | R4 | ranks / fronts work
+    char* fwork = nullptr;  // fast path workspace (dominance.hip)
     if (fast) {
-        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
-        const size_t rb = align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
-        fwork = (char*)scratch_slot(ctx, 4, pb + rb + std::max(fast_dom_ranks_bytes(U),
-                                                               fast_fronts_bytes(U)));
+        fwork = (char*)scratch_slot(ctx, 4, fast_dom_bytes(n, U));
         if (!fwork) return DM_ERR_NOMEM;
     }
 
@@ -510,11 +506,9 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
     unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
     if (fast) {
-        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
-        int4* R4 = (int4*)(fwork + pb);
-        char* rwork = fwork + pb + align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
-        if ((rc = fast_dom_ranks(s, ufit, m, U, R4, rwork))) return rc;
-        if ((rc = fast_dom_matrix(s, R4, m, U, D, fwork, count))) return rc;
+        if ((rc = fast_dom_build(s, ctx->num_cus, wv, m, n, perm, segin, uidx, ufit, U, D, count,
+                                 fwork)))
+            return rc;
     } else if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
         const int64_t ngroups = (W + DB_WPW - 1) / DB_WPW;
         int32_t* cpart = (int32_t*)scratch_slot(ctx, 4, (size_t)ngroups * U * 4);
@@ -551,12 +545,10 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     const int64_t N = std::min<int64_t>(n, k);
     int32_t rnk = 0;
     if (fast && !first_only && sorted_inds < N && F < U && F > 0) {
-        const size_t pb = align_up(fast_dom_partial_bytes(U), 256);
-        char* frwork = fwork + pb + align_up((size_t)((U + 63) / 64) * 64 * 16, 256);
         int64_t total = 0;
         // ufs doubles as the device front-start array
-        if ((rc = fast_fronts(ctx, D, U, (int32_t)F, sorted_inds, N, gsize, ulist, rankU, count,
-                              ufs, frwork, ufront, &total)))
+        if ((rc = fast_fronts(ctx, D, n, U, (int32_t)F, sorted_inds, N, gsize, ulist, rankU, count,
+                              ufs, fwork, ufront, &total)))
             return rc;
         sorted_inds = total;
     }

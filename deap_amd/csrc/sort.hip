@@ -4,106 +4,166 @@
 
 namespace dm {
 
+// One-sweep LSD radix sort (8-bit digits).  Per sort: one memset (global
+// digit histograms + look-back status), one histogram launch for all passes,
+// then ONE launch per pass: each 1,024-key tile ranks its keys stably (wave
+// ballots over the 8 bit-planes of the digit, per-(round, wave) digit counts
+// in LDS), publishes its digit counts and finds the counts of all earlier
+// tiles by decoupled look-back (thread d follows digit d), then scatters.
 constexpr int RS_THREADS = 256;
-constexpr int RS_ITEMS = 16;                      // rounds of 256 elements per tile
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;    // 4096 elements per block
+constexpr int RS_ROUNDS = 4;                       // rounds of 256 keys per tile
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;    // 1,024 keys per tile
 constexpr int RS_BINS = 256;
+constexpr int RS_MAX_PASSES = 8;
+constexpr int RS_HIST_BLOCKS = 512;
 
 size_t radix_sort_temp_bytes(int64_t n) {
-    const int64_t blocks = (n + RS_TILE - 1) / RS_TILE;
-    return align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256) + scan_temp_bytes(blocks * RS_BINS) +
-           align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
+    const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    return align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256) +
+           align_up((size_t)tiles * RS_MAX_PASSES * RS_BINS * 4, 256);
 }
 
-__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* keys, int64_t n,
-                                                             int shift, int32_t* counts,
-                                                             int64_t blocks) {
-    __shared__ int32_t h[RS_BINS];
-    h[threadIdx.x] = 0;
+// ghist[p][d] += count of digit d of pass p (shift begin + 8p)
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* __restrict__ keys,
+                                                             int64_t n, int begin, int passes,
+                                                             int32_t* __restrict__ ghist) {
+    __shared__ int32_t h[RS_MAX_PASSES][RS_BINS];
+    for (int p = 0; p < passes; ++p) h[p][threadIdx.x] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        const int64_t i = base + r * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1);
+    for (int64_t i = (int64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * RS_THREADS) {
+        const uint64_t k = keys[i] >> begin;
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 0xFF], 1);
     }
     __syncthreads();
-    counts[(int64_t)threadIdx.x * blocks + blockIdx.x] = h[threadIdx.x];  // digit-major
+    for (int p = 0; p < passes; ++p) {
+        const int32_t c = h[p][threadIdx.x];
+        if (c) atomicAdd(&ghist[p * RS_BINS + threadIdx.x], c);
+    }
 }
 
-// Stable scatter: ranks inside a round come from wave ballots; rounds are
-// processed in element order, so equal digits keep their input order.
-__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(
-    const uint64_t* keys_in, const int32_t* vals_in, uint64_t* keys_out, int32_t* vals_out,
-    int64_t n, int shift, const int32_t* offsets, int64_t blocks) {
-    __shared__ int32_t base_off[RS_BINS];
-    __shared__ int32_t wave_cnt[RS_THREADS / 64][RS_BINS];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    base_off[tid] = offsets[(int64_t)tid * blocks + blockIdx.x];
-    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+// look-back status word of (tile, digit): flag (1 = tile count, 2 = inclusive
+// prefix) in bits 30-31, the count below
+constexpr uint32_t RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_COUNT = (1u << 30) - 1;
+
+__global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
+    const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
+    uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n, int shift,
+    const int32_t* __restrict__ ghist, uint32_t* status) {
+    __shared__ int32_t cnt[RS_ROUNDS][RS_THREADS / 64][RS_BINS];
+    __shared__ int32_t gofs[RS_BINS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t tile = blockIdx.x;
+    const int64_t base = tile * RS_TILE;
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r)
+#pragma unroll
+        for (int w = 0; w < RS_THREADS / 64; ++w) cnt[r][w][tid] = 0;
+    // exclusive scan of the global digit histogram (thread d -> digit d)
+    gofs[tid] = ghist[tid];
+    __syncthreads();
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        for (int w = 0; w < RS_THREADS / 64; ++w) wave_cnt[w][tid] = 0;
-        __syncthreads();
+    uint64_t k[RS_ROUNDS];
+    int32_t v[RS_ROUNDS];
+    int d[RS_ROUNDS], rk[RS_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
         const int64_t i = base + r * RS_THREADS + tid;
         const bool ok = i < n;
-        uint64_t k = 0;
-        int32_t v = 0;
-        int d = 0;
-        if (ok) {
-            k = keys_in[i];
-            v = vals_in[i];
-            d = (int)((k >> shift) & 0xFF);
-        }
-        // lanes with the same digit: intersect the 8 bit-planes of the digit
+        k[r] = ok ? keys_in[i] : 0;
+        v[r] = ok ? vals_in[i] : 0;
+        d[r] = ok ? (int)((k[r] >> shift) & 0xFF) : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        const bool ok = d[r] >= 0;
         uint64_t same = __ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-            const uint64_t plane = __ballot(ok && ((d >> b) & 1));
-            same &= ((d >> b) & 1) ? plane : ~plane;
+            const uint64_t plane = __ballot(ok && ((d[r] >> b) & 1));
+            same &= ((d[r] >> b) & 1) ? plane : ~plane;
         }
-        const int rank_in_wave = __popcll(same & below);
-        const int cnt_in_wave = __popcll(same);
-        // the lowest lane of each digit group publishes the group count
-        if (ok && rank_in_wave == 0) wave_cnt[wave][d] = cnt_in_wave;
+        rk[r] = __popcll(same & below);
+        if (ok && rk[r] == 0) cnt[r][wave][d[r]] = __popcll(same);
+    }
+    int32_t gex = 0;  // global exclusive offset of digit tid
+    {
+        int32_t x = gofs[tid];
         __syncthreads();
-        if (ok) {
-            int pos = base_off[d] + rank_in_wave;
-            for (int w = 0; w < wave; ++w) pos += wave_cnt[w][d];
-            keys_out[pos] = k;
-            vals_out[pos] = v;
+        // Hillis-Steele inclusive scan over the 256 digits
+        for (int o = 1; o < RS_BINS; o <<= 1) {
+            const int32_t y = tid >= o ? gofs[tid - o] : 0;
+            __syncthreads();
+            gofs[tid] += y;
+            __syncthreads();
         }
-        __syncthreads();
-        // advance the per-digit running offset by this round's total
-        int add = 0;
-        for (int w = 0; w < RS_THREADS / 64; ++w) add += wave_cnt[w][tid];
-        base_off[tid] += add;
-        __syncthreads();
+        gex = gofs[tid] - x;
+    }
+    // tile-local exclusive offsets per (round, wave) in key order; tile total
+    int32_t run = 0;
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r)
+#pragma unroll
+        for (int w = 0; w < RS_THREADS / 64; ++w) {
+            const int32_t c = cnt[r][w][tid];
+            cnt[r][w][tid] = run;
+            run += c;
+        }
+    // decoupled look-back over the earlier tiles for digit tid
+    uint32_t* my = status + tile * RS_BINS + tid;
+    int32_t excl = 0;
+    if (tile == 0) {
+        __hip_atomic_store(my, RS_PREFIX | (uint32_t)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(my, RS_AGG | (uint32_t)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t t = tile - 1; t >= 0;) {
+            const uint32_t st = __hip_atomic_load(status + t * RS_BINS + tid, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (st == 0) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += (int32_t)(st & RS_COUNT);
+            if (st & RS_PREFIX) break;
+            --t;
+        }
+        __hip_atomic_store(my, RS_PREFIX | (uint32_t)(excl + run), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gofs[tid] = gex + excl;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        if (d[r] >= 0) {
+            const int32_t pos = gofs[d[r]] + cnt[r][wave][d[r]] + rk[r];
+            keys_out[pos] = k[r];
+            vals_out[pos] = v[r];
+        }
     }
 }
 
 int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                      int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp) {
-    if (n <= 1) return DM_OK;
-    const int64_t blocks = (n + RS_TILE - 1) / RS_TILE;
-    char* t = (char*)temp;
-    int32_t* counts = (int32_t*)t;
-    t += align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
-    int32_t* offsets = (int32_t*)t;
-    t += align_up((size_t)blocks * RS_BINS * sizeof(int32_t), 256);
-    void* scan_tmp = t;
+    if (n <= 1 || end_bit <= begin_bit) return DM_OK;
+    DM_CHECK_ARG(n < (1ll << 30), "radix sort of more than 2^30 keys");
+    const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    const int passes = std::min(RS_MAX_PASSES, (end_bit - begin_bit + 7) / 8);
+    int32_t* ghist = (int32_t*)temp;
+    uint32_t* status = (uint32_t*)((char*)temp + align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256));
+    DM_HIP(hipMemsetAsync(temp, 0,
+                          align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256) +
+                              (size_t)passes * tiles * RS_BINS * 4,
+                          s));
+    const unsigned hb = (unsigned)std::min<int64_t>(RS_HIST_BLOCKS, (n + RS_THREADS * 8 - 1) / (RS_THREADS * 8));
+    rs_hist_kernel<<<hb, RS_THREADS, 0, s>>>(keys, n, begin_bit, passes, ghist);
     uint64_t* kin = keys;
     int32_t* vin = vals;
     uint64_t* kout = keys_tmp;
     int32_t* vout = vals_tmp;
-    int passes = 0;
-    for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
-        rs_hist_kernel<<<(unsigned)blocks, RS_THREADS, 0, s>>>(kin, n, shift, counts, blocks);
-        int rc = exclusive_scan_i32(s, counts, offsets, blocks * RS_BINS, nullptr, scan_tmp);
-        if (rc) return rc;
-        rs_scatter_kernel<<<(unsigned)blocks, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift,
-                                                                  offsets, blocks);
+    for (int p = 0; p < passes; ++p) {
+        rs_pass_kernel<<<(unsigned)tiles, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n,
+                                                             begin_bit + 8 * p, ghist + p * RS_BINS,
+                                                             status + (size_t)p * tiles * RS_BINS);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

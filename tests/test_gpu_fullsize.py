@@ -17,6 +17,11 @@ pytestmark = pytest.mark.gpu
 N = 1 << 20
 
 
+def _dp():
+    from deap_amd.device import DevicePopulation
+    return DevicePopulation
+
+
 def _rel_close(a, b, tol):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
@@ -98,3 +103,59 @@ def test_benched_kernel_at_full_size(gpu, cfg):
     assert np.array_equal(got_g, g)
     assert _rel_close(got_wv, wv, 0 if gt == "bits" else 1e-12)
     assert (~ok).sum() > 1000  # the sample exercised crossover and mutation
+
+
+def _sphere_fitness(n, m, seed):
+    """DTLZ2-shaped objective vectors: random directions on the positive unit
+    sphere scaled by 1 + g, g >= 0 (the C5 population's fitness layout)."""
+    rng = np.random.default_rng(seed)
+    d = np.abs(rng.normal(size=(n, m)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return d * (1.0 + rng.exponential(0.3, size=(n, 1)))
+
+
+@pytest.mark.parametrize("m", [3, 2])
+def test_sel_nsga2_at_full_size(gpu, monkeypatch, m):
+    """C5 at its benched size (selNSGA2 over 2N = 2^18 DTLZ2-shaped fitnesses
+    -> N = 2^17, deap/tools/emo.py:15-50): the integer-rank lower-triangle
+    dominance + device peel (default) against the fp64 ballot kernel
+    (DM_DOM_BALLOT): the same fronts, chosen indices and crowding distances."""
+    import torch
+    from deap_amd import tools
+    n = 1 << 18
+    wv = -_sphere_fitness(n, m, 100 + m)  # minimisation: weights -1
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(-1.0,) * m, gtype="f64",
+                           wvalues=wv, valid=np.ones(n))
+    got = []
+    for env in (None, "DM_DOM_BALLOT"):
+        monkeypatch.delenv("DM_DOM_BALLOT", raising=False)
+        if env:
+            monkeypatch.setenv(env, "1")
+        fronts = [f.cpu().numpy() for f in tools.sortNondominated(pop, n // 2)]
+        chosen = tools.selNSGA2(pop, n // 2).cpu().numpy()
+        crowd = pop.crowding_dist[:n].cpu().numpy().copy()
+        got.append((fronts, chosen, crowd))
+    (f0, c0, d0), (f1, c1, d1) = got
+    assert len(f0) == len(f1) > 5
+    assert all(np.array_equal(a, b) for a, b in zip(f0, f1))
+    assert np.array_equal(c0, c1)
+    assert np.array_equal(d0[c0], d1[c1])
+    torch.cuda.synchronize()
+
+
+def test_sort_nondominated_objective0_ties(gpu, monkeypatch):
+    """Objective 0 takes 7 values only (most block pairs straddle a tie, the
+    full-compare path), the others are continuous: fast path == LDS kernel."""
+    from deap_amd import tools
+    rng = np.random.default_rng(77)
+    n = 40013
+    wv = np.concatenate([rng.integers(0, 7, size=(n, 1)).astype(np.float64),
+                         rng.uniform(0, 1, size=(n, 2))], 1)
+    wv[rng.integers(0, n, 500)] = wv[rng.integers(0, n, 500)]  # duplicated fitnesses
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0, -1.0, 1.0), gtype="f64",
+                           wvalues=wv, valid=np.ones(n))
+    fast = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
+    monkeypatch.setenv("DM_DOM_LDS", "1")
+    ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
+    assert fast == ref
+    assert sum(len(f) for f in fast) == n
