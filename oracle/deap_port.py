@@ -226,3 +226,301 @@ def run(problem="rastrigin", n=4096, dim=1000, ngen=2, workers=None, seed=1):
     Returns (ind-gen/s, seconds, workers)."""
     _pop, dt, used = evolve(problem, n, dim, ngen, workers, seed)
     return n * ngen / dt, dt, used
+
+
+# ---------------------------------------------------------------------------
+# NSGA-II selection — the C5 CPU baseline (deap/tools/emo.py).  Same data
+# types as the reference (Fitness objects hashed on wvalues, lists of
+# individuals, dict-grouped unique fitnesses) and the same algorithms, so the
+# timing is DEAP's; outputs are pinned by tests/golden/nsga2*.npz.
+# ---------------------------------------------------------------------------
+import bisect  # noqa: E402
+from collections import defaultdict  # noqa: E402
+
+
+class MOFitness(Fitness):
+    """base.Fitness with several objectives: hashed / compared on wvalues
+    (base.py:231,246), ``dominates`` as base.py:209-224."""
+    weights = (-1.0, -1.0, -1.0)
+
+    def __hash__(self):
+        return hash(self.wvalues)
+
+    def __eq__(self, other):
+        return self.wvalues == other.wvalues
+
+    def dominates(self, other, obj=slice(None)):
+        better = False
+        for mine, theirs in zip(self.wvalues[obj], other.wvalues[obj]):
+            if mine > theirs:
+                better = True
+            elif mine < theirs:
+                return False
+        return better
+
+
+class MOInd(list):
+    """An individual of examples/ga/nsga2.py (a sequence with a fitness)."""
+
+    def __init__(self, seq=(), weights=(-1.0, -1.0, -1.0)):
+        super().__init__(seq)
+        self.fitness = MOFitness()
+        self.fitness.weights = weights
+
+
+def sort_nondominated(individuals, k, first_front_only=False):
+    """emo.py:53-117: all-pairs dominance over the unique fitnesses, then the
+    peel of fronts until k individuals are sorted."""
+    if k == 0:
+        return []
+    groups = defaultdict(list)
+    for ind in individuals:
+        groups[ind.fitness].append(ind)
+    fits = list(groups.keys())
+    n_above = defaultdict(int)
+    below = defaultdict(list)
+    front = []
+    for i, a in enumerate(fits):
+        for b in fits[i + 1:]:
+            if a.dominates(b):
+                n_above[b] += 1
+                below[a].append(b)
+            elif b.dominates(a):
+                n_above[a] += 1
+                below[b].append(a)
+        if n_above[a] == 0:
+            front.append(a)
+    fronts = [[]]
+    for f in front:
+        fronts[-1].extend(groups[f])
+    done = len(fronts[-1])
+    if not first_front_only:
+        target = min(len(individuals), k)
+        while done < target:
+            fronts.append([])
+            released = []
+            for p in front:
+                for d in below[p]:
+                    n_above[d] -= 1
+                    if n_above[d] == 0:
+                        released.append(d)
+                        done += len(groups[d])
+                        fronts[-1].extend(groups[d])
+            front = released
+    return fronts
+
+
+def assign_crowding_dist(individuals):
+    """emo.py:119-143."""
+    if len(individuals) == 0:
+        return
+    dist = [0.0] * len(individuals)
+    crowd = [(ind.fitness.values, i) for i, ind in enumerate(individuals)]
+    nobj = len(individuals[0].fitness.values)
+    for o in range(nobj):
+        crowd.sort(key=lambda e: e[0][o])
+        dist[crowd[0][1]] = float("inf")
+        dist[crowd[-1][1]] = float("inf")
+        if crowd[-1][0][o] == crowd[0][0][o]:
+            continue
+        norm = nobj * float(crowd[-1][0][o] - crowd[0][0][o])
+        for lo, mid, hi in zip(crowd[:-2], crowd[1:-1], crowd[2:]):
+            dist[mid[1]] += (hi[0][o] - lo[0][o]) / norm
+    for i, d in enumerate(dist):
+        individuals[i].fitness.crowding_dist = d
+
+
+def sel_nsga2(individuals, k, nd="standard"):
+    """emo.py:15-50."""
+    if nd == "standard":
+        fronts = sort_nondominated(individuals, k)
+    elif nd == "log":
+        fronts = sort_log_nondominated(individuals, k)
+    else:
+        raise Exception("selNSGA2: The choice of non-dominated sorting method %r is invalid." % nd)
+    for f in fronts:
+        assign_crowding_dist(f)
+    chosen = [ind for f in fronts[:-1] for ind in f]
+    rest = k - len(chosen)
+    if rest > 0:
+        last = sorted(fronts[-1], key=lambda ind: ind.fitness.crowding_dist, reverse=True)
+        chosen.extend(last[:rest])
+    return chosen
+
+
+# Fortin et al. (2013), generalised reduced run-time non-dominated sort, as
+# emo.py:201-455 implements it: fitnesses in descending lexicographic order,
+# recursive median splits on the last objective, sweeps on the first two.
+def _dominated_by(w1, w2):
+    """emo.py:206-220: w2 dominates w1."""
+    strict = False
+    for a, b in zip(w1, w2):
+        if a > b:
+            return False
+        if a < b:
+            strict = True
+    return strict
+
+
+def _median(seq, obj):
+    """emo.py:222-232 (mean of the two middle values for even lengths)."""
+    vals = sorted(s[obj] for s in seq)
+    n = len(vals)
+    return vals[(n - 1) // 2] if n % 2 else (vals[(n - 1) // 2] + vals[n // 2]) / 2.0
+
+
+def _halves(items, obj, med):
+    """Two ways of splitting at the median (ties with the upper or the lower
+    part), emo.py:299-325 / 375-412."""
+    up_a, low_a, up_b, low_b = [], [], [], []
+    for f in items:
+        v = f[obj]
+        if v > med:
+            up_a.append(f)
+            up_b.append(f)
+        elif v < med:
+            low_a.append(f)
+            low_b.append(f)
+        else:
+            up_a.append(f)
+            low_b.append(f)
+    return up_a, low_a, up_b, low_b
+
+
+def _stair_max(fstairs, idx, rank):
+    return max(fstairs[:idx], key=rank.__getitem__)
+
+
+def _nd_a(fits, obj, rank):
+    """sortNDHelperA (emo.py:278-297)."""
+    if len(fits) < 2:
+        return
+    if len(fits) == 2:
+        if _dominated_by(fits[1][:obj + 1], fits[0][:obj + 1]):
+            rank[fits[1]] = max(rank[fits[1]], rank[fits[0]] + 1)
+    elif obj == 1:
+        _sweep_a(fits, rank)
+    elif len(frozenset(f[obj] for f in fits)) == 1:
+        _nd_a(fits, obj - 1, rank)
+    else:
+        up_a, low_a, up_b, low_b = _halves(fits, obj, _median(fits, obj))
+        if abs(len(up_a) - len(low_a)) <= abs(len(up_b) - len(low_b)):
+            best, worst = up_a, low_a
+        else:
+            best, worst = up_b, low_b
+        _nd_a(best, obj, rank)
+        _nd_b(best, worst, obj - 1, rank)
+        _nd_a(worst, obj, rank)
+
+
+def _sweep_a(fits, rank):
+    """sweepA (emo.py:327-344)."""
+    stairs = [-fits[0][1]]
+    fstairs = [fits[0]]
+    for f in fits[1:]:
+        idx = bisect.bisect_right(stairs, -f[1])
+        if 0 < idx <= len(stairs):
+            rank[f] = max(rank[f], rank[_stair_max(fstairs, idx, rank)] + 1)
+        for i in range(idx, len(fstairs)):
+            if rank[fstairs[i]] == rank[f]:
+                del stairs[i]
+                del fstairs[i]
+                break
+        stairs.insert(idx, -f[1])
+        fstairs.insert(idx, f)
+
+
+def _nd_b(best, worst, obj, rank):
+    """sortNDHelperB (emo.py:346-373)."""
+    if not best or not worst:
+        return
+    if len(best) == 1 or len(worst) == 1:
+        for h in worst:
+            hs = h[:obj + 1]
+            for b in best:
+                bs = b[:obj + 1]
+                if _dominated_by(hs, bs) or hs == bs:
+                    rank[h] = max(rank[h], rank[b] + 1)
+    elif obj == 1:
+        _sweep_b(best, worst, rank)
+    elif min(b[obj] for b in best) >= max(h[obj] for h in worst):
+        _nd_b(best, worst, obj - 1, rank)
+    elif max(b[obj] for b in best) >= min(h[obj] for h in worst):
+        med = _median(best if len(best) > len(worst) else worst, obj)
+        b1a, b2a, b1b, b2b = _halves(best, obj, med)
+        w1a, w2a, w1b, w2b = _halves(worst, obj, med)
+        if (abs(len(b1a) - len(b2a) + len(w1a) - len(w2a))
+                <= abs(len(b1b) - len(b2b) + len(w1b) - len(w2b))):
+            b1, b2, w1, w2 = b1a, b2a, w1a, w2a
+        else:
+            b1, b2, w1, w2 = b1b, b2b, w1b, w2b
+        _nd_b(b1, w1, obj, rank)
+        _nd_b(b1, w2, obj - 1, rank)
+        _nd_b(b2, w2, obj, rank)
+
+
+def _sweep_b(best, worst, rank):
+    """sweepB (emo.py:414-443)."""
+    stairs, fstairs = [], []
+    it = iter(best)
+    nb = next(it, False)
+    for h in worst:
+        while nb and h[:2] <= nb[:2]:
+            keep = True
+            for i, fs in enumerate(fstairs):
+                if rank[fs] == rank[nb]:
+                    if fs[1] > nb[1]:
+                        keep = False
+                    else:
+                        del stairs[i], fstairs[i]
+                    break
+            if keep:
+                idx = bisect.bisect_right(stairs, -nb[1])
+                stairs.insert(idx, -nb[1])
+                fstairs.insert(idx, nb)
+            nb = next(it, False)
+        idx = bisect.bisect_right(stairs, -h[1])
+        if 0 < idx <= len(stairs):
+            rank[h] = max(rank[h], rank[_stair_max(fstairs, idx, rank)] + 1)
+
+
+def sort_log_nondominated(individuals, k, first_front_only=False):
+    """emo.py:234-276."""
+    if k == 0:
+        return []
+    groups = defaultdict(list)
+    for ind in individuals:
+        groups[ind.fitness.wvalues].append(ind)
+    fits = list(groups.keys())
+    rank = dict.fromkeys(fits, 0)
+    fits.sort(reverse=True)
+    _nd_a(fits, len(individuals[0].fitness.wvalues) - 1, rank)
+    fronts = [[] for _ in range(max(rank.values()) + 1)]
+    for f in fits:
+        fronts[rank[f]].extend(groups[f])
+    if first_front_only:
+        return fronts[0]
+    total = 0
+    for i, f in enumerate(fronts):
+        total += len(f)
+        if total >= k:
+            return fronts[:i + 1]
+    return fronts
+
+
+def nsga2_population(wvalues, weights):
+    """Individuals of examples/ga/nsga2.py carrying the given wvalues."""
+    pop = []
+    for row in wvalues:
+        ind = MOInd([0.0], weights)
+        ind.fitness.wvalues = tuple(float(x) for x in row)
+        pop.append(ind)
+    return pop
+
+
+def time_sel_nsga2(wvalues, weights, k, nd="standard"):
+    """Seconds of one sel_nsga2 call on host individuals."""
+    pop = nsga2_population(wvalues, weights)
+    t0 = time.perf_counter()
+    sel_nsga2(pop, k, nd)
+    return time.perf_counter() - t0

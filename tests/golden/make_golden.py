@@ -909,6 +909,54 @@ def gen_support(D, rng):
     return out
 
 
+def sphere_fitness(n, m, seed):
+    """DTLZ2-shaped objective vectors (directions on the positive unit sphere
+    scaled by 1 + g): the shape of the C5 population's fitnesses."""
+    rng = np.random.default_rng(seed)
+    d = np.abs(rng.normal(size=(n, m)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return d * (1.0 + rng.exponential(0.3, size=(n, 1)))
+
+
+def gen_port_nsga2(D):
+    """Calibration of the C5 CPU baseline (oracle/deap_port.py sel_nsga2 with
+    nd='standard' / 'log'): reference selNSGA2 vs port wall time on the same
+    DTLZ2-shaped minimisation fitnesses in this container (+-20 %), and the
+    chosen individuals (identical)."""
+    import json
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import deap_port
+    tools = D["deap.tools"]
+    weights = (-1.0, -1.0, -1.0)
+    Ind = make_types(D, "d", weights)
+    cal = {"note": "seconds of one selNSGA2(2N -> N) on DTLZ2-shaped fitnesses, this build "
+                   "container, median of 3 (reference = 2to3 copy of /root/reference/deap; "
+                   "port = oracle/deap_port.time_sel_nsga2)", "cpu_count": os.cpu_count(),
+           "cases": []}
+    for nd, n in (("standard", 1024), ("standard", 2048), ("log", 16384), ("log", 65536)):
+        wv = -sphere_fitness(n, 3, 5)
+        ref_t, port_t = [], []
+        for _ in range(3):
+            pop = to_inds(Ind, np.zeros((n, 1)), wv)
+            t0 = time.perf_counter()
+            chosen = tools.selNSGA2(pop, n // 2, nd=nd)
+            ref_t.append(time.perf_counter() - t0)
+            port_t.append(deap_port.time_sel_nsga2(wv, weights, n // 2, nd))
+        ident = {id(ind): i for i, ind in enumerate(pop)}
+        ref_idx = [ident[id(c)] for c in chosen]
+        ppop = deap_port.nsga2_population(wv, weights)
+        pident = {id(ind): i for i, ind in enumerate(ppop)}
+        port_idx = [pident[id(c)] for c in deap_port.sel_nsga2(ppop, n // 2, nd)]
+        r, p = sorted(ref_t)[1], sorted(port_t)[1]
+        cal["cases"].append({"nd": nd, "n": n, "objectives": 3, "reference_s": round(r, 4),
+                             "port_s": round(p, 4), "port_over_reference": round(p / r, 4),
+                             "same_choice": ref_idx == port_idx})
+        print(cal["cases"][-1])
+    with open(os.path.join(HERE, "port_nsga2_calibration.json"), "w") as f:
+        json.dump(cal, f, indent=1)
+
+
 def main():
     D = load_reference()
     if sys.argv[1:] == ["log"]:
@@ -925,6 +973,9 @@ def main():
         np.savez_compressed(os.path.join(HERE, "support.npz"),
                             **gen_support(D, np.random.default_rng(17)))
         np.savez_compressed(os.path.join(HERE, "port.npz"), **gen_port(D))
+        return
+    if sys.argv[1:] == ["port_nsga2"]:
+        gen_port_nsga2(D)
         return
     if sys.argv[1:] == ["dcd"]:  # regenerate one fixture without touching the rest
         np.savez_compressed(os.path.join(HERE, "dcd.npz"),

@@ -123,3 +123,47 @@ def test_hall_of_fame_host_matches_reference(case):
         hof.update(pop)
         assert [list(h) for h in hof] == d["hof%d_hof_genes%d" % (j, gen)].tolist()
         assert [list(h.fitness.wvalues) for h in hof] == d["hof%d_hof_wv%d" % (j, gen)].tolist()
+
+
+def _port_fronts(wv, weights, k, nd):
+    from oracle import deap_port
+    pop = deap_port.nsga2_population(wv, weights)
+    ident = {id(ind): i for i, ind in enumerate(pop)}
+    fronts = (deap_port.sort_log_nondominated(pop, k) if nd == "log"
+              else deap_port.sort_nondominated(pop, k))
+    pop2 = deap_port.nsga2_population(wv, weights)
+    ident2 = {id(ind): i for i, ind in enumerate(pop2)}
+    chosen = [ident2[id(c)] for c in deap_port.sel_nsga2(pop2, k, nd)]
+    return [[ident[id(x)] for x in f] for f in fronts], chosen
+
+
+def test_deap_port_nsga2_reproduces_reference():
+    """The C5 CPU baseline (oracle/deap_port.py sel_nsga2 with nd='standard'
+    and 'log', emo.py:15-143,234-455 on reference-typed individuals) gives the
+    reference's fronts and chosen individuals on the golden cases."""
+    d = golden("nsga2.npz")
+    for j in range(6):
+        key = "nd%d_" % j
+        wv, k = d[key + "wv"], int(d[key + "k"])
+        fronts, chosen = _port_fronts(wv, tuple(d[key + "weights"]), k, "standard")
+        assert [i for f in fronts for i in f] == d[key + "order"].tolist(), j
+        assert chosen == d[key + "chosen"].tolist(), j
+    d = golden("nsga2log.npz")
+    for j in range(6):
+        key = "log%d_" % j
+        wv, k = d[key + "wv"], int(d[key + "k"])
+        fronts, chosen = _port_fronts(wv, tuple([-1.0, 1.0, -1.0, 1.0][:wv.shape[1]]), k, "log")
+        assert [len(f) for f in fronts] == d[key + "sizes"].tolist(), j
+        assert [i for f in fronts for i in f] == d[key + "order"].tolist(), j
+        assert chosen == d[key + "chosen"].tolist(), j
+
+
+def test_deap_port_nsga2_speed_calibrated_against_reference():
+    """Port vs reference selNSGA2 wall time, measured in the build container
+    by tests/golden/make_golden.py port_nsga2: within +-20 %, same choice."""
+    with open(os.path.join(GOLDEN, "port_nsga2_calibration.json")) as f:
+        cal = json.load(f)
+    assert {c["nd"] for c in cal["cases"]} == {"standard", "log"}
+    for c in cal["cases"]:
+        assert 0.8 <= c["port_over_reference"] <= 1.2, c
+        assert c["same_choice"], c
