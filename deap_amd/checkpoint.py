@@ -150,4 +150,45 @@ def load(path, device=None, individual_class=None, capacity=None):
     return out
 
 
-__all__ = ["save", "load", "read_header", "header"]
+def export_reference_dict(population, generation=None, halloffame=None, logbook=None,
+                          stream=None, individual_class=None):
+    """The checkpoint dict of the reference's tutorial
+    (doc/tutorials/advanced/checkpoint.rst:21-65):
+    ``dict(population=..., generation=..., halloffame=..., logbook=...,
+    rndstate=...)`` with the population materialised as host individuals
+    (``individual_class`` — e.g. a DEAP ``creator.Individual`` — or plain
+    lists carrying a ``fitness``; ``fitness.wvalues`` set for valid rows), the
+    hall of fame and logbook as given, and ``rndstate`` = the counter-based
+    stream state ``(seed, island, counter)`` (the device does not draw from
+    Python's ``random``; the tuple resumes the same stream through
+    :func:`import_reference_dict`).  A user who pickles it, as the tutorial
+    does, gets a file that their DEAP code can read."""
+    return {"population": population.to_individuals(individual_class),
+            "generation": generation, "halloffame": halloffame, "logbook": logbook,
+            "rndstate": tuple(stream.getstate()) if stream is not None else None}
+
+
+def import_reference_dict(cp, weights=None, gtype=None, device=None, capacity=None):
+    """Rebuild a device population from a reference-shaped checkpoint dict
+    (``population``: individuals with ``fitness.wvalues`` — valid iff non-empty
+    — as DEAP pickles them, or as :func:`export_reference_dict` produced them).
+    ``weights`` default to the first individual's ``fitness.weights``; genome
+    type by ``gtype`` or inferred (DevicePopulation.from_individuals).
+    Returns a dict with ``population`` (DevicePopulation), ``generation``,
+    ``halloffame``, ``logbook`` and ``stream`` (a RandomStream when ``rndstate``
+    is a ``(seed, island, counter)`` tuple, else None)."""
+    from .device import DevicePopulation
+    from .ops import RandomStream
+    pop = DevicePopulation.from_individuals(list(cp["population"]), weights, gtype, device,
+                                            capacity)
+    stream = None
+    rs = cp.get("rndstate")
+    if isinstance(rs, (tuple, list)) and len(rs) == 3 and all(isinstance(x, int) for x in rs):
+        stream = RandomStream()
+        stream.setstate(tuple(rs))
+    return {"population": pop, "generation": cp.get("generation"),
+            "halloffame": cp.get("halloffame"), "logbook": cp.get("logbook"), "stream": stream}
+
+
+__all__ = ["save", "load", "read_header", "header", "export_reference_dict",
+           "import_reference_dict"]

@@ -310,12 +310,32 @@ class _HostIndividual(list):
 
 
 def _make_fitness(weights):
+    return HostFitness(weights)
+
+
+def _host_fitness_class():
     from .base import Fitness
 
-    class _Fit(Fitness):
-        pass
-    _Fit.weights = tuple(weights)
-    return _Fit()
+    class HostFitness(Fitness):
+        """Fitness of materialised host individuals: the weights live on the
+        instance, so the individuals pickle (the reference's checkpoint
+        pattern, doc/tutorials/advanced/checkpoint.rst:21-65)."""
+
+        def __init__(self, weights=(1.0,), values=()):
+            self.weights = tuple(weights)
+            super().__init__(values)
+
+        def __deepcopy__(self, memo):
+            c = HostFitness(self.weights)
+            c.wvalues = self.wvalues
+            return c
+
+    HostFitness.__module__ = __name__
+    HostFitness.__qualname__ = "HostFitness"
+    return HostFitness
+
+
+HostFitness = _host_fitness_class()
 
 
 def pack_bits(bits):

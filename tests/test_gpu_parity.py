@@ -586,6 +586,45 @@ def test_checkpoint_resume_is_bit_exact(gpu, tmp_path):
     assert log.select("nevals")[3:] == log3.select("nevals")[1:]
 
 
+def test_checkpoint_reference_dict_round_trip(gpu):
+    """export_reference_dict writes the tutorial's checkpoint dict
+    (doc/tutorials/advanced/checkpoint.rst:21-65: population, generation,
+    halloffame, logbook, rndstate) with materialised individuals; pickled and
+    reloaded (as the tutorial does), import_reference_dict rebuilds the device
+    population bit for bit and the resumed run equals the uninterrupted one."""
+    import pickle
+    from deap_amd import algorithms, checkpoint, tools
+    from deap_amd.ops import RandomStream
+
+    def start():
+        stream = RandomStream(7, island=1)
+        pop = tools.initPopulation(n=513, dim=64, low=-5.12, high=5.12, gtype="f64",
+                                   weights=(-1.0,), stream=stream)
+        return pop, stream
+
+    tb = _toolbox("blend", "gaussian", 0.05, 0.5, evaluate="rastrigin")
+    pop, stream = start()
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 4, verbose=False, stream=stream)
+    full = pop.to_numpy()
+    pop2, stream2 = start()
+    hof = tools.HallOfFame(5)
+    pop2, log2 = algorithms.eaSimple(pop2, tb, 0.5, 0.2, 2, halloffame=hof, verbose=False,
+                                     stream=stream2)
+    before = pop2.to_numpy()
+    cp = checkpoint.export_reference_dict(pop2, 2, hof, log2, stream2)
+    assert set(cp) == {"population", "generation", "halloffame", "logbook", "rndstate"}
+    assert len(cp["population"]) == 513 and all(i.fitness.valid for i in cp["population"])
+    cp = pickle.loads(pickle.dumps(cp))
+    back = checkpoint.import_reference_dict(cp, device=pop2.device)
+    for a, b in zip(before, back["population"].to_numpy()):
+        assert np.array_equal(a, b)
+    assert back["generation"] == 2 and len(back["halloffame"]) == 5
+    pop3, _ = algorithms.eaSimple(back["population"], tb, 0.5, 0.2, 2, verbose=False,
+                                  stream=back["stream"])
+    for a, b in zip(full, pop3.to_numpy()):
+        assert np.array_equal(a, b)
+
+
 def _dcd_pop(wv, crowd):
     import torch
     n = len(wv)
