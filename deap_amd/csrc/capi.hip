@@ -430,6 +430,14 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
         delete c;
         return DM_ERR_HIP;
     }
+    const size_t spread = sizeof(long long) * kEvalSpread * kEvalSpreadStride;
+    if (hipMalloc(&c->evals_spread, spread) != hipSuccess ||
+        hipMemset(c->evals_spread, 0, spread) != hipSuccess) {
+        set_error("counter allocation failed");
+        (void)hipFree(c->zig);
+        delete c;
+        return DM_ERR_HIP;
+    }
     *out = c;
     return DM_OK;
 }
@@ -441,6 +449,7 @@ int dm_ctx_destroy(dm_ctx* ctx) {
         if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->zig) (void)hipFree(ctx->zig);
+    if (ctx->evals_spread) (void)hipFree(ctx->evals_spread);
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     delete ctx;
     return DM_OK;

@@ -42,6 +42,7 @@ void set_error(const char* fmt, ...);
 }  // namespace dm
 
 // Opaque context: one device, one stream, grow-only scratch arena.
+constexpr int kEvalSpread = 64, kEvalSpreadStride = 16;  // counters, int64 stride
 struct dm_ctx {
     static constexpr int kSlots = 5;
     int device = 0;
@@ -52,6 +53,10 @@ struct dm_ctx {
     size_t pinned_bytes = 0;
     int num_cus = 256;
     double* zig = nullptr;  // ziggurat tables (device), see zig_normal
+    // 64 nevals partial counters, 128 B apart (kEvalSpread), zero between
+    // uses: the packed-bit hot kernel adds per-workgroup counts, a one-wave
+    // kernel moves their sum into nevals and re-zeroes them
+    long long* evals_spread = nullptr;
     // Hot-kernel timing (dm_ctx_set_timing): HIP event pairs recorded on the
     // launch stream around each generation kernel, for bench.py's roofline.
     std::vector<hipEvent_t> tev;

@@ -119,8 +119,15 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         const int nch = parents->dim <= 512 ? 2 : 4;
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
         if (!plans) return DM_ERR_NOMEM;
-        launch_pair_plans(a, plans, nullptr, ctx->stream);
+        // nevals is counted by the plan kernel (spread counters + fold): one
+        // same-address atomic per hot-kernel wave serialised 65,536 atomics
+        const bool count = ec != EC_NONE && a.nevals;
+        launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
+        if (count) {
+            launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
+            DM_LAUNCH_CHECK();
+        }
         PipeArgs q{};
         q.pgenes = a.pgenes;
         q.cgenes = a.cgenes;
@@ -131,7 +138,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.mu_vec = a.mu_vec;
         q.sigma_vec = a.sigma_vec;
         q.zig = a.zig;
-        q.nevals = a.nevals;
+        q.nevals = nullptr;
         q.nc = a.nc;
         q.pstride = a.pstride;
         q.cstride = a.cstride;
@@ -153,15 +160,36 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
-    // packed-bit hot path (C2): same plan kernel (which also counts nevals) + a
-    // one-shot burst kernel (generation_pipe_bits.hip)
+    // packed-bit hot path (C2): one fused burst kernel for tournaments of at most
+    // 8 aspirants (decisions drawn in-kernel), else the plan kernel (which also
+    // counts nevals) + the burst kernel (generation_pipe_bits.hip)
     if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 64 &&
         parents->nobj == 1 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
         !std::getenv("DM_DISABLE_PIPE")) {
+        if ((sel == DM_SEL_RANDOM || tournsize <= 8) && !std::getenv("DM_BITS_PLAN")) {
+            // one launch: decisions drawn inside the burst kernel (+ the
+            // nevals reduction of its per-workgroup partials)
+            const bool count = ec != EC_NONE && a.nevals && !std::getenv("DM_BITS_NOCOUNT");
+            timing_begin(ctx);
+            launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
+                                  ctx->stream);
+            timing_end(ctx);
+            DM_LAUNCH_CHECK();
+            if (count) {
+                launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
+                DM_LAUNCH_CHECK();
+            }
+            return DM_OK;
+        }
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
         if (!plans) return DM_ERR_NOMEM;
-        launch_pair_plans(a, plans, ec != EC_NONE ? a.nevals : nullptr, ctx->stream);
+        const bool count = ec != EC_NONE && a.nevals;
+        launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
+        if (count) {
+            launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
+            DM_LAUNCH_CHECK();
+        }
         timing_begin(ctx);
         launch_gen_bits_pipe(a, plans, ec != EC_NONE, ctx->num_cus, ctx->stream);
         timing_end(ctx);

@@ -101,6 +101,252 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
     }
 }
 
+// ---------------------------------------------------------------------------
+// Single-launch form (the C2 hot path): the per-pair decisions are drawn
+// inside the burst kernel, so the plan kernel, its 32-B plans and its
+// separate pass over the parents' fitness disappear.  A wave owns DM_BITS_PP
+// = 4 pairs = 8 children; for the selection phase lane L takes child L & 7
+// and Philox call L >> 3 (its two aspirants), lanes 32-39 the crossover
+// calls of the 4 pairs and lanes 40-47 the mutation flags of the 8 children,
+// so ONE Philox evaluation per lane draws every decision of the wave (t <=
+// 8); each aspirant's fitness and validity come from one vector load, the
+// tournament (first-drawn wins, a later aspirant replaces only on
+// Fitness.__gt__ = not(a <= b), selection.py:68) runs over lane shuffles.  The
+// winners reach the row loads through readlane (scalar row addresses), the
+// clone's inherited fitness stays in the child's lane, and each wave stores
+// its 8 fitness values and 8 validity bytes as one contiguous store each.
+// `nevals`: per-workgroup partials (ballot + LDS), summed by a second launch.
+// Same Philox counters as pair_plan_kernel / gen_bits_kernel: bit-identical
+// children (tests/test_gpu_parity.py::test_native_hot_kernel_equals_replay_kernel).
+// ---------------------------------------------------------------------------
+template <int CX, int MUT, bool EVAL, bool TOURN>
+__global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long long* spread) {
+    constexpr int PP = DM_BITS_PP;
+    constexpr int NCH = 2 * PP;  // children per wave
+    static_assert(NCH == 8, "lane layout assumes 8 children per wave");
+    const int lane = threadIdx.x & 63;
+    const int64_t npairs = (a.nc + 1) / 2;
+    const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PP;
+    const int64_t cbase = 2 * p0;
+    const uint32_t np = (uint32_t)a.np;
+
+    // ---- decisions: ONE Philox call per lane covers every draw of the wave
+    //   lanes  0-31: selection, child L & 7, call L >> 3 (aspirants 2call, 2call+1)
+    //   lanes 32-39: crossover of pair (L - 32) & 3, call (L - 32) >> 2
+    //   lanes 40-47: mutation flag of child L - 40
+    const int t = TOURN ? a.tournsize : 1;
+    const int S = (t + 1) >> 1;  // selection calls per child (t <= 8)
+    uint32_t stage = ST_SEL, item = 0, sub = 0;
+    bool draw = false;
+    if (lane < 32) {
+        item = (uint32_t)(cbase + (lane & 7));
+        sub = (uint32_t)(lane >> 3);
+        draw = (int)sub < S && cbase + (lane & 7) < a.nc;
+    } else if (lane < 40) {
+        const int64_t pp = p0 + ((lane - 32) & 3);
+        stage = ST_CX;
+        item = (uint32_t)pp;
+        sub = (uint32_t)((lane - 32) >> 2);
+        draw = CX != DM_CX_NONE && 2 * pp + 1 < a.nc;
+    } else if (lane < 48) {
+        stage = ST_MUT;
+        item = (uint32_t)(cbase + lane - 40);
+        draw = MUT != DM_MUT_NONE && cbase + lane - 40 < a.nc;
+    }
+    u32x4 w{};
+    if (draw) w = a.rng(stage, item, sub);
+    // selection lanes: both aspirants of the call, fitness and validity
+    int32_t k0 = 0, k1 = 0;
+    double f0 = 0.0, f1 = 0.0;
+    uint32_t v0 = 0, v1 = 0;
+    if (draw && lane < 32) {
+        k0 = (int32_t)bounded64(w.x, w.y, np);
+        f0 = a.pwv[k0];
+        v0 = a.pvalid[k0];
+        if (2 * (int)sub + 1 < t) {
+            k1 = (int32_t)bounded64(w.z, w.w, np);
+            f1 = a.pwv[k1];
+            v1 = a.pvalid[k1];
+        }
+    }
+    // tournament of child L (lanes 0-7): first-drawn wins, a later aspirant
+    // replaces only on Fitness.__gt__ (one objective: not(a <= b))
+    int32_t k = k0;
+    double f = f0;
+    uint32_t v = v0;
+    if (TOURN) {
+        for (int jj = 1; jj < t; ++jj) {
+            const int src = (jj >> 1) * 8 + (lane & 7);
+            const double fj = __shfl((jj & 1) ? f1 : f0, src, 64);
+            const int32_t kj = __shfl((jj & 1) ? k1 : k0, src, 64);
+            const uint32_t vj = __shfl((jj & 1) ? v1 : v0, src, 64);
+            if (!(fj <= f)) {
+                f = fj;
+                k = kj;
+                v = vj;
+            }
+        }
+    }
+    // crossover lanes 32-35: flag and cxTwoPoint cuts of pair L - 32
+    // (call 1's words come from lane L + 4)
+    const uint32_t w2x = (uint32_t)__shfl((int)w.x, (lane + 4) & 63, 64);
+    const uint32_t w2y = (uint32_t)__shfl((int)w.y, (lane + 4) & 63, 64);
+    uint32_t cxf_l = 0, cuts = 0;
+    if (draw && lane >= 32 && lane < 36 && (uint64_t)w.x < a.thr_cx) {
+        cxf_l = 1;
+        if (CX == DM_CX_TWOPOINT) {
+            int32_t r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
+            int32_t r2 = 1 + (int32_t)bounded64(w2x, w2y, (uint32_t)(a.dim - 1));
+            if (r2 >= r1) {
+                r2 += 1;
+            } else {
+                const int32_t tt = r1;
+                r1 = r2;
+                r2 = tt;
+            }
+            cuts = (uint32_t)r1 | ((uint32_t)r2 << 16);
+        }
+    }
+    const bool mut_l = draw && lane >= 40 && lane < 48 && (uint64_t)w.x < a.thr_mut;
+    // per child (lanes 0-7): its pair's crossover flag, its mutation flag
+    const int ch = lane & 7;
+    const int64_t c = cbase + ch;
+    const bool live = lane < NCH && c < a.nc;
+    const bool cx_c = __shfl((int)cxf_l, 32 + (ch >> 1), 64) != 0;
+    const bool mut = live && __shfl((int)mut_l, 40 + ch, 64) != 0;
+    const bool inv = live && (cx_c || mut || !v);
+    const uint64_t mut_bits = __ballot(mut);
+    const uint64_t inv_bits = __ballot(inv);
+
+    // ---- rows: every parent row of the wave's pairs in flight first
+    const int words = a.words64;
+    const bool lw = lane < words;
+    auto row = [&](int32_t s) {
+        return reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)s * a.pstride);
+    };
+    int32_t s0[PP], s1[PP];
+    uint32_t cut[PP], cxf[PP];
+    uint64_t y0[PP], y1[PP];
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+        s0[q] = __builtin_amdgcn_readlane(k, 2 * q);
+        s1[q] = __builtin_amdgcn_readlane(k, 2 * q + 1);
+        cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)cuts, 32 + q);
+        cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)cxf_l, 32 + q);
+        y0[q] = 0;
+        y1[q] = 0;
+        if (lw && p0 + q < npairs) {
+            y0[q] = row(s0[q])[lane];
+            if (2 * (p0 + q) + 1 < a.nc) y1[q] = row(s1[q])[lane];
+        }
+    }
+    uint32_t my_count = 0;
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+        const int64_t pq = p0 + q;
+        if (pq >= npairs) break;
+        const int64_t c0 = 2 * pq, c1 = 2 * pq + 1;
+        const bool h1 = c1 < a.nc;
+        uint64_t x0 = y0[q], x1 = y1[q];
+        if (lw) {
+            if (CX == DM_CX_TWOPOINT && cxf[q]) {
+                const int cp1 = (int)(cut[q] & 0xFFFFu), cp2 = (int)(cut[q] >> 16);
+                const uint64_t m = range_mask(cp1 - lane * 64, cp2 - lane * 64);
+                const uint64_t tt = (x0 ^ x1) & m;
+                x0 ^= tt;
+                x1 ^= tt;
+            }
+            if (MUT == DM_MUT_FLIPBIT) {
+                if ((mut_bits >> (2 * q)) & 1) x0 ^= flip_mask_word<false>(a, c0, lane);
+                if ((mut_bits >> (2 * q + 1)) & 1) x1 ^= flip_mask_word<false>(a, c1, lane);
+            }
+            uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
+            uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
+            __builtin_nontemporal_store(x0, w0 + lane);
+            if (h1) __builtin_nontemporal_store(x1, w1 + lane);
+        }
+        if (EVAL) {
+            uint32_t pc = lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
+            if ((lane >> 1) == q) my_count = (lane & 1) ? (pc >> 16) : (pc & 0xFFFFu);
+        }
+    }
+    // ---- fitness / validity of the wave's 8 children (contiguous stores)
+    if (live) {
+        if (EVAL) {
+            a.cwv[c] = inv ? (double)my_count * a.w0 : f;
+            a.cvalid[c] = 1;
+        } else {  // no evaluation requested: clones keep their fitness
+            a.cwv[c] = f;
+            a.cvalid[c] = inv ? 0 : 1;
+        }
+    }
+    if (EVAL && spread) {
+        // per-workgroup count into one of kEvalSpread counters (2^15
+        // same-address atomics per C2 generation serialised at one L2 channel
+        // and cost 0.19 ms); evals_sum_kernel folds them into nevals
+        __shared__ int32_t wave_evals[4];
+        if (lane == 0) wave_evals[threadIdx.x >> 6] = __popcll(inv_bits);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int tot = wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
+            if (tot)
+                atomicAdd((unsigned long long*)(spread + (blockIdx.x % kEvalSpread) * kEvalSpreadStride),
+                          (unsigned long long)tot);
+        }
+    }
+}
+
+// *nevals += sum of the spread counters, which are re-zeroed (one wave).
+__global__ __launch_bounds__(64) void evals_sum_kernel(long long* __restrict__ spread,
+                                                       int64_t* __restrict__ nevals) {
+    const int i = threadIdx.x;
+    long long t = 0;
+    if (i < kEvalSpread) {
+        t = spread[i * kEvalSpreadStride];
+        spread[i * kEvalSpreadStride] = 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (i == 0) *nevals += t;
+}
+
+int64_t gen_bits_fused_blocks(const GenArgs& a) {
+    const int64_t waves = ((a.nc + 1) / 2 + DM_BITS_PP - 1) / DM_BITS_PP;
+    return (waves + 3) / 4;
+}
+
+template <int CX, int MUT, bool EVAL, bool TOURN>
+static void launch_bf(const GenArgs& a, long long* wg, hipStream_t s) {
+    gen_bits_fused_kernel<CX, MUT, EVAL, TOURN>
+        <<<dim3((unsigned)gen_bits_fused_blocks(a)), 256, 0, s>>>(a, wg);
+}
+template <int CX, int MUT>
+static void launch_bf_e(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {
+    const bool tourn = a.sel == DM_SEL_TOURNAMENT;
+    if (eval)
+        tourn ? launch_bf<CX, MUT, true, true>(a, wg, s) : launch_bf<CX, MUT, true, false>(a, wg, s);
+    else
+        tourn ? launch_bf<CX, MUT, false, true>(a, wg, s) : launch_bf<CX, MUT, false, false>(a, wg, s);
+}
+
+// spread: the context's zeroed nevals counters, or null when nevals is not
+// counted; launch_evals_sum then folds them into a.nevals.
+void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s) {
+    const bool mf = a.mut == DM_MUT_FLIPBIT;
+    long long* wg = (eval && a.nevals) ? spread : nullptr;
+    if (a.cx == DM_CX_TWOPOINT)
+        mf ? launch_bf_e<DM_CX_TWOPOINT, DM_MUT_FLIPBIT>(a, eval, wg, s)
+           : launch_bf_e<DM_CX_TWOPOINT, DM_MUT_NONE>(a, eval, wg, s);
+    else
+        mf ? launch_bf_e<DM_CX_NONE, DM_MUT_FLIPBIT>(a, eval, wg, s)
+           : launch_bf_e<DM_CX_NONE, DM_MUT_NONE>(a, eval, wg, s);
+}
+void launch_evals_sum(long long* spread, int64_t* nevals, hipStream_t s) {
+    evals_sum_kernel<<<1, 64, 0, s>>>(spread, nevals);
+}
+
 template <int CX, int MUT, bool EVAL>
 static void launch_bp(const GenArgs& a, const PairPlan* plans, int num_cus, hipStream_t s) {
     // one-shot grid: every wave takes DM_BITS_PP consecutive pairs once

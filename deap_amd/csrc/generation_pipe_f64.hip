@@ -75,11 +75,13 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     return fl;
 }
 
-// With count_evals set, the plan kernel also adds the generation's `nevals`
-// (children whose fitness is invalidated, algorithms.py:171-174) to
-// *count_evals: one ballot per wave, one atomic per workgroup.
+// With count_evals set (the context's spread counters, kEvalSpread of them),
+// the plan kernel also counts the generation's `nevals` (children whose
+// fitness is invalidated, algorithms.py:171-174): one ballot per wave, one
+// atomic per workgroup into counter blockIdx % kEvalSpread; launch_evals_sum
+// folds them into nevals.
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
-                                                        int64_t* __restrict__ count_evals) {
+                                                        long long* __restrict__ count_evals) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
     if (count_evals) {
@@ -92,14 +94,17 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
         __syncthreads();
         if (threadIdx.x == 0) {
             const int64_t t = (int64_t)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
-            if (t) atomicAdd((unsigned long long*)count_evals, (unsigned long long)t);
+            if (t)
+                atomicAdd((unsigned long long*)(count_evals +
+                                                (blockIdx.x % kEvalSpread) * kEvalSpreadStride),
+                          (unsigned long long)t);
         }
         return;
     }
     if (p < npairs) plan_one(a, plans, p);
 }
 
-void launch_pair_plans(const GenArgs& a, PairPlan* plans, int64_t* count_evals, hipStream_t s) {
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s) {
     const int64_t npairs = (a.nc + 1) / 2;
     pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals);
 }

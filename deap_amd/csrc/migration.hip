@@ -87,24 +87,89 @@ __device__ __forceinline__ bool fit_prefilter(const double* a, uint8_t va, const
     return true;
 }
 
-// bitmap[j][w]: bit r%64 of word r/64 set iff row r equals immigrant j.
-__global__ void match_kernel(const char* genes, const double* wv, const uint8_t* valid, int64_t n,
-                             int64_t stride, int dim, int gtype, int nobj, const void* imm_block,
-                             int64_t k, int64_t words, unsigned long long* bitmap) {
+// Genome equality of rows a and b computed by a whole wave (value semantics
+// of the genome type; lanes stride the genes, pad bytes never read).
+__device__ __forceinline__ bool wave_genome_eq(const char* a, const char* b, int gtype, int dim,
+                                               int lane) {
+    bool ok = true;
+    if (gtype == DM_BITS) {
+        const uint64_t* x = (const uint64_t*)a;
+        const uint64_t* y = (const uint64_t*)b;
+        for (int w = lane; w < (dim + 63) / 64; w += 64) ok = ok && x[w] == y[w];
+    } else if (gtype == DM_F32) {
+        const float* x = (const float*)a;
+        const float* y = (const float*)b;
+        for (int i = lane; i < dim; i += 64) ok = ok && x[i] == y[i];
+    } else {
+        const double* x = (const double*)a;
+        const double* y = (const double*)b;
+        for (int i = lane; i < dim; i += 64) ok = ok && x[i] == y[i];
+    }
+    return __ballot(!ok) == 0;
+}
+
+// bitmap[j][w]: bit r%64 of word r/64 set iff row r equals immigrant j;
+// first[j] = the lowest such row.  A wave owns 64 consecutive rows (one bitmap
+// word per immigrant, written with a plain store), lane = row: the row's
+// fitness / validity are loaded once and compared with a tile of 64
+// immigrants staged in LDS; a fitness match (or an invalid fitness on either
+// side) is confirmed by a genome comparison done by the whole wave.
+__global__ __launch_bounds__(256) void match_kernel(const char* genes, const double* wv,
+                                                    const uint8_t* valid, int64_t n, int64_t stride,
+                                                    int dim, int gtype, int nobj,
+                                                    const void* imm_block, int64_t k, int64_t words,
+                                                    unsigned long long* bitmap, int32_t* first) {
     Block im = block_view((void*)imm_block, stride, nobj, k);
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        for (int64_t j = 0; j < k; ++j) {
-            // list.index tests `is` before `==` (PyObject_RichCompareBool): the
-            // immigrant's own row matches even when its genome holds a NaN
-            if (r == im.src[j]) {
-                atomicOr(&bitmap[j * words + (r >> 6)], 1ull << (r & 63));
-                continue;
+    __shared__ double swv[64 * DM_MAX_OBJ];
+    __shared__ int32_t ssrc[64];
+    __shared__ uint8_t sval[64];
+    const int lane = threadIdx.x & 63;
+    const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t jt = 0; jt < k; jt += 64) {
+        const int jn = (int)(k - jt < 64 ? k - jt : 64);
+        __syncthreads();
+        if (threadIdx.x < jn) {
+            const int64_t j = jt + threadIdx.x;
+            ssrc[threadIdx.x] = im.src[j];
+            sval[threadIdx.x] = im.valid[j];
+            for (int o = 0; o < nobj; ++o) swv[threadIdx.x * nobj + o] = im.wv[j * nobj + o];
+        }
+        __syncthreads();
+        for (int64_t r0 = wave0 * 64; r0 < n; r0 += nwaves * 64) {
+            const int64_t r = r0 + lane;
+            const bool in = r < n;
+            double f[DM_MAX_OBJ];
+#pragma unroll
+            for (int o = 0; o < DM_MAX_OBJ; ++o) f[o] = (in && o < nobj) ? wv[r * nobj + o] : 0.0;
+            const uint8_t vr = in ? valid[r] : 0;
+            for (int jj = 0; jj < jn; ++jj) {
+                const int64_t j = jt + jj;
+                // list.index tests `is` before `==` (PyObject_RichCompareBool):
+                // the immigrant's own row matches even when its genome holds a NaN
+                const bool self = in && r == ssrc[jj];
+                bool eq = self;
+                // fitness prefilter (fit_prefilter, registers unrolled)
+                bool pre = in && !self;
+                if (pre && vr && sval[jj]) {
+#pragma unroll
+                    for (int o = 0; o < DM_MAX_OBJ; ++o)
+                        if (o < nobj && !(f[o] == swv[jj * nobj + o])) pre = false;
+                }
+                uint64_t hits = __ballot(pre);
+                while (hits) {  // wave-uniform
+                    const int l = __ffsll((long long)hits) - 1;
+                    hits &= hits - 1;
+                    const bool e = wave_genome_eq(genes + (r0 + l) * stride, im.genes + j * stride,
+                                                  gtype, dim, lane);
+                    if (lane == l) eq = e;
+                }
+                const uint64_t m = __ballot(eq);
+                if (lane == 0 && m) {
+                    bitmap[j * words + (r0 >> 6)] = m;
+                    atomicMin(&first[j], (int32_t)(r0 + __ffsll((long long)m) - 1));
+                }
             }
-            if (!fit_prefilter(wv + r * nobj, valid[r], im.wv + j * nobj, im.valid[j], nobj))
-                continue;
-            if (genome_eq(genes + r * stride, im.genes + j * stride, gtype, dim))
-                atomicOr(&bitmap[j * words + (r >> 6)], 1ull << (r & 63));
         }
     }
 }
@@ -126,7 +191,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
                                                       int64_t n, int64_t stride, int nobj,
                                                       const void* em_block, int64_t k,
                                                       int64_t words, unsigned long long* bitmap,
-                                                      const uint8_t* E, int32_t* slots,
+                                                      const uint8_t* E, const int32_t* first,
+                                                      int32_t* slots,
                                                       int32_t* content, int32_t* err) {
     Block em = block_view((void*)em_block, stride, nobj, k);
     __shared__ int64_t best;
@@ -138,8 +204,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
     for (int64_t j = 0; j < k; ++j) {
         if (threadIdx.x == 0) best = INT64_MAX;
         __syncthreads();
-        // (a) first original match still present: scan words in blocks of 256
-        for (int64_t wb = 0; wb < words; wb += blockDim.x) {
+        // (a) first original match still present: scan words in blocks of 256,
+        // from the first match the match kernel saw (bits are only ever cleared)
+        const int64_t w0 = first[j] < n ? (int64_t)(first[j] >> 6) : words;
+        for (int64_t wb = w0; wb < words; wb += blockDim.x) {
             const int64_t w = wb + threadIdx.x;
             if (w < words) {
                 const unsigned long long x = bitmap[j * words + w];
@@ -221,23 +289,29 @@ static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block
     const int64_t n = pop->n;
     const int64_t words = (n + 63) / 64;
     const size_t bm = align_up((size_t)k * words * 8, 256);
-    char* base = (char*)scratch_slot(ctx, 3, bm + align_up((size_t)k * k, 256) +
-                                                 align_up((size_t)std::max<int64_t>(n, 1) * 4, 256));
+    const size_t cb = align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);
+    char* base = (char*)scratch_slot(ctx, 3, bm + align_up((size_t)k * k, 256) + cb +
+                                                 align_up((size_t)k * 4, 256));
     if (!base) return DM_ERR_NOMEM;
     unsigned long long* bitmap = (unsigned long long*)base;
     uint8_t* E = (uint8_t*)(base + bm);
     int32_t* content = (int32_t*)(base + bm + align_up((size_t)k * k, 256));
+    int32_t* first = (int32_t*)((char*)content + cb);
     hipStream_t s = ctx->stream;
     DM_HIP(hipMemsetAsync(bitmap, 0, (size_t)k * words * 8, s));
     DM_HIP(hipMemsetAsync(content, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+    DM_HIP(hipMemsetAsync(first, 0x7F, (size_t)k * 4, s));  // INT32 ~max: no match yet
+    // one wave per 64 rows, at most 16 waves per CU slot pass
+    const unsigned grid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((words + 3) / 4, (int64_t)ctx->num_cus * 16));
     match_kernel<<<grid, 256, 0, s>>>((const char*)pop->genes, pop->wvalues, pop->valid, n,
                                       pop->stride, pop->dim, pop->gtype, pop->nobj,
-                                      immigrant_block, k, words, bitmap);
+                                      immigrant_block, k, words, bitmap, first);
     em_im_eq_kernel<<<(unsigned)std::max<int64_t>(1, (k * k + 255) / 256), 256, 0, s>>>(
         emigrant_block, immigrant_block, k, pop->stride, pop->dim, pop->gtype, pop->nobj, E);
     resolve_kernel<<<1, 256, 0, s>>>((char*)pop->genes, pop->wvalues, pop->valid, n, pop->stride,
-                                     pop->nobj, emigrant_block, k, words, bitmap, E, out_slots,
+                                     pop->nobj, emigrant_block, k, words, bitmap, E, first,
+                                     out_slots,
                                      content, err);
     DM_LAUNCH_CHECK();
     return DM_OK;

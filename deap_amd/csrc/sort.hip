@@ -330,95 +330,112 @@ int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool des
 
 
 // Top-k of a single-objective population (k <= TOPK_MAX): the order of the
-// first k entries of the stable sort, from two launches instead of a full
-// 8-pass radix sort of n keys — each block bitonic-sorts its slice of
-// (key, index) pairs in LDS and keeps its first k; one block then sorts the
-// blocks' candidates.  Pairs are distinct (the index breaks ties), so the
-// result is exactly the stable order: ties by ascending index.
+// first k entries of the stable sort without sorting n keys.  A wave holds
+// 1,024 (key, index) pairs in registers (16 per lane) and extracts its k
+// smallest in k rounds (lane minimum, 6-step shuffle minimum, the winner's
+// slot cleared); a pass turns n pairs into ceil(n / 1024) * k candidates and
+// is repeated until one wave's span remains (2^20 -> 15,360 -> 225 -> k for
+// k = 15).  Pairs are distinct (the index breaks ties), so the result is
+// exactly the stable order: ties by ascending index.  (The previous version
+// bitonic-sorted 4,096-pair slices in LDS and then all candidates in one
+// workgroup: 0.21 ms per selBest of 2^20; profiles/r02h.)
 constexpr int TOPK_MAX = 32;
+constexpr int TOPK_PER = 16;            // pairs per lane
+constexpr int TOPK_SPAN = 64 * TOPK_PER;  // pairs per wave
 
-template <int ITEMS>
-__device__ void bitonic_lds(uint64_t* key, int32_t* idx) {
-    for (int size = 2; size <= ITEMS; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < ITEMS / 2; t += blockDim.x) {
-                const int lo = 2 * t - (t & (stride - 1));
-                const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const uint64_t ka = key[lo], kb = key[hi];
-                const int32_t ia = idx[lo], ib = idx[hi];
-                const bool gt = ka > kb || (ka == kb && ia > ib);
-                if (gt == up) {
-                    key[lo] = kb;
-                    key[hi] = ka;
-                    idx[lo] = ib;
-                    idx[hi] = ia;
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-template <int ITEMS>
-__global__ __launch_bounds__(256) void topk_block_kernel(const double* wv, int64_t n, bool desc,
-                                                         int k, uint64_t* ckey, int32_t* cidx) {
-    __shared__ uint64_t key[ITEMS];
-    __shared__ int32_t idx[ITEMS];
-    const int64_t base = (int64_t)blockIdx.x * ITEMS;
-    for (int i = threadIdx.x; i < ITEMS; i += blockDim.x) {
-        const int64_t r = base + i;
+template <bool FROM_WV>
+__global__ __launch_bounds__(256) void topk_wave_kernel(const double* __restrict__ wv, bool desc,
+                                                        const uint64_t* __restrict__ ikey,
+                                                        const int32_t* __restrict__ iidx, int64_t n,
+                                                        int k, uint64_t* __restrict__ okey,
+                                                        int32_t* __restrict__ oidx,
+                                                        int32_t* __restrict__ out_final) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t base = wave * TOPK_SPAN;
+    if (base >= n) return;  // wave-uniform
+    uint64_t key[TOPK_PER];
+    int32_t idx[TOPK_PER];
+#pragma unroll
+    for (int j = 0; j < TOPK_PER; ++j) {
+        const int64_t r = base + j * 64 + lane;
+        key[j] = ~0ull;
+        idx[j] = INT32_MAX;
         if (r < n) {
-            const uint64_t q = ordered_key(wv[r]);
-            key[i] = desc ? ~q : q;
-            idx[i] = (int32_t)r;
-        } else {
-            key[i] = ~0ull;
-            idx[i] = INT32_MAX;
+            if (FROM_WV) {
+                const uint64_t q = ordered_key(wv[r]);
+                key[j] = desc ? ~q : q;
+                idx[j] = (int32_t)r;
+            } else {
+                key[j] = ikey[r];
+                idx[j] = iidx[r];
+            }
         }
     }
-    __syncthreads();
-    bitonic_lds<ITEMS>(key, idx);
-    for (int i = threadIdx.x; i < k; i += blockDim.x) {
-        ckey[(int64_t)blockIdx.x * k + i] = key[i];
-        cidx[(int64_t)blockIdx.x * k + i] = idx[i];
+    for (int round = 0; round < k; ++round) {
+        uint64_t bk = key[0];
+        int32_t bi = idx[0];
+#pragma unroll
+        for (int j = 1; j < TOPK_PER; ++j)
+            if (key[j] < bk || (key[j] == bk && idx[j] < bi)) {
+                bk = key[j];
+                bi = idx[j];
+            }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t ok = __shfl_xor(bk, o, 64);
+            const int32_t oi = __shfl_xor(bi, o, 64);
+            if (ok < bk || (ok == bk && oi < bi)) {
+                bk = ok;
+                bi = oi;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TOPK_PER; ++j)
+            if (idx[j] == bi && key[j] == bk) {
+                key[j] = ~0ull;
+                idx[j] = INT32_MAX;
+            }
+        if (lane == 0) {
+            if (out_final) {
+                out_final[round] = bi;
+            } else {
+                okey[wave * k + round] = bk;
+                oidx[wave * k + round] = bi;
+            }
+        }
     }
-}
-
-template <int ITEMS>
-__global__ __launch_bounds__(1024) void topk_merge_kernel(const uint64_t* ckey, const int32_t* cidx,
-                                                          int ncand, int k, int32_t* out) {
-    __shared__ uint64_t key[ITEMS];
-    __shared__ int32_t idx[ITEMS];
-    for (int i = threadIdx.x; i < ITEMS; i += blockDim.x) {
-        key[i] = i < ncand ? ckey[i] : ~0ull;
-        idx[i] = i < ncand ? cidx[i] : INT32_MAX;
-    }
-    __syncthreads();
-    bitonic_lds<ITEMS>(key, idx);
-    for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = idx[i];
 }
 
 static int sel_topk(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx, bool best) {
     const int64_t n = pop->n;
-    const int items = n <= (1ll << 18) ? 1024 : n <= (1ll << 20) ? 4096 : 8192;
-    const int64_t blocks = (n + items - 1) / items;
-    const int64_t ncand = blocks * k;
-    char* w = (char*)scratch_slot(ctx, 3, align_up((size_t)ncand * 8, 256) + (size_t)ncand * 4);
+    auto waves = [](int64_t m) { return (m + TOPK_SPAN - 1) / TOPK_SPAN; };
+    const int64_t c1 = waves(n) * k;  // candidates after the first pass
+    const size_t kb = align_up((size_t)c1 * 8, 256), ib = align_up((size_t)c1 * 4, 256);
+    char* w = (char*)scratch_slot(ctx, 3, 2 * (kb + ib));
     if (!w) return DM_ERR_NOMEM;
-    uint64_t* ckey = (uint64_t*)w;
-    int32_t* cidx = (int32_t*)(w + align_up((size_t)ncand * 8, 256));
+    uint64_t* key[2] = {(uint64_t*)w, (uint64_t*)(w + kb + ib)};
+    int32_t* idx[2] = {(int32_t*)(w + kb), (int32_t*)(w + 2 * kb + ib)};
     hipStream_t s = ctx->stream;
-    if (items == 1024)
-        topk_block_kernel<1024><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
-    else if (items == 4096)
-        topk_block_kernel<4096><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
-    else
-        topk_block_kernel<8192><<<(unsigned)blocks, 256, 0, s>>>(pop->wvalues, n, best, (int)k, ckey, cidx);
-    if (ncand <= 1024)
-        topk_merge_kernel<1024><<<1, 1024, 0, s>>>(ckey, cidx, (int)ncand, (int)k, out_idx);
-    else
-        topk_merge_kernel<8192><<<1, 1024, 0, s>>>(ckey, cidx, (int)ncand, (int)k, out_idx);
+    auto grid = [&](int64_t m) { return dim3((unsigned)((waves(m) + 3) / 4)); };
+    if (n <= TOPK_SPAN) {
+        topk_wave_kernel<true><<<1, 64, 0, s>>>(pop->wvalues, best, nullptr, nullptr, n, (int)k,
+                                                nullptr, nullptr, out_idx);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    topk_wave_kernel<true><<<grid(n), 256, 0, s>>>(pop->wvalues, best, nullptr, nullptr, n, (int)k,
+                                                   key[0], idx[0], nullptr);
+    int64_t m = c1;
+    int cur = 0;
+    while (m > TOPK_SPAN) {
+        topk_wave_kernel<false><<<grid(m), 256, 0, s>>>(nullptr, best, key[cur], idx[cur], m, (int)k,
+                                                        key[cur ^ 1], idx[cur ^ 1], nullptr);
+        m = waves(m) * k;
+        cur ^= 1;
+    }
+    topk_wave_kernel<false><<<1, 64, 0, s>>>(nullptr, best, key[cur], idx[cur], m, (int)k, nullptr,
+                                             nullptr, out_idx);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -436,7 +453,7 @@ static int sel_sorted(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_id
     if (k == 0) return DM_OK;
     DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
     // small k of a single objective (migRing emigrants, HallOfFame candidates)
-    if (pop->nobj == 1 && k <= TOPK_MAX && pop->n > 4 * k && pop->n <= 256ll * 8192 &&
+    if (pop->nobj == 1 && k <= TOPK_MAX && pop->n > 4 * k &&
         !std::getenv("DM_SELBEST_FULLSORT"))
         return sel_topk(ctx, pop, k, out_idx, best);
     int32_t* full = out_idx;

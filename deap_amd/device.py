@@ -282,22 +282,22 @@ class DevicePopulation:
         else:
             genes, wv, valid = self.rows_numpy(indices)
             rows = range(len(genes))
-        out = []
-        for i in rows:
-            vals = genes[i].tolist()
-            if cls_ is None:
-                ind = _HostIndividual(vals)
-                ind.fitness = _make_fitness(self.weights)
-            elif issubclass(cls_, _array.array):
-                ind = cls_(vals)
-            else:
-                ind = cls_(vals)
-            if not hasattr(ind, "fitness"):
-                ind.fitness = _make_fitness(self.weights)
-            if valid[i]:
-                ind.fitness.wvalues = tuple(float(x) for x in wv[i])
-            out.append(ind)
-        return out
+        return [self.make_individual(genes[i], wv[i], valid[i], cls_) for i in rows]
+
+    def make_individual(self, gene_row, wv_row, valid, individual_class=None):
+        """One host individual from a host copy of its row (unpacked genes)."""
+        cls_ = individual_class or self.individual_class
+        vals = gene_row.tolist()
+        if cls_ is None:
+            ind = _HostIndividual(vals)
+            ind.fitness = _make_fitness(self.weights)
+        else:
+            ind = cls_(vals)
+        if not hasattr(ind, "fitness"):
+            ind.fitness = _make_fitness(self.weights)
+        if valid:
+            ind.fitness.wvalues = tuple(float(x) for x in wv_row)
+        return ind
 
     def __repr__(self):
         names = {v: k for k, v in GTYPE_NAMES.items()}

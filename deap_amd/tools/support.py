@@ -289,6 +289,11 @@ class Logbook(list):
 _VALUE_SIMILAR = (operator.eq, np.array_equal)
 
 
+def _host_fitness(weights):
+    from ..device import HostFitness
+    return HostFitness(weights)
+
+
 class HallOfFame:
     def __init__(self, maxsize, similar=operator.eq):
         self.maxsize = maxsize
@@ -338,7 +343,13 @@ class HallOfFame:
         never in the final hall — it would be the worst entry when a better
         row of C arrives and be evicted, or be skipped as not better than the
         worst — and while present it only holds a slot a row of C later takes
-        (equal genomes have equal fitness within one evaluated population)."""
+        (equal genomes have equal fitness within one evaluated population).
+
+        Only C's rows leave the GPU (one gather), as numpy rows: ``similar``
+        is evaluated as row equality in numpy (element-wise ``==``: NaN genes
+        are never similar and -0.0 == 0.0, as list / array equality of
+        separate objects behaves), and host individuals are built only for
+        the rows that enter the hall."""
         from .selection import selBest
         n = len(pop)
         K = min(n, max(4 * self.maxsize, 64))
@@ -346,16 +357,70 @@ class HallOfFame:
             order = selBest(pop, K).cpu().tolist()
             trial = copy.copy(self)
             trial.keys, trial.items = list(self.keys), list(self.items)
+            trial._garr = dict(self._garr_cache())
             rows = sorted(set(order) | ({0} if len(self) == 0 else set()))
-            inds = dict(zip(rows, pop.to_individuals(indices=rows)))
-            trial._loop(rows, inds)
+            genes, wv, ok = pop.rows_numpy(rows)
+            fits = []
+            for r in range(len(rows)):
+                f = _host_fitness(pop.weights)
+                if ok[r]:
+                    f.wvalues = tuple(float(x) for x in wv[r])
+                fits.append(f)
+            trial._loop_rows(pop, rows, genes, wv, ok, fits)
             if K >= n:
                 break
-            t = inds[order[-1]].fitness
+            t = fits[rows.index(order[-1])]
             if len(trial) == self.maxsize and trial[-1].fitness > t:
                 break
             K = min(n, 4 * K)
         self.keys, self.items = trial.keys, trial.items
+        self._garr = {id(it): trial._garr[id(it)] for it in self.items
+                      if trial._garr.get(id(it), (None,))[0] is it}
+
+    def _garr_cache(self):
+        cache = getattr(self, "_garr", None)
+        if cache is None:
+            cache = self._garr = {}
+        return cache
+
+    def _genome(self, item):
+        """numpy view of a hofer's genome, cached by identity (the entry keeps
+        its object, so a recycled id never aliases another individual)."""
+        cache = self._garr_cache()
+        ent = cache.get(id(item))
+        if ent is None or ent[0] is not item:
+            ent = cache[id(item)] = (item, np.asarray(item))
+        return ent[1]
+
+    def __getstate__(self):
+        state = dict(self.__dict__)
+        state.pop("_garr", None)
+        return state
+
+    def _loop_rows(self, pop, rows, genes, wv, ok, fits):
+        """support.py:528-548 over candidate rows held as numpy rows."""
+        def make(r):
+            ind = pop.make_individual(genes[r], wv[r], ok[r])
+            self._garr_cache()[id(ind)] = (ind, genes[r])
+            return ind
+        for r in range(len(rows)):
+            if len(self) == 0 and self.maxsize != 0:
+                # first iteration with an empty hall: population[0] goes in
+                self._insert_owned(make(rows.index(0)))
+                continue
+            if fits[r] > self[-1].fitness or len(self) < self.maxsize:
+                g = genes[r]
+                if any(np.array_equal(g, self._genome(h)) for h in self):
+                    continue
+                if len(self) >= self.maxsize:
+                    self.remove(-1)
+                self._insert_owned(make(r))
+
+    def _insert_owned(self, item):
+        """insert() without the deepcopy: ``item`` is a fresh host individual."""
+        i = bisect.bisect_right(self.keys, item.fitness)
+        self.items.insert(len(self) - i, item)
+        self.keys.insert(i, item.fitness)
 
     def _loop(self, rows, inds):
         """support.py:528-548 over the rows of a candidate set, in order."""

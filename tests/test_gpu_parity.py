@@ -456,6 +456,8 @@ def test_sel_best_large_ties(gpu):
     ("bits", 4096, 40001, "twopoint", "flipbit", "onemax", "tournament"),
     ("bits", 100, 3000, "twopoint", "flipbit", "onemax", "random"),
     ("bits", 1000, 999, "twopoint", "flipbit", "onemax", "tournament7"),
+    # more than 8 aspirants: the plan kernel + burst kernel form
+    ("bits", 500, 2001, "twopoint", "flipbit", "onemax", "tournament9"),
 ])
 def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
     """The hot path (per-pair plan kernel + rolling-pipeline kernel, native
@@ -473,7 +475,7 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
                                    stream=stream)
         getattr(benchmarks, objective)(pop)
         tb = _toolbox(cx, mut, 0.05, 0.5, evaluate=objective,
-                      tournsize=7 if sel == "tournament7" else 3)
+                      tournsize=int(sel[10:] or 3) if sel.startswith("tournament") else 3)
         if sel == "random":
             tb.register("select", tools.selRandom)
         decs = [] if mode == "dump" else None
