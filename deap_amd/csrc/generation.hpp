@@ -460,40 +460,95 @@ __device__ __forceinline__ uint64_t range_mask(int lo, int hi) {  // bits [lo, h
     return up & ~dn;
 }
 
-// mutFlipBit on one word (mutation.py:139-141): Bernoulli(indpb) per gene.
-template <bool RP>
-__device__ __forceinline__ uint64_t flip_mask_word(const GenArgs& a, int64_t c, int wi) {
-    if ((RP && a.mode == DM_RNG_INJECT)) return a.dec.mut_mask[c * a.words64 + wi];
-    const int nbits = min(64, a.dim - wi * 64);
+// mutFlipBit (mutation.py:124-142): Bernoulli(indpb) per gene, drawn as ONE
+// geometric-skip sequence over the whole row: uniform i of
+// child c is word i & 3 of Philox(ST_FLIP, c, i >> 2), u = (w + 1) / 2^32,
+// gap_i = min(floor(log2f(u) / log2(1 - indpb)), 65536) (fp32), and the
+// flipped genes are P_m = P_{m-1} + 1 + gap_m (P_{-1} = -1) while P_m < dim.
+// A group of G lanes draws 4G gaps per round (lane `sub` = Philox call
+// round * G + sub) and places them with a group prefix sum, so a 4096-gene
+// row at indpb 0.05 takes one Philox call per lane.  The positions of the
+// current round stay in registers across the G-word chunks of a row; a
+// chunk's words are assembled in LDS (G words per group, ds_or).
+template <int G>
+struct FlipRow {
+    int32_t pos[4];  // this lane's positions in the current round (ascending)
+    int32_t last;    // last position of the round (group-uniform)
+    uint32_t round;
+};
+
+template <int G>
+__device__ __forceinline__ void flip_round(const GenArgs& a, int64_t c, int sub, int32_t base,
+                                           FlipRow<G>& st) {
+    const u32x4 w = a.rng(ST_FLIP, (uint32_t)c, st.round * G + (uint32_t)sub);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    int32_t s = 0, loc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float u = ((float)ws[j] + 1.0f) * 2.3283064365386963e-10f;
+        const float gap = floorf(__log2f(fminf(u, 1.0f)) * a.flip_inv_log2);
+        s += 1 + (int32_t)fminf(gap, 65536.0f);
+        loc[j] = s;
+    }
+    int32_t incl = s;  // group inclusive scan of the lanes' sums
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+        const int32_t t = __shfl_up(incl, d, G);
+        if (sub >= d) incl += t;
+    }
+    const int32_t excl = base + incl - s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st.pos[j] = excl + loc[j];
+    st.last = base + __shfl(incl, G - 1, G);
+}
+
+template <int G>
+__device__ __forceinline__ void flip_begin(const GenArgs& a, int64_t c, int sub, FlipRow<G>& st) {
+    st.round = 0;
+    if (a.thr_ind > 0 && a.thr_ind < (1ull << 32)) flip_round<G>(a, c, sub, -1, st);
+}
+
+// The flip mask of word wb + sub of child c (chunk [64 wb, 64 (wb + G)) of the
+// row); called by every lane of the group, chunks in ascending order.
+// `lds`: this group's G words.  Inject / dump as the replay modes need.
+template <int G, bool RP>
+__device__ __forceinline__ uint64_t flip_mask_chunk(const GenArgs& a, int64_t c, int wb, int sub,
+                                                    FlipRow<G>& st, uint64_t* lds) {
+    const int wi = wb + sub;
+    const bool in = wi < a.words64;
+    if ((RP && a.mode == DM_RNG_INJECT)) return in ? a.dec.mut_mask[c * a.words64 + wi] : 0ull;
     uint64_t mask = 0;
     if (a.thr_ind >= (1ull << 32)) {
-        mask = nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
+        const int nbits = min(64, a.dim - wi * 64);
+        mask = !in ? 0ull : nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
     } else if (a.thr_ind > 0) {
-        // geometric skips: gap ~ floor(log2(u) / log2(1 - p)), u in (0, 1]
-        int pos = -1;
-        for (uint32_t call = 0;; ++call) {
-            const u32x4 w = a.rng(ST_FLIP, (uint32_t)c, ((uint32_t)wi << 8) | call);
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-            bool done = false;
+        const int32_t lo = wb * 64;
+        const int32_t hi = min(a.dim, (wb + G) * 64);
+        lds[sub] = 0;
+        __builtin_amdgcn_wave_barrier();
+        while (true) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if (!done) {
-                    const float u = ((float)ws[j] + 1.0f) * 2.3283064365386963e-10f;
-                    const float gap = floorf(__log2f(fminf(u, 1.0f)) * a.flip_inv_log2);
-                    pos += 1 + (int)fminf(gap, 64.0f);
-                    if (pos >= nbits) done = true;
-                    else mask |= 1ull << pos;
-                }
+                const int32_t q = st.pos[j];
+                if (q >= lo && q < hi) atomicOr((unsigned long long*)&lds[(q - lo) >> 6], 1ull << (q & 63));
             }
-            if (done || call >= 255) break;
+            if (st.last >= hi) break;  // the round reaches the next chunk (kept)
+            st.round += 1;
+            flip_round<G>(a, c, sub, st.last, st);
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        mask = lds[sub];
+        __builtin_amdgcn_wave_barrier();
     }
-    if ((RP && a.mode == DM_RNG_DUMP)) a.dec.mut_mask[c * a.words64 + wi] = mask;
+    if ((RP && a.mode == DM_RNG_DUMP) && in) a.dec.mut_mask[c * a.words64 + wi] = mask;
     return mask;
 }
 
 template <int G, int CX, int MUT, int EC, bool RP>
 __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
+    __shared__ uint64_t flip_lds_all[256];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~(G - 1));
     const int lane = threadIdx.x & 63;
     const int sub = lane & (G - 1);
     const bool leader = sub == 0;
@@ -514,8 +569,18 @@ __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
         uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
         uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
         int64_t pc0 = 0, pc1 = 0;
+        FlipRow<G> fr0, fr1;
+        if (MUT == DM_MUT_FLIPBIT) {
+            if (d.mut0) flip_begin<G>(a, c0, sub, fr0);
+            if (d.mut1) flip_begin<G>(a, c1, sub, fr1);
+        }
         for (int wb = 0; wb < a.words64; wb += G) {
             const int wi = wb + sub;
+            uint64_t f0 = 0, f1 = 0;  // flip masks: every lane of the group takes part
+            if (MUT == DM_MUT_FLIPBIT) {
+                if (d.mut0) f0 = flip_mask_chunk<G, RP>(a, c0, wb, sub, fr0, flip_lds);
+                if (d.mut1) f1 = flip_mask_chunk<G, RP>(a, c1, wb, sub, fr1, flip_lds);
+            }
             if (wi < a.words64) {
                 uint64_t x0 = r0[wi];
                 uint64_t x1 = has1 ? r1[wi] : 0ull;
@@ -525,10 +590,8 @@ __global__ __launch_bounds__(256) void gen_bits_kernel(GenArgs a) {
                     x0 ^= t;
                     x1 ^= t;
                 }
-                if (MUT == DM_MUT_FLIPBIT) {
-                    if (d.mut0) x0 ^= flip_mask_word<RP>(a, c0, wi);
-                    if (d.mut1) x1 ^= flip_mask_word<RP>(a, c1, wi);
-                }
+                x0 ^= f0;
+                x1 ^= f1;
                 __builtin_nontemporal_store(x0, &w0[wi]);
                 if (has1) __builtin_nontemporal_store(x1, &w1[wi]);
                 pc0 += __popcll(x0);

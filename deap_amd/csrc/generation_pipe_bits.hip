@@ -16,7 +16,7 @@
 //     (tools_gpu/bwtest5.hip, profiles/r01f).
 //
 // Per pair: cxTwoPoint = masked word swap (crossover.py:37-60), mutFlipBit =
-// geometric-skip flip masks (flip_mask_word, mutation.py:124-142), OneMax =
+// row-level geometric-skip flip masks (flip_mask_row, mutation.py:124-142), OneMax =
 // popcount (README.md:85-86) of both children reduced in ONE wave reduction
 // (two 16-bit counts packed in a 32-bit lane value; a row has <= 4096 ones).
 // Children are bit-identical to gen_bits_kernel's native mode:
@@ -25,6 +25,22 @@
 
 namespace dm {
 
+// Flip mask of word `lane` of child c's row (<= 64 words): the row-level
+// geometric stream of flip_mask_chunk drawn by the whole wave.
+__device__ __forceinline__ uint64_t flip_mask_row(const GenArgs& a, int64_t c, int lane,
+                                                  uint64_t* lds) {
+    FlipRow<64> st;
+    flip_begin<64>(a, c, lane, st);
+    return flip_mask_chunk<64, false>(a, c, 0, lane, st, lds);
+}
+
+// Profiling-only ablations of the fused kernel (product build: 0): bit 0
+// skips the mutFlipBit masks, bit 1 the aspirants' fitness loads, bit 2 the
+// Philox evaluation of the decisions.
+#ifndef DM_BITS_ABLATE
+#define DM_BITS_ABLATE 0
+#endif
+
 #ifndef DM_BITS_PP
 #define DM_BITS_PP 4  // pairs per wave (tools_gpu/bwtest5.hip: 2-4 best)
 #endif
@@ -32,6 +48,8 @@ namespace dm {
 template <int CX, int MUT, bool EVAL>
 __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const PairPlan* plans) {
     constexpr int PP = DM_BITS_PP;
+    __shared__ uint64_t flip_lds_all[256];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~63);
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PP;
@@ -65,6 +83,11 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
         const uint32_t fl = cur.flags;
         const bool has1 = fl & PF_HAS1, inv0 = fl & PF_INV0, inv1 = fl & PF_INV1;
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
+        uint64_t f0 = 0, f1 = 0;  // flip masks, drawn by the whole wave per row
+        if (MUT == DM_MUT_FLIPBIT) {
+            if (fl & PF_MUT0) f0 = flip_mask_row(a, c0, lane, flip_lds);
+            if (fl & PF_MUT1) f1 = flip_mask_row(a, c1, lane, flip_lds);
+        }
         if (lw) {
             if (CX == DM_CX_TWOPOINT && (fl & PF_CX)) {
                 const int cp1 = (int)(cur.cuts & 0xFFFFu), cp2 = (int)(cur.cuts >> 16);
@@ -73,10 +96,8 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
                 x0 ^= t;
                 x1 ^= t;
             }
-            if (MUT == DM_MUT_FLIPBIT) {
-                if (fl & PF_MUT0) x0 ^= flip_mask_word<false>(a, c0, lane);
-                if (fl & PF_MUT1) x1 ^= flip_mask_word<false>(a, c1, lane);
-            }
+            x0 ^= f0;  // mutation after the crossover (algorithms.py:72-81)
+            x1 ^= f1;
             uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
             uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
             __builtin_nontemporal_store(x0, w0 + lane);
@@ -119,11 +140,13 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
 // Same Philox counters as pair_plan_kernel / gen_bits_kernel: bit-identical
 // children (tests/test_gpu_parity.py::test_native_hot_kernel_equals_replay_kernel).
 // ---------------------------------------------------------------------------
-template <int CX, int MUT, bool EVAL, bool TOURN>
+template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long long* spread) {
-    constexpr int PP = DM_BITS_PP;
     constexpr int NCH = 2 * PP;  // children per wave
-    static_assert(NCH == 8, "lane layout assumes 8 children per wave");
+    static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
+    constexpr int CXL = 32, MUTL = 32 + 2 * PP;  // first crossover / mutation lane
+    __shared__ uint64_t flip_lds_all[256];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~63);
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PP;
@@ -131,42 +154,47 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
     const uint32_t np = (uint32_t)a.np;
 
     // ---- decisions: ONE Philox call per lane covers every draw of the wave
-    //   lanes  0-31: selection, child L & 7, call L >> 3 (aspirants 2call, 2call+1)
-    //   lanes 32-39: crossover of pair (L - 32) & 3, call (L - 32) >> 2
-    //   lanes 40-47: mutation flag of child L - 40
+    //   lanes 0-31: selection, child L % NCH, call L / NCH (aspirants 2call, 2call+1)
+    //   lanes CXL..CXL+2PP-1: crossover of pair (L - CXL) % PP, call (L - CXL) / PP
+    //   lanes MUTL..MUTL+NCH-1: mutation flag of child L - MUTL
     const int t = TOURN ? a.tournsize : 1;
-    const int S = (t + 1) >> 1;  // selection calls per child (t <= 8)
+    const int S = (t + 1) >> 1;  // selection calls per child (t <= 64 / NCH)
     uint32_t stage = ST_SEL, item = 0, sub = 0;
     bool draw = false;
-    if (lane < 32) {
-        item = (uint32_t)(cbase + (lane & 7));
-        sub = (uint32_t)(lane >> 3);
-        draw = (int)sub < S && cbase + (lane & 7) < a.nc;
-    } else if (lane < 40) {
-        const int64_t pp = p0 + ((lane - 32) & 3);
+    if (lane < CXL) {
+        item = (uint32_t)(cbase + (lane % NCH));
+        sub = (uint32_t)(lane / NCH);
+        draw = (int)sub < S && cbase + (lane % NCH) < a.nc;
+    } else if (lane < MUTL) {
+        const int64_t pp = p0 + ((lane - CXL) % PP);
         stage = ST_CX;
         item = (uint32_t)pp;
-        sub = (uint32_t)((lane - 32) >> 2);
+        sub = (uint32_t)((lane - CXL) / PP);
         draw = CX != DM_CX_NONE && 2 * pp + 1 < a.nc;
-    } else if (lane < 48) {
+    } else if (lane < MUTL + NCH) {
         stage = ST_MUT;
-        item = (uint32_t)(cbase + lane - 40);
-        draw = MUT != DM_MUT_NONE && cbase + lane - 40 < a.nc;
+        item = (uint32_t)(cbase + lane - MUTL);
+        draw = MUT != DM_MUT_NONE && cbase + lane - MUTL < a.nc;
     }
     u32x4 w{};
-    if (draw) w = a.rng(stage, item, sub);
+    if (draw) {
+        if (DM_BITS_ABLATE & 4)
+            w = u32x4{item * 2654435761u ^ sub, item * 40503u + stage, item ^ 0x9E3779B9u, sub + item};
+        else
+            w = a.rng(stage, item, sub);
+    }
     // selection lanes: both aspirants of the call, fitness and validity
     int32_t k0 = 0, k1 = 0;
     double f0 = 0.0, f1 = 0.0;
     uint32_t v0 = 0, v1 = 0;
-    if (draw && lane < 32) {
+    if (draw && lane < CXL) {
         k0 = (int32_t)bounded64(w.x, w.y, np);
-        f0 = a.pwv[k0];
-        v0 = a.pvalid[k0];
+        f0 = (DM_BITS_ABLATE & 2) ? (double)(k0 & 255) : a.pwv[k0];
+        v0 = (DM_BITS_ABLATE & 2) ? 1u : a.pvalid[k0];
         if (2 * (int)sub + 1 < t) {
             k1 = (int32_t)bounded64(w.z, w.w, np);
-            f1 = a.pwv[k1];
-            v1 = a.pvalid[k1];
+            f1 = (DM_BITS_ABLATE & 2) ? (double)(k1 & 255) : a.pwv[k1];
+            v1 = (DM_BITS_ABLATE & 2) ? 1u : a.pvalid[k1];
         }
     }
     // tournament of child L (lanes 0-7): first-drawn wins, a later aspirant
@@ -176,7 +204,7 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
     uint32_t v = v0;
     if (TOURN) {
         for (int jj = 1; jj < t; ++jj) {
-            const int src = (jj >> 1) * 8 + (lane & 7);
+            const int src = (jj >> 1) * NCH + (lane % NCH);
             const double fj = __shfl((jj & 1) ? f1 : f0, src, 64);
             const int32_t kj = __shfl((jj & 1) ? k1 : k0, src, 64);
             const uint32_t vj = __shfl((jj & 1) ? v1 : v0, src, 64);
@@ -187,12 +215,12 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
             }
         }
     }
-    // crossover lanes 32-35: flag and cxTwoPoint cuts of pair L - 32
-    // (call 1's words come from lane L + 4)
-    const uint32_t w2x = (uint32_t)__shfl((int)w.x, (lane + 4) & 63, 64);
-    const uint32_t w2y = (uint32_t)__shfl((int)w.y, (lane + 4) & 63, 64);
+    // crossover lanes CXL..CXL+PP-1: flag and cxTwoPoint cuts of pair L - CXL
+    // (call 1's words come from lane L + PP)
+    const uint32_t w2x = (uint32_t)__shfl((int)w.x, (lane + PP) & 63, 64);
+    const uint32_t w2y = (uint32_t)__shfl((int)w.y, (lane + PP) & 63, 64);
     uint32_t cxf_l = 0, cuts = 0;
-    if (draw && lane >= 32 && lane < 36 && (uint64_t)w.x < a.thr_cx) {
+    if (draw && lane >= CXL && lane < CXL + PP && (uint64_t)w.x < a.thr_cx) {
         cxf_l = 1;
         if (CX == DM_CX_TWOPOINT) {
             int32_t r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
@@ -207,13 +235,15 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
             cuts = (uint32_t)r1 | ((uint32_t)r2 << 16);
         }
     }
-    const bool mut_l = draw && lane >= 40 && lane < 48 && (uint64_t)w.x < a.thr_mut;
+    const bool mut_l = draw && lane >= MUTL && lane < MUTL + NCH && (uint64_t)w.x < a.thr_mut;
     // per child (lanes 0-7): its pair's crossover flag, its mutation flag
-    const int ch = lane & 7;
+    const int ch = lane % NCH;
     const int64_t c = cbase + ch;
     const bool live = lane < NCH && c < a.nc;
-    const bool cx_c = __shfl((int)cxf_l, 32 + (ch >> 1), 64) != 0;
-    const bool mut = live && __shfl((int)mut_l, 40 + ch, 64) != 0;
+    // (shuffles outside any condition: a bpermute reads 0 from inactive lanes)
+    const bool cx_c = __shfl((int)cxf_l, CXL + (ch >> 1), 64) != 0;
+    const int mut_c = __shfl((int)mut_l, MUTL + ch, 64);
+    const bool mut = live && mut_c != 0;
     const bool inv = live && (cx_c || mut || !v);
     const uint64_t mut_bits = __ballot(mut);
     const uint64_t inv_bits = __ballot(inv);
@@ -231,8 +261,8 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
     for (int q = 0; q < PP; ++q) {
         s0[q] = __builtin_amdgcn_readlane(k, 2 * q);
         s1[q] = __builtin_amdgcn_readlane(k, 2 * q + 1);
-        cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)cuts, 32 + q);
-        cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)cxf_l, 32 + q);
+        cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)cuts, CXL + q);
+        cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)cxf_l, CXL + q);
         y0[q] = 0;
         y1[q] = 0;
         if (lw && p0 + q < npairs) {
@@ -248,6 +278,11 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
         const int64_t c0 = 2 * pq, c1 = 2 * pq + 1;
         const bool h1 = c1 < a.nc;
         uint64_t x0 = y0[q], x1 = y1[q];
+        uint64_t f0 = 0, f1 = 0;  // flip masks, drawn by the whole wave per row
+        if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1)) {
+            if ((mut_bits >> (2 * q)) & 1) f0 = flip_mask_row(a, c0, lane, flip_lds);
+            if ((mut_bits >> (2 * q + 1)) & 1) f1 = flip_mask_row(a, c1, lane, flip_lds);
+        }
         if (lw) {
             if (CX == DM_CX_TWOPOINT && cxf[q]) {
                 const int cp1 = (int)(cut[q] & 0xFFFFu), cp2 = (int)(cut[q] >> 16);
@@ -256,10 +291,8 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
                 x0 ^= tt;
                 x1 ^= tt;
             }
-            if (MUT == DM_MUT_FLIPBIT) {
-                if ((mut_bits >> (2 * q)) & 1) x0 ^= flip_mask_word<false>(a, c0, lane);
-                if ((mut_bits >> (2 * q + 1)) & 1) x1 ^= flip_mask_word<false>(a, c1, lane);
-            }
+            x0 ^= f0;  // mutation after the crossover (algorithms.py:72-81)
+            x1 ^= f1;
             uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
             uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
             __builtin_nontemporal_store(x0, w0 + lane);
@@ -312,36 +345,48 @@ __global__ __launch_bounds__(64) void evals_sum_kernel(long long* __restrict__ s
     if (i == 0) *nevals += t;
 }
 
-int64_t gen_bits_fused_blocks(const GenArgs& a) {
-    const int64_t waves = ((a.nc + 1) / 2 + DM_BITS_PP - 1) / DM_BITS_PP;
-    return (waves + 3) / 4;
+// 8 pairs per wave (ONE Philox call per lane draws every decision of the
+// wave: 16 children x 2 selection calls, 8 x 2 crossover calls, 16 mutation
+// flags) when t <= 4; 4 pairs per wave for 4 < t <= 8.
+static int fused_pp(const GenArgs& a) {
+    return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) && !std::getenv("DM_BITS_PP4") ? 8 : 4;
 }
 
-template <int CX, int MUT, bool EVAL, bool TOURN>
+template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 static void launch_bf(const GenArgs& a, long long* wg, hipStream_t s) {
-    gen_bits_fused_kernel<CX, MUT, EVAL, TOURN>
-        <<<dim3((unsigned)gen_bits_fused_blocks(a)), 256, 0, s>>>(a, wg);
+    const int64_t waves = ((a.nc + 1) / 2 + PP - 1) / PP;
+    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN>
+        <<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(a, wg);
 }
-template <int CX, int MUT>
+template <int PP, int CX, int MUT>
 static void launch_bf_e(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {
     const bool tourn = a.sel == DM_SEL_TOURNAMENT;
     if (eval)
-        tourn ? launch_bf<CX, MUT, true, true>(a, wg, s) : launch_bf<CX, MUT, true, false>(a, wg, s);
+        tourn ? launch_bf<PP, CX, MUT, true, true>(a, wg, s)
+              : launch_bf<PP, CX, MUT, true, false>(a, wg, s);
     else
-        tourn ? launch_bf<CX, MUT, false, true>(a, wg, s) : launch_bf<CX, MUT, false, false>(a, wg, s);
+        tourn ? launch_bf<PP, CX, MUT, false, true>(a, wg, s)
+              : launch_bf<PP, CX, MUT, false, false>(a, wg, s);
+}
+template <int PP>
+static void launch_bf_pp(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {
+    const bool mf = a.mut == DM_MUT_FLIPBIT;
+    if (a.cx == DM_CX_TWOPOINT)
+        mf ? launch_bf_e<PP, DM_CX_TWOPOINT, DM_MUT_FLIPBIT>(a, eval, wg, s)
+           : launch_bf_e<PP, DM_CX_TWOPOINT, DM_MUT_NONE>(a, eval, wg, s);
+    else
+        mf ? launch_bf_e<PP, DM_CX_NONE, DM_MUT_FLIPBIT>(a, eval, wg, s)
+           : launch_bf_e<PP, DM_CX_NONE, DM_MUT_NONE>(a, eval, wg, s);
 }
 
 // spread: the context's zeroed nevals counters, or null when nevals is not
 // counted; launch_evals_sum then folds them into a.nevals.
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s) {
-    const bool mf = a.mut == DM_MUT_FLIPBIT;
     long long* wg = (eval && a.nevals) ? spread : nullptr;
-    if (a.cx == DM_CX_TWOPOINT)
-        mf ? launch_bf_e<DM_CX_TWOPOINT, DM_MUT_FLIPBIT>(a, eval, wg, s)
-           : launch_bf_e<DM_CX_TWOPOINT, DM_MUT_NONE>(a, eval, wg, s);
+    if (fused_pp(a) == 8)
+        launch_bf_pp<8>(a, eval, wg, s);
     else
-        mf ? launch_bf_e<DM_CX_NONE, DM_MUT_FLIPBIT>(a, eval, wg, s)
-           : launch_bf_e<DM_CX_NONE, DM_MUT_NONE>(a, eval, wg, s);
+        launch_bf_pp<4>(a, eval, wg, s);
 }
 void launch_evals_sum(long long* spread, int64_t* nevals, hipStream_t s) {
     evals_sum_kernel<<<1, 64, 0, s>>>(spread, nevals);

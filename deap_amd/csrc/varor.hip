@@ -161,6 +161,8 @@ __global__ __launch_bounds__(256) void varor_float_kernel(GenArgs a, double cxpb
 
 template <int G>
 __global__ __launch_bounds__(256) void varor_bits_kernel(GenArgs a, double cxpb, double cxmutpb) {
+    __shared__ uint64_t flip_lds_all[256];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~(G - 1));
     const int lane = threadIdx.x & 63;
     const int sub = lane & (G - 1);
     const bool leader = sub == 0;
@@ -174,13 +176,19 @@ __global__ __launch_bounds__(256) void varor_bits_kernel(GenArgs a, double cxpb,
         const uint64_t* rb = reinterpret_cast<const uint64_t*>(a.pgenes + d.b * a.pstride);
         uint64_t* wc = reinterpret_cast<uint64_t*>(a.cgenes + c * a.cstride);
         int64_t pc = 0;
-        for (int wi = sub; wi < a.words64; wi += G) {
+        const bool flip = d.op == 1 && a.mut == DM_MUT_FLIPBIT;  // group-uniform
+        FlipRow<G> fr;
+        if (flip) flip_begin<G>(a, c, sub, fr);
+        for (int wb = 0; wb < a.words64; wb += G) {
+            const int wi = wb + sub;
+            const uint64_t fm = flip ? flip_mask_chunk<G, true>(a, c, wb, sub, fr, flip_lds) : 0ull;
+            if (wi >= a.words64) continue;
             uint64_t x = ra[wi];
             if (d.op == 0 && a.cx == DM_CX_TWOPOINT) {
                 const uint64_t m = range_mask(d.c1 - wi * 64, d.c2 - wi * 64);
                 x = (x & ~m) | (rb[wi] & m);
             }
-            if (d.op == 1 && a.mut == DM_MUT_FLIPBIT) x ^= flip_mask_word<true>(a, c, wi);
+            x ^= fm;
             wc[wi] = x;
             pc += __popcll(x);
         }
