@@ -166,12 +166,25 @@ class _Bookkeeping:
         self.logbook = Logbook()
         self.logbook.header = ["gen", "nevals"] + (stats.fields if stats else [])
 
+    pending_hof = None
+
+    def complete_hof(self):
+        if self.pending_hof is not None:
+            done, self.pending_hof = self.pending_hof, None
+            done()
+
     def nevals_ptr(self, gen):
         return ctypes.c_void_p(self.nevals.data_ptr() + 8 * gen)
 
-    def record(self, gen, population):
+    def record(self, gen, population, defer_hof=False):
+        """``defer_hof``: queue the HallOfFame's device work now and run its
+        host part at ``complete_hof()`` (after the next generation is queued)."""
         if self.hof is not None:
-            self.hof.update(population)
+            begin = getattr(self.hof, "update_begin", None)
+            if defer_hof and begin is not None:
+                self.pending_hof = begin(population)
+            else:
+                self.hof.update(population)
         rec = self.stats.compile(population) if self.stats else {}
         self.records.append((gen, rec))
         if self.verbose:
@@ -253,10 +266,15 @@ def eaSimple(population, toolbox, cxpb, mutpb, ngen, stats=None, halloffame=None
     book.record(0, population)
 
     offspring = population.like(len(population), capacity=population.capacity)
+    # the HallOfFame's host loop for generation g runs while generation g + 1
+    # is on the GPU (g's rows are rewritten only by generation g + 2)
+    defer = not verbose
     for gen in range(1, ngen + 1):
         step.step(population, offspring, stream, book.nevals_ptr(gen), mode, decisions, gen - 1)
+        book.complete_hof()
         population.swap_storage(offspring)                                 # :181
-        book.record(gen, population)
+        book.record(gen, population, defer_hof=defer)
+    book.complete_hof()
     return population, book.finish()
 
 

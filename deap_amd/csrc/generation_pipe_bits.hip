@@ -41,6 +41,10 @@ __device__ __forceinline__ uint64_t flip_mask_row(const GenArgs& a, int64_t c, i
 #define DM_BITS_ABLATE 0
 #endif
 
+#ifndef DM_BITS_NTLOAD
+#define DM_BITS_NTLOAD 0  // non-temporal parent-row loads in the fused kernel (A/B)
+#endif
+
 #ifndef DM_BITS_PP
 #define DM_BITS_PP 4  // pairs per wave (tools_gpu/bwtest5.hip: 2-4 best)
 #endif
@@ -140,20 +144,33 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
 // Same Philox counters as pair_plan_kernel / gen_bits_kernel: bit-identical
 // children (tests/test_gpu_parity.py::test_native_hot_kernel_equals_replay_kernel).
 // ---------------------------------------------------------------------------
-template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
-__global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long long* spread) {
-    constexpr int NCH = 2 * PP;  // children per wave
-    static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
+// Decision draws of one group (PP pairs) of a wave, before the tournament:
+// the Philox words of every lane and the aspirants' fitness loads in flight.
+struct BitsDraw {
+    int32_t k0, k1;
+    double f0, f1;
+    uint32_t cxf_l, cuts;
+    bool mut_l;
+};
+// A group after its tournament: winners, flags and parent rows in flight.
+template <int PP>
+struct BitsGroup {
+    int64_t p0;
+    int32_t s0[PP], s1[PP];
+    uint32_t cut[PP], cxf[PP];
+    uint64_t y0[PP], y1[PP];
+    uint64_t mut_bits;
+    double f;      // lane L < 2PP: child L's winner fitness (the clone's)
+    uint32_t v;    // ... its validity
+    bool cx_c, mut;
+};
+
+template <int PP, int CX, int MUT, bool TOURN>
+__device__ __forceinline__ BitsDraw bits_draw(const GenArgs& a, int64_t p0, int lane) {
+    constexpr int NCH = 2 * PP;
     constexpr int CXL = 32, MUTL = 32 + 2 * PP;  // first crossover / mutation lane
-    __shared__ uint64_t flip_lds_all[256];
-    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~63);
-    const int lane = threadIdx.x & 63;
-    const int64_t npairs = (a.nc + 1) / 2;
-    const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PP;
     const int64_t cbase = 2 * p0;
     const uint32_t np = (uint32_t)a.np;
-
-    // ---- decisions: ONE Philox call per lane covers every draw of the wave
     //   lanes 0-31: selection, child L % NCH, call L / NCH (aspirants 2call, 2call+1)
     //   lanes CXL..CXL+2PP-1: crossover of pair (L - CXL) % PP, call (L - CXL) / PP
     //   lanes MUTL..MUTL+NCH-1: mutation flag of child L - MUTL
@@ -183,45 +200,22 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
         else
             w = a.rng(stage, item, sub);
     }
-    // selection lanes: both aspirants of the call, fitness and validity
-    int32_t k0 = 0, k1 = 0;
-    double f0 = 0.0, f1 = 0.0;
-    uint32_t v0 = 0, v1 = 0;
+    BitsDraw d{};
+    // selection lanes: both aspirants of the call and their fitness
     if (draw && lane < CXL) {
-        k0 = (int32_t)bounded64(w.x, w.y, np);
-        f0 = (DM_BITS_ABLATE & 2) ? (double)(k0 & 255) : a.pwv[k0];
-        v0 = (DM_BITS_ABLATE & 2) ? 1u : a.pvalid[k0];
+        d.k0 = (int32_t)bounded64(w.x, w.y, np);
+        d.f0 = (DM_BITS_ABLATE & 2) ? (double)(d.k0 & 255) : a.pwv[d.k0];
         if (2 * (int)sub + 1 < t) {
-            k1 = (int32_t)bounded64(w.z, w.w, np);
-            f1 = (DM_BITS_ABLATE & 2) ? (double)(k1 & 255) : a.pwv[k1];
-            v1 = (DM_BITS_ABLATE & 2) ? 1u : a.pvalid[k1];
-        }
-    }
-    // tournament of child L (lanes 0-7): first-drawn wins, a later aspirant
-    // replaces only on Fitness.__gt__ (one objective: not(a <= b))
-    int32_t k = k0;
-    double f = f0;
-    uint32_t v = v0;
-    if (TOURN) {
-        for (int jj = 1; jj < t; ++jj) {
-            const int src = (jj >> 1) * NCH + (lane % NCH);
-            const double fj = __shfl((jj & 1) ? f1 : f0, src, 64);
-            const int32_t kj = __shfl((jj & 1) ? k1 : k0, src, 64);
-            const uint32_t vj = __shfl((jj & 1) ? v1 : v0, src, 64);
-            if (!(fj <= f)) {
-                f = fj;
-                k = kj;
-                v = vj;
-            }
+            d.k1 = (int32_t)bounded64(w.z, w.w, np);
+            d.f1 = (DM_BITS_ABLATE & 2) ? (double)(d.k1 & 255) : a.pwv[d.k1];
         }
     }
     // crossover lanes CXL..CXL+PP-1: flag and cxTwoPoint cuts of pair L - CXL
     // (call 1's words come from lane L + PP)
     const uint32_t w2x = (uint32_t)__shfl((int)w.x, (lane + PP) & 63, 64);
     const uint32_t w2y = (uint32_t)__shfl((int)w.y, (lane + PP) & 63, 64);
-    uint32_t cxf_l = 0, cuts = 0;
     if (draw && lane >= CXL && lane < CXL + PP && (uint64_t)w.x < a.thr_cx) {
-        cxf_l = 1;
+        d.cxf_l = 1;
         if (CX == DM_CX_TWOPOINT) {
             int32_t r1 = 1 + (int32_t)bounded64(w.z, w.w, (uint32_t)a.dim);
             int32_t r2 = 1 + (int32_t)bounded64(w2x, w2y, (uint32_t)(a.dim - 1));
@@ -232,60 +226,96 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
                 r1 = r2;
                 r2 = tt;
             }
-            cuts = (uint32_t)r1 | ((uint32_t)r2 << 16);
+            d.cuts = (uint32_t)r1 | ((uint32_t)r2 << 16);
         }
     }
-    const bool mut_l = draw && lane >= MUTL && lane < MUTL + NCH && (uint64_t)w.x < a.thr_mut;
-    // per child (lanes 0-7): its pair's crossover flag, its mutation flag
-    const int ch = lane % NCH;
-    const int64_t c = cbase + ch;
-    const bool live = lane < NCH && c < a.nc;
-    // (shuffles outside any condition: a bpermute reads 0 from inactive lanes)
-    const bool cx_c = __shfl((int)cxf_l, CXL + (ch >> 1), 64) != 0;
-    const int mut_c = __shfl((int)mut_l, MUTL + ch, 64);
-    const bool mut = live && mut_c != 0;
-    const bool inv = live && (cx_c || mut || !v);
-    const uint64_t mut_bits = __ballot(mut);
-    const uint64_t inv_bits = __ballot(inv);
+    d.mut_l = draw && lane >= MUTL && lane < MUTL + NCH && (uint64_t)w.x < a.thr_mut;
+    return d;
+}
 
-    // ---- rows: every parent row of the wave's pairs in flight first
-    const int words = a.words64;
-    const bool lw = lane < words;
-    auto row = [&](int32_t s) {
-        return reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)s * a.pstride);
-    };
-    int32_t s0[PP], s1[PP];
-    uint32_t cut[PP], cxf[PP];
-    uint64_t y0[PP], y1[PP];
+template <int PP, bool TOURN>
+__device__ __forceinline__ void bits_resolve(const GenArgs& a, const BitsDraw& d, int64_t p0,
+                                             int lane, BitsGroup<PP>& g) {
+    constexpr int NCH = 2 * PP;
+    constexpr int CXL = 32, MUTL = 32 + 2 * PP;
+    const int t = TOURN ? a.tournsize : 1;
+    // tournament of child L (lanes 0..NCH-1): first-drawn wins, a later
+    // aspirant replaces only on Fitness.__gt__ (one objective: not(a <= b))
+    int32_t k = d.k0;
+    double f = d.f0;
+    if (TOURN) {
+        for (int jj = 1; jj < t; ++jj) {
+            const int src = (jj >> 1) * NCH + (lane % NCH);
+            const double fj = __shfl((jj & 1) ? d.f1 : d.f0, src, 64);
+            const int32_t kj = __shfl((jj & 1) ? d.k1 : d.k0, src, 64);
+            if (!(fj <= f)) {
+                f = fj;
+                k = kj;
+            }
+        }
+    }
+    // per child (lanes 0..NCH-1): its pair's crossover flag, its mutation flag
+    // (shuffles outside any condition: a bpermute reads 0 from inactive lanes)
+    const int ch = lane % NCH;
+    const bool live = lane < NCH && 2 * p0 + ch < a.nc;
+    g.p0 = p0;
+    g.f = f;
+    g.cx_c = __shfl((int)d.cxf_l, CXL + (ch >> 1), 64) != 0;
+    const int mut_c = __shfl((int)d.mut_l, MUTL + ch, 64);
+    g.mut = live && mut_c != 0;
+    g.mut_bits = __ballot(g.mut);
+    // the winner's validity is only needed for the fitness store: loaded with
+    // the rows, off the decision chain (one random byte per child, not t)
+    g.v = 1;
+    if (live && !(g.cx_c || g.mut)) g.v = a.pvalid[k];
+    const int64_t npairs = (a.nc + 1) / 2;
+    const bool lw = lane < a.words64;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-        s0[q] = __builtin_amdgcn_readlane(k, 2 * q);
-        s1[q] = __builtin_amdgcn_readlane(k, 2 * q + 1);
-        cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)cuts, CXL + q);
-        cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)cxf_l, CXL + q);
-        y0[q] = 0;
-        y1[q] = 0;
+        g.s0[q] = __builtin_amdgcn_readlane(k, 2 * q);
+        g.s1[q] = __builtin_amdgcn_readlane(k, 2 * q + 1);
+        g.cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)d.cuts, CXL + q);
+        g.cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)d.cxf_l, CXL + q);
+        g.y0[q] = 0;
+        g.y1[q] = 0;
         if (lw && p0 + q < npairs) {
-            y0[q] = row(s0[q])[lane];
-            if (2 * (p0 + q) + 1 < a.nc) y1[q] = row(s1[q])[lane];
+            const uint64_t* r0 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s0[q] * a.pstride);
+            const uint64_t* r1 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s1[q] * a.pstride);
+#if DM_BITS_NTLOAD
+            g.y0[q] = __builtin_nontemporal_load(r0 + lane);
+            if (2 * (p0 + q) + 1 < a.nc) g.y1[q] = __builtin_nontemporal_load(r1 + lane);
+#else
+            g.y0[q] = r0[lane];
+            if (2 * (p0 + q) + 1 < a.nc) g.y1[q] = r1[lane];
+#endif
         }
     }
+}
+
+// Vary, store and evaluate the group's children; returns how many fitnesses
+// were invalidated (nevals).
+template <int PP, int CX, int MUT, bool EVAL>
+__device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, int lane,
+                                           uint64_t* flip_lds) {
+    constexpr int NCH = 2 * PP;
+    const int64_t npairs = (a.nc + 1) / 2;
+    const bool lw = lane < a.words64;
     uint32_t my_count = 0;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-        const int64_t pq = p0 + q;
+        const int64_t pq = g.p0 + q;
         if (pq >= npairs) break;
         const int64_t c0 = 2 * pq, c1 = 2 * pq + 1;
         const bool h1 = c1 < a.nc;
-        uint64_t x0 = y0[q], x1 = y1[q];
+        uint64_t x0 = g.y0[q], x1 = g.y1[q];
         uint64_t f0 = 0, f1 = 0;  // flip masks, drawn by the whole wave per row
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1)) {
-            if ((mut_bits >> (2 * q)) & 1) f0 = flip_mask_row(a, c0, lane, flip_lds);
-            if ((mut_bits >> (2 * q + 1)) & 1) f1 = flip_mask_row(a, c1, lane, flip_lds);
+            if ((g.mut_bits >> (2 * q)) & 1) f0 = flip_mask_row(a, c0, lane, flip_lds);
+            if ((g.mut_bits >> (2 * q + 1)) & 1) f1 = flip_mask_row(a, c1, lane, flip_lds);
         }
         if (lw) {
-            if (CX == DM_CX_TWOPOINT && cxf[q]) {
-                const int cp1 = (int)(cut[q] & 0xFFFFu), cp2 = (int)(cut[q] >> 16);
+            if (CX == DM_CX_TWOPOINT && g.cxf[q]) {
+                const int cp1 = (int)(g.cut[q] & 0xFFFFu), cp2 = (int)(g.cut[q] >> 16);
                 const uint64_t m = range_mask(cp1 - lane * 64, cp2 - lane * 64);
                 const uint64_t tt = (x0 ^ x1) & m;
                 x0 ^= tt;
@@ -305,14 +335,61 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
             if ((lane >> 1) == q) my_count = (lane & 1) ? (pc >> 16) : (pc & 0xFFFFu);
         }
     }
-    // ---- fitness / validity of the wave's 8 children (contiguous stores)
+    // fitness / validity of the group's children (contiguous stores)
+    const int64_t c = 2 * g.p0 + (lane % NCH);
+    const bool live = lane < NCH && c < a.nc;
+    const bool inv = live && (g.cx_c || g.mut || !g.v);
     if (live) {
         if (EVAL) {
-            a.cwv[c] = inv ? (double)my_count * a.w0 : f;
+            a.cwv[c] = inv ? (double)my_count * a.w0 : g.f;
             a.cvalid[c] = 1;
         } else {  // no evaluation requested: clones keep their fitness
-            a.cwv[c] = f;
+            a.cwv[c] = g.f;
             a.cvalid[c] = inv ? 0 : 1;
+        }
+    }
+    return __popcll(__ballot(inv));
+}
+
+#ifndef DM_BITS_MINW
+#define DM_BITS_MINW 1  // minimum waves per SIMD the fused kernel is compiled for (A/B)
+#endif
+
+template <int PP, int CX, int MUT, bool EVAL, bool TOURN, bool PERSIST>
+__global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenArgs a,
+                                                                           long long* spread) {
+    static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
+    __shared__ uint64_t flip_lds_all[256];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~63);
+    const int lane = threadIdx.x & 63;
+    const int64_t npairs = (a.nc + 1) / 2;
+    const int64_t ngroups = (npairs + PP - 1) / PP;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int evals = 0;
+    if (!PERSIST && grp < ngroups) {  // one group per wave
+        BitsGroup<PP> g;
+        const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
+        bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
+        evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
+    } else if (PERSIST && grp < ngroups) {
+        // software pipeline over the wave's groups (one group when the grid
+        // covers them all): the next group's Philox draws and fitness loads
+        // are issued while this group's parent rows are in flight
+        BitsGroup<PP> g;
+        {
+            const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
+            bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
+        }
+        while (true) {
+            const int64_t nxt = grp + nw;
+            const bool more = nxt < ngroups;
+            BitsDraw dn{};
+            if (more) dn = bits_draw<PP, CX, MUT, TOURN>(a, nxt * PP, lane);
+            evals += bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
+            if (!more) break;
+            bits_resolve<PP, TOURN>(a, dn, nxt * PP, lane, g);
+            grp = nxt;
         }
     }
     if (EVAL && spread) {
@@ -320,7 +397,7 @@ __global__ __launch_bounds__(256) void gen_bits_fused_kernel(GenArgs a, long lon
         // same-address atomics per C2 generation serialised at one L2 channel
         // and cost 0.19 ms); evals_sum_kernel folds them into nevals
         __shared__ int32_t wave_evals[4];
-        if (lane == 0) wave_evals[threadIdx.x >> 6] = __popcll(inv_bits);
+        if (lane == 0) wave_evals[threadIdx.x >> 6] = evals;
         __syncthreads();
         if (threadIdx.x == 0) {
             const int tot = wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
@@ -352,11 +429,24 @@ static int fused_pp(const GenArgs& a) {
     return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) && !std::getenv("DM_BITS_PP4") ? 8 : 4;
 }
 
+// Grid: one wave per group (one-shot) unless DM_BITS_BPC caps the
+// workgroups per CU (persistent, software-pipelined).
 template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 static void launch_bf(const GenArgs& a, long long* wg, hipStream_t s) {
     const int64_t waves = ((a.nc + 1) / 2 + PP - 1) / PP;
-    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN>
-        <<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(a, wg);
+    int64_t blocks = (waves + 3) / 4;
+    static const int bpc = std::getenv("DM_BITS_BPC") ? std::max(1, atoi(std::getenv("DM_BITS_BPC"))) : 0;
+    if (bpc) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        blocks = std::min<int64_t>(blocks, (int64_t)cus * bpc);
+        gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, true>
+            <<<dim3((unsigned)blocks), 256, 0, s>>>(a, wg);
+        return;
+    }
+    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, false>
+        <<<dim3((unsigned)blocks), 256, 0, s>>>(a, wg);
 }
 template <int PP, int CX, int MUT>
 static void launch_bf_e(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {

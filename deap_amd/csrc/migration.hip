@@ -199,8 +199,37 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
     __shared__ int32_t placed_slot[4096];
     __shared__ int32_t placed_em[4096];
     __shared__ int nplaced;
-    if (threadIdx.x == 0) nplaced = 0;
+    __shared__ int fast;
+    if (threadIdx.x == 0) {
+        nplaced = 0;
+        fast = 1;
+    }
     __syncthreads();
+    // Fast path: when every immigrant has a first match, the first matches
+    // are pairwise distinct and no emigrant equals any immigrant, no
+    // placement can change another immigrant's match, so the sequential loop
+    // below would write emigrant j into first[j] for every j: do the k row
+    // copies in parallel (one wave per row).
+    for (int64_t t = threadIdx.x; t < k * k; t += blockDim.x) {
+        const int64_t e = t / k, j = t % k;
+        if (E[t] || first[j] >= n || (e < j && first[e] == first[j])) fast = 0;
+    }
+    __syncthreads();
+    if (fast) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+        for (int64_t j = wave; j < k; j += nwave) {
+            const int64_t slot = first[j];
+            const uint4* src = reinterpret_cast<const uint4*>(em.genes + j * stride);
+            uint4* dst = reinterpret_cast<uint4*>(genes + slot * stride);
+            for (int64_t i = lane; i < stride / 16; i += 64) dst[i] = src[i];
+            if (lane < nobj) wv[slot * nobj + lane] = em.wv[j * nobj + lane];
+            if (lane == 0) {
+                valid[slot] = em.valid[j];
+                slots[j] = (int32_t)slot;
+            }
+        }
+        return;
+    }
     for (int64_t j = 0; j < k; ++j) {
         if (threadIdx.x == 0) best = INT64_MAX;
         __syncthreads();

@@ -162,6 +162,12 @@ class DevicePopulation:
             raise ValueError("resize beyond capacity %d" % self.capacity)
         self.n = int(n)
 
+    def view(self):
+        """A second handle on the current buffers: later ``swap_storage`` calls
+        on this population do not move the view."""
+        import copy
+        return copy.copy(self)
+
     def like(self, n=None, capacity=None):
         """Empty population with the same layout."""
         n = self.n if n is None else n

@@ -350,32 +350,95 @@ class HallOfFame:
         are never similar and -0.0 == 0.0, as list / array equality of
         separate objects behaves), and host individuals are built only for
         the rows that enter the hall."""
-        from .selection import selBest
-        n = len(pop)
-        K = min(n, max(4 * self.maxsize, 64))
+        K = min(len(pop), max(4 * self.maxsize, 64))
         while True:
-            order = selBest(pop, K).cpu().tolist()
-            trial = copy.copy(self)
-            trial.keys, trial.items = list(self.keys), list(self.items)
-            trial._garr = dict(self._garr_cache())
-            rows = sorted(set(order) | ({0} if len(self) == 0 else set()))
-            genes, wv, ok = pop.rows_numpy(rows)
-            fits = []
-            for r in range(len(rows)):
-                f = _host_fitness(pop.weights)
-                if ok[r]:
-                    f.wvalues = tuple(float(x) for x in wv[r])
-                fits.append(f)
-            trial._loop_rows(pop, rows, genes, wv, ok, fits)
-            if K >= n:
-                break
+            if self._try_candidates(pop, K, *self._fetch_candidates(pop, K)()):
+                return
+            K = min(len(pop), 4 * K)
+
+    def _fetch_candidates(self, pop, K):
+        """Device part of one candidate round: selBest(K) and the gather of
+        those rows (and row 0), copied to pinned host memory asynchronously.
+        Returns a callable that waits for the copies (only them: work queued
+        on the stream after this call is not waited for) and yields
+        (order, rows, genes, wvalues, valid) for _try_candidates."""
+        import torch
+        from .selection import selBest
+        order = selBest(pop, K).to(torch.int64)
+        idx = torch.cat([order, torch.zeros(1, dtype=torch.int64, device=order.device)])
+        dev = (pop.genes_view()[idx], pop.wvalues[: len(pop)][idx], pop.valid[: len(pop)][idx])
+        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (idx,) + dev]
+        for h, t in zip(host, (idx,) + dev):
+            h.copy_(t, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+
+        def wait():
+            done.synchronize()
+            o, g, w, v = (h.numpy() for h in host)
+            return o, g, w, v
+        return wait
+
+    def _try_candidates(self, pop, K, idx, graw, wv, valid):
+        """One round of the candidate loop over the gathered rows; commits and
+        returns True when accepted (see _update_candidates)."""
+        from ..device import unpack_bits
+        from .. import _lib
+        n = len(pop)
+        order = idx[:-1].tolist()
+        pos = {int(r): i for i, r in enumerate(idx.tolist())}  # row -> gathered position
+        rows = sorted(set(order) | ({0} if len(self) == 0 else set()))
+        sel = np.array([pos[r] for r in rows], dtype=np.int64)
+        genes = graw[sel]
+        if pop.gtype == _lib.DM_BITS:
+            genes = unpack_bits(genes.view(np.uint64), pop.dim)
+        genes = np.ascontiguousarray(genes)
+        wv, ok = wv[sel].copy(), valid[sel].astype(bool)
+        trial = copy.copy(self)
+        trial.keys, trial.items = list(self.keys), list(self.items)
+        trial._garr = dict(self._garr_cache())
+        fits = []
+        for r in range(len(rows)):
+            f = _host_fitness(pop.weights)
+            if ok[r]:
+                f.wvalues = tuple(float(x) for x in wv[r])
+            fits.append(f)
+        trial._loop_rows(pop, rows, genes, wv, ok, fits)
+        if K < n:
             t = fits[rows.index(order[-1])]
-            if len(trial) == self.maxsize and trial[-1].fitness > t:
-                break
-            K = min(n, 4 * K)
+            if not (len(trial) == self.maxsize and trial[-1].fitness > t):
+                return False
         self.keys, self.items = trial.keys, trial.items
         self._garr = {id(it): trial._garr[id(it)] for it in self.items
                       if trial._garr.get(id(it), (None,))[0] is it}
+        return True
+
+    def update_begin(self, population):
+        """``update(population)`` split in two for a generation loop: the
+        device work is queued now and the host part runs in the returned
+        callable, which a driver calls after queueing the next generation so
+        the host loop overlaps that generation's kernel.  ``population``'s
+        rows must stay unchanged until the callable returns (eaSimple's
+        parent buffer is rewritten two generations later)."""
+        from ..device import DevicePopulation
+        if not (isinstance(population, DevicePopulation) and self.similar in _VALUE_SIMILAR
+                and len(population) and self.maxsize):
+            self.update(population)
+            return lambda: None
+        view = population.view()
+        K = min(len(view), max(4 * self.maxsize, 64))
+        fetched = self._fetch_candidates(view, K)
+
+        def complete():
+            if not self._try_candidates(view, K, *fetched()):
+                self._update_candidates_from(view, min(len(view), 4 * K))
+        return complete
+
+    def _update_candidates_from(self, pop, K):
+        while True:
+            if self._try_candidates(pop, K, *self._fetch_candidates(pop, K)()):
+                return
+            K = min(len(pop), 4 * K)
 
     def _garr_cache(self):
         cache = getattr(self, "_garr", None)
