@@ -244,7 +244,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(args.config),
-                "kernel": "gen_bits_burst_kernel" if gtype == "bits" else "gen_pipe_kernel",
+                "kernel": "gen_bits_fused_kernel" if gtype == "bits" else "gen_pipe_kernel",
                 "kernel_ms": round(kern_ms, 4), "bytes_per_ind_gen": bpi}
     workload = {"c3": "C3 Rastrigin-1000D fp64 eaSimple",
                 "c3r": "C3 Rosenbrock-1000D fp64 eaSimple",

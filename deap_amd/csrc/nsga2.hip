@@ -674,7 +674,7 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
     Weights wt{};
     for (int o = 0; o < m; ++o) wt.w[o] = weights[o];
     char* base = (char*)scratch(ctx, 2 * align_up((size_t)T * 8, 256) +
-                                         3 * align_up((size_t)T * 4, 256) +
+                                         4 * align_up((size_t)T * 4, 256) +
                                          radix_sort_temp_bytes(T) + 4096);
     if (!base) return DM_ERR_NOMEM;
     Bump bp{base};
@@ -683,22 +683,27 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
     int32_t* pos = bp.take<int32_t>(T);
     int32_t* vtmp = bp.take<int32_t>(T);
     int32_t* fid = bp.take<int32_t>(T);
+    int32_t* fpos = bp.take<int32_t>(T);
     void* rtemp = bp.take<char>(radix_sort_temp_bytes(T));
     front_id_kernel<<<g1(T), 256, 0, s>>>(fstart_dev, nfronts, T, fid);
     crowd_init_kernel<<<g1(T), 256, 0, s>>>(order, T, crowd);
     int fbits = 8;
     while (fbits < 32 && (1ll << fbits) <= nfronts) fbits += 8;
+    // The reference sorts one `crowd` list by objective 0, then 1, ...
+    // (emo.py:131-133, stable): the order for objective i is the previous
+    // one stably sorted by v_i, i.e. lexicographic in (v_i, ..., v_0,
+    // position) — one 64-bit sort per objective carried over; the grouping
+    // by front (a stable sort by front id) works on a copy.
+    iota32_kernel<<<g1(T), 256, 0, s>>>(pos, T);
     for (int i = 0; i < m; ++i) {
-        iota32_kernel<<<g1(T), 256, 0, s>>>(pos, T);
-        for (int o = 0; o <= i; ++o) {  // stable sorts by v_0, v_1, ..., v_i
-            crowd_key_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, o, wt, order, pos, keys, T);
-            int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, 64, rtemp);
-            if (rc) return rc;
-        }
-        fid_key_kernel<<<g1(T), 256, 0, s>>>(fid, pos, keys, T);
-        int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, fbits, rtemp);
+        crowd_key_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, keys, T);
+        int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, 64, rtemp);
         if (rc) return rc;
-        crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
+        DM_HIP(hipMemcpyAsync(fpos, pos, (size_t)T * 4, hipMemcpyDeviceToDevice, s));
+        fid_key_kernel<<<g1(T), 256, 0, s>>>(fid, fpos, keys, T);
+        rc = radix_sort_pairs(s, keys, fpos, ktmp, vtmp, T, 0, fbits, rtemp);
+        if (rc) return rc;
+        crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, fpos, fid,
                                                   fstart_dev, T, crowd);
     }
     DM_LAUNCH_CHECK();

@@ -217,3 +217,50 @@ def test_sel_best_topk_path_matches_stable_sort(gpu, n, k):
     wv2 = rng.normal(size=(n, 1))
     pop2 = _dp().from_numpy(np.zeros((n, 1)), weights=(-1.0,), wvalues=wv2, valid=np.ones(n))
     assert tools.selBest(pop2, k).cpu().numpy().tolist() == ops.sel_best(wv2, k).tolist()
+
+
+@pytest.mark.parametrize("gt,dim,maxsize", [("bits", 64, 5), ("f64", 30, 12)])
+def test_ea_simple_deferred_hall_of_fame_equals_reference_loop(gpu, gt, dim, maxsize):
+    """eaSimple runs each generation's HallOfFame host loop while the next
+    generation is on the GPU (update_begin / complete).  The hall it leaves is
+    the one the reference loop (support.py:528-548) builds when it walks every
+    individual of every generation on the host — small genomes so that
+    duplicates (clones of the best) are frequent."""
+    import operator
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    tb = base.Toolbox()
+    if gt == "bits":
+        tb.register("evaluate", benchmarks.onemax)
+        tb.register("mate", tools.cxTwoPoint)
+        tb.register("mutate", tools.mutFlipBit, indpb=0.02)
+        low, high, w = 0, 1, (1.0,)
+    else:
+        tb.register("evaluate", benchmarks.sphere)
+        tb.register("mate", tools.cxBlend, alpha=0.5)
+        tb.register("mutate", tools.mutGaussian, mu=0, sigma=0.3, indpb=0.05)
+        low, high, w = -1.0, 1.0, (-1.0,)
+    tb.register("select", tools.selTournament, tournsize=3)
+    st = RandomStream(11)
+    pop = tools.initPopulation(n=3001, dim=dim, low=low, high=high, gtype=gt, weights=w,
+                               stream=st)
+    snaps = []
+
+    class Recorder(tools.HallOfFame):
+        # the deferred hall, plus a host copy of every population it is given
+        def update_begin(self, population):
+            snaps.append(population.to_individuals())
+            return super().update_begin(population)
+
+        def update(self, population):
+            snaps.append(population.to_individuals())
+            return super().update(population)
+
+    hof = Recorder(maxsize)
+    algorithms.eaSimple(pop, tb, 0.5, 0.2, 6, halloffame=hof, verbose=False, stream=st)
+    ref = tools.HallOfFame(maxsize, similar=operator.eq)
+    for inds in snaps:
+        ref.update(inds)        # the reference loop over host individuals
+    assert len(snaps) == 7
+    assert [list(h) for h in hof] == [list(h) for h in ref]
+    assert [h.fitness.wvalues for h in hof] == [h.fitness.wvalues for h in ref]
