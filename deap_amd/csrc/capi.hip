@@ -430,7 +430,7 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
         delete c;
         return DM_ERR_HIP;
     }
-    const size_t spread = sizeof(long long) * kEvalSpread * kEvalSpreadStride;
+    const size_t spread = sizeof(long long) * kEvalSpreadWords;
     if (hipMalloc(&c->evals_spread, spread) != hipSuccess ||
         hipMemset(c->evals_spread, 0, spread) != hipSuccess) {
         set_error("counter allocation failed");

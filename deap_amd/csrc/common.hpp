@@ -43,6 +43,9 @@ void set_error(const char* fmt, ...);
 
 // Opaque context: one device, one stream, grow-only scratch arena.
 constexpr int kEvalSpread = 64, kEvalSpreadStride = 16;  // counters, int64 stride
+// evals_spread layout (int64 words): count[g] at g*16, ticket[g] at (64+g)*16,
+// the total at 128*16 and its ticket at 129*16 (g < kEvalSpread)
+constexpr int kEvalSpreadWords = (2 * kEvalSpread + 2) * kEvalSpreadStride;
 struct dm_ctx {
     static constexpr int kSlots = 5;
     int device = 0;
@@ -53,9 +56,9 @@ struct dm_ctx {
     size_t pinned_bytes = 0;
     int num_cus = 256;
     double* zig = nullptr;  // ziggurat tables (device), see zig_normal
-    // 64 nevals partial counters, 128 B apart (kEvalSpread), zero between
-    // uses: the packed-bit hot kernel adds per-workgroup counts, a one-wave
-    // kernel moves their sum into nevals and re-zeroes them
+    // nevals counters (kEvalSpreadWords, zero between launches; see
+    // evals_fold): a kernel's workgroups add their counts to 64 counters 128 B
+    // apart, the last workgroup of the launch adds the total to nevals
     long long* evals_spread = nullptr;
     // Hot-kernel timing (dm_ctx_set_timing): HIP event pairs recorded on the
     // launch stream around each generation kernel, for bench.py's roofline.
@@ -64,6 +67,45 @@ struct dm_ctx {
 };
 
 namespace dm {
+// Called by ONE thread of every workgroup of a launch (all of them, count 0
+// included) with the workgroup's count: adds it into counter blockIdx % 64,
+// and the workgroup that completes the launch adds the total to *nevals and
+// leaves every counter at zero.  Same-address atomics stay bounded (one
+// atomic per workgroup into ONE address serialised at one L2 channel: 0.19
+// ms per C2 generation).  Ordering uses returning atomics and a vmcnt wait
+// (each is performed before the next issues), never a fence: an agent-scope
+// release writes the L2 back and cost 0.7 ms per C2 launch.
+__device__ __forceinline__ unsigned long long atomic_add_ret(unsigned long long* p,
+                                                            unsigned long long v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long atomic_exch_ret(unsigned long long* p,
+                                                             unsigned long long v) {
+    return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void evals_fold(long long* spread, int64_t* nevals, long long count) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(spread);
+    const unsigned nb = gridDim.x;
+    const unsigned g = blockIdx.x % kEvalSpread;
+    const unsigned gsize = nb / kEvalSpread + (g < nb % kEvalSpread ? 1u : 0u);
+    // each atomic is performed (returned) before the next issues
+    atomic_add_ret(w + g * kEvalSpreadStride, (unsigned long long)count);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long tk = atomic_add_ret(w + (kEvalSpread + g) * kEvalSpreadStride, 1ull);
+    if (tk != gsize - 1) return;
+    // last workgroup of group g: every count of the group is in
+    const unsigned long long gt = atomic_exch_ret(w + g * kEvalSpreadStride, 0ull);
+    atomic_exch_ret(w + (kEvalSpread + g) * kEvalSpreadStride, 0ull);
+    atomic_add_ret(w + 2 * kEvalSpread * kEvalSpreadStride, gt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned ngroups = nb < (unsigned)kEvalSpread ? nb : (unsigned)kEvalSpread;
+    const unsigned long long tt = atomic_add_ret(w + (2 * kEvalSpread + 1) * kEvalSpreadStride, 1ull);
+    if (tt != ngroups - 1) return;
+    const unsigned long long tot = atomic_exch_ret(w + 2 * kEvalSpread * kEvalSpreadStride, 0ull);
+    atomic_exch_ret(w + (2 * kEvalSpread + 1) * kEvalSpreadStride, 0ull);
+    *nevals += (int64_t)tot;
+}
+
 // Event pair i around the next generation-kernel launch (no-op when timing is
 // off or every pair has been used).
 inline void timing_begin(dm_ctx* ctx) {

@@ -124,10 +124,6 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         const bool count = ec != EC_NONE && a.nevals;
         launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
-        if (count) {
-            launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
-            DM_LAUNCH_CHECK();
-        }
         PipeArgs q{};
         q.pgenes = a.pgenes;
         q.cgenes = a.cgenes;
@@ -175,10 +171,6 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                                   ctx->stream);
             timing_end(ctx);
             DM_LAUNCH_CHECK();
-            if (count) {
-                launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
-                DM_LAUNCH_CHECK();
-            }
             return DM_OK;
         }
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
@@ -186,10 +178,6 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         const bool count = ec != EC_NONE && a.nevals;
         launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         DM_LAUNCH_CHECK();
-        if (count) {
-            launch_evals_sum(ctx->evals_spread, a.nevals, ctx->stream);
-            DM_LAUNCH_CHECK();
-        }
         timing_begin(ctx);
         launch_gen_bits_pipe(a, plans, ec != EC_NONE, ctx->num_cus, ctx->stream);
         timing_end(ctx);

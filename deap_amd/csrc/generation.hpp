@@ -508,6 +508,27 @@ __device__ __forceinline__ void flip_begin(const GenArgs& a, int64_t c, int sub,
     if (a.thr_ind > 0 && a.thr_ind < (1ull << 32)) flip_round<G>(a, c, sub, -1, st);
 }
 
+// Flip bits of chunk [64 wb, 64 (wb + G)) of child c's row ORed into the G
+// LDS words `lds` (zeroed first); 0 < indpb < 1.
+template <int G>
+__device__ __forceinline__ void flip_chunk_lds(const GenArgs& a, int64_t c, int wb, int sub,
+                                               FlipRow<G>& st, uint64_t* lds) {
+    const int32_t lo = wb * 64;
+    const int32_t hi = min(a.dim, (wb + G) * 64);
+    lds[sub] = 0;
+    __builtin_amdgcn_wave_barrier();
+    while (true) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t q = st.pos[j];
+            if (q >= lo && q < hi) atomicOr((unsigned long long*)&lds[(q - lo) >> 6], 1ull << (q & 63));
+        }
+        if (st.last >= hi) break;  // the round reaches the next chunk (kept)
+        st.round += 1;
+        flip_round<G>(a, c, sub, st.last, st);
+    }
+}
+
 // The flip mask of word wb + sub of child c (chunk [64 wb, 64 (wb + G)) of the
 // row); called by every lane of the group, chunks in ascending order.
 // `lds`: this group's G words.  Inject / dump as the replay modes need.
@@ -522,20 +543,7 @@ __device__ __forceinline__ uint64_t flip_mask_chunk(const GenArgs& a, int64_t c,
         const int nbits = min(64, a.dim - wi * 64);
         mask = !in ? 0ull : nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
     } else if (a.thr_ind > 0) {
-        const int32_t lo = wb * 64;
-        const int32_t hi = min(a.dim, (wb + G) * 64);
-        lds[sub] = 0;
-        __builtin_amdgcn_wave_barrier();
-        while (true) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int32_t q = st.pos[j];
-                if (q >= lo && q < hi) atomicOr((unsigned long long*)&lds[(q - lo) >> 6], 1ull << (q & 63));
-            }
-            if (st.last >= hi) break;  // the round reaches the next chunk (kept)
-            st.round += 1;
-            flip_round<G>(a, c, sub, st.last, st);
-        }
+        flip_chunk_lds<G>(a, c, wb, sub, st, lds);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         mask = lds[sub];

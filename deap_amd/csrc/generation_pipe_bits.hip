@@ -34,6 +34,35 @@ __device__ __forceinline__ uint64_t flip_mask_row(const GenArgs& a, int64_t c, i
     return flip_mask_chunk<64, false>(a, c, 0, lane, st, lds);
 }
 
+// The flip masks of every mutated child of a group (bit c of `mut_bits` =
+// child 2 p0 + c) into that child's 64 LDS words: issued right after the
+// group's row loads, so this VALU / LDS work overlaps their latency.
+// Slots of 64 LDS words per wave for precomputed flip masks (children ranked
+// by index among the group's mutated ones; P(more than 6 of 16) = 2.7 % at
+// mutpb 0.2) plus one scratch slot for the rest, computed in bits_finish.
+constexpr int FLIP_SLOTS = 6;
+
+template <int NCH>
+__device__ __forceinline__ void flip_rows_to_lds(const GenArgs& a, int64_t cbase, uint64_t mut_bits,
+                                                 int lane, uint64_t* lds) {
+    if (a.thr_ind == 0) return;
+    int slot = 0;
+    for (uint64_t mb = mut_bits; mb && slot < FLIP_SLOTS; mb &= mb - 1, ++slot) {  // wave-uniform
+        const int ch = __ffsll((long long)mb) - 1;
+        uint64_t* w = lds + slot * 64;
+        if (a.thr_ind >= (1ull << 32)) {
+            const int nbits = min(64, a.dim - lane * 64);
+            w[lane] = lane >= a.words64 ? 0ull : nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
+            continue;
+        }
+        FlipRow<64> st;
+        flip_begin<64>(a, cbase + ch, lane, st);
+        flip_chunk_lds<64>(a, cbase + ch, 0, lane, st, w);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Profiling-only ablations of the fused kernel (product build: 0): bit 0
 // skips the mutFlipBit masks, bit 1 the aspirants' fitness loads, bit 2 the
 // Philox evaluation of the decisions.
@@ -308,10 +337,16 @@ __device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, i
         const int64_t c0 = 2 * pq, c1 = 2 * pq + 1;
         const bool h1 = c1 < a.nc;
         uint64_t x0 = g.y0[q], x1 = g.y1[q];
-        uint64_t f0 = 0, f1 = 0;  // flip masks, drawn by the whole wave per row
+        uint64_t f0 = 0, f1 = 0;  // flip masks: precomputed slot, or drawn now
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1)) {
-            if ((g.mut_bits >> (2 * q)) & 1) f0 = flip_mask_row(a, c0, lane, flip_lds);
-            if ((g.mut_bits >> (2 * q + 1)) & 1) f1 = flip_mask_row(a, c1, lane, flip_lds);
+            const uint64_t below = g.mut_bits & ((1ull << (2 * q)) - 1);
+            const int r0 = __popcll(below), r1 = r0 + (int)((g.mut_bits >> (2 * q)) & 1);
+            if ((g.mut_bits >> (2 * q)) & 1)
+                f0 = r0 < FLIP_SLOTS ? flip_lds[r0 * 64 + lane]
+                                     : flip_mask_row(a, c0, lane, flip_lds + FLIP_SLOTS * 64);
+            if ((g.mut_bits >> (2 * q + 1)) & 1)
+                f1 = r1 < FLIP_SLOTS ? flip_lds[r1 * 64 + lane]
+                                     : flip_mask_row(a, c1, lane, flip_lds + FLIP_SLOTS * 64);
         }
         if (lw) {
             if (CX == DM_CX_TWOPOINT && g.cxf[q]) {
@@ -359,8 +394,9 @@ template <int PP, int CX, int MUT, bool EVAL, bool TOURN, bool PERSIST>
 __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenArgs a,
                                                                            long long* spread) {
     static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
-    __shared__ uint64_t flip_lds_all[256];
-    uint64_t* flip_lds = flip_lds_all + (threadIdx.x & ~63);
+    // FLIP_SLOTS + 1 flip-mask rows of 64 words per wave (3.5 KiB)
+    __shared__ uint64_t flip_lds_all[4 * (FLIP_SLOTS + 1) * 64];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x >> 6) * ((FLIP_SLOTS + 1) * 64);
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t ngroups = (npairs + PP - 1) / PP;
@@ -371,6 +407,8 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
         BitsGroup<PP> g;
         const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
         bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
+        if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
+            flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
         evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
     } else if (PERSIST && grp < ngroups) {
         // software pipeline over the wave's groups (one group when the grid
@@ -386,41 +424,24 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
             const bool more = nxt < ngroups;
             BitsDraw dn{};
             if (more) dn = bits_draw<PP, CX, MUT, TOURN>(a, nxt * PP, lane);
+            if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
+                flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
             evals += bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
             if (!more) break;
             bits_resolve<PP, TOURN>(a, dn, nxt * PP, lane, g);
             grp = nxt;
         }
     }
-    if (EVAL && spread) {
-        // per-workgroup count into one of kEvalSpread counters (2^15
-        // same-address atomics per C2 generation serialised at one L2 channel
-        // and cost 0.19 ms); evals_sum_kernel folds them into nevals
+    if (EVAL && spread) {  // nevals: workgroup count, folded by the last workgroup
         __shared__ int32_t wave_evals[4];
         if (lane == 0) wave_evals[threadIdx.x >> 6] = evals;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const int tot = wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
-            if (tot)
-                atomicAdd((unsigned long long*)(spread + (blockIdx.x % kEvalSpread) * kEvalSpreadStride),
-                          (unsigned long long)tot);
-        }
+        if (threadIdx.x == 0)
+            evals_fold(spread, a.nevals,
+                       (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
     }
 }
 
-// *nevals += sum of the spread counters, which are re-zeroed (one wave).
-__global__ __launch_bounds__(64) void evals_sum_kernel(long long* __restrict__ spread,
-                                                       int64_t* __restrict__ nevals) {
-    const int i = threadIdx.x;
-    long long t = 0;
-    if (i < kEvalSpread) {
-        t = spread[i * kEvalSpreadStride];
-        spread[i * kEvalSpreadStride] = 0;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (i == 0) *nevals += t;
-}
 
 // 8 pairs per wave (ONE Philox call per lane draws every decision of the
 // wave: 16 children x 2 selection calls, 8 x 2 crossover calls, 16 mutation
@@ -470,16 +491,13 @@ static void launch_bf_pp(const GenArgs& a, bool eval, long long* wg, hipStream_t
 }
 
 // spread: the context's zeroed nevals counters, or null when nevals is not
-// counted; launch_evals_sum then folds them into a.nevals.
+// counted (the kernel's last workgroup adds the total to a.nevals).
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s) {
     long long* wg = (eval && a.nevals) ? spread : nullptr;
     if (fused_pp(a) == 8)
         launch_bf_pp<8>(a, eval, wg, s);
     else
         launch_bf_pp<4>(a, eval, wg, s);
-}
-void launch_evals_sum(long long* spread, int64_t* nevals, hipStream_t s) {
-    evals_sum_kernel<<<1, 64, 0, s>>>(spread, nevals);
 }
 
 template <int CX, int MUT, bool EVAL>

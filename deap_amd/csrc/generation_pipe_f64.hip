@@ -75,11 +75,10 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     return fl;
 }
 
-// With count_evals set (the context's spread counters, kEvalSpread of them),
-// the plan kernel also counts the generation's `nevals` (children whose
-// fitness is invalidated, algorithms.py:171-174): one ballot per wave, one
-// atomic per workgroup into counter blockIdx % kEvalSpread; launch_evals_sum
-// folds them into nevals.
+// With count_evals set (the context's spread counters), the plan kernel also
+// counts the generation's `nevals` (children whose fitness is invalidated,
+// algorithms.py:171-174) into a.nevals: one ballot per wave, evals_fold per
+// workgroup.
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
                                                         long long* __restrict__ count_evals) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -92,13 +91,9 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const int64_t t = (int64_t)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3];
-            if (t)
-                atomicAdd((unsigned long long*)(count_evals +
-                                                (blockIdx.x % kEvalSpread) * kEvalSpreadStride),
-                          (unsigned long long)t);
-        }
+        if (threadIdx.x == 0)
+            evals_fold(count_evals, a.nevals,
+                       (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
     if (p < npairs) plan_one(a, plans, p);
