@@ -385,11 +385,24 @@ __global__ __launch_bounds__(256) void stats_kernel(const double* wv, const uint
     }
     if (threadIdx.x == 0) part[(int64_t)o * nparts + blockIdx.x] = sh[0];
 }
-__global__ void stats_combine_kernel(const StatAcc* part, int64_t nparts, int nobj, double* out) {
-    const int o = threadIdx.x;
-    if (o >= nobj) return;
+// One workgroup per objective: the partials merged in LDS as a fixed binary
+// tree (deterministic; a serial merge of 256 partials by one thread took
+// 0.18 ms of dependent loads per call, profiles/r02 bookkeeping run).
+__global__ __launch_bounds__(256) void stats_combine_kernel(const StatAcc* part, int64_t nparts,
+                                                            int nobj, double* out) {
+    const int o = blockIdx.x;
+    __shared__ StatAcc sh[256];
     StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0};
-    for (int64_t b = 0; b < nparts; ++b) stat_merge(a, part[(int64_t)o * nparts + b]);  // block order
+    for (int64_t b = threadIdx.x; b < nparts; b += blockDim.x)  // nparts <= 1024
+        stat_merge(a, part[(int64_t)o * nparts + b]);
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) stat_merge(sh[threadIdx.x], sh[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x) return;
+    a = sh[0];
     double* q = out + o * 8;
     const double qnan = __longlong_as_double(0x7FF8000000000000ll);
     const bool nan = a.nan > 0;
@@ -650,7 +663,7 @@ int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights, doub
     if (!part) return DM_ERR_NOMEM;
     stats_kernel<<<dim3((unsigned)nparts, pop->nobj), 256, 0, ctx->stream>>>(
         pop->wvalues, pop->valid, pop->n, pop->nobj, w, part, nparts);
-    stats_combine_kernel<<<1, 64, 0, ctx->stream>>>(part, nparts, pop->nobj, out);
+    stats_combine_kernel<<<pop->nobj, 256, 0, ctx->stream>>>(part, nparts, pop->nobj, out);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

@@ -63,6 +63,21 @@ __device__ __forceinline__ void flip_rows_to_lds(const GenArgs& a, int64_t cbase
     __builtin_amdgcn_wave_barrier();
 }
 
+// Sum of a u32 over the wave, wave-uniform result: DPP adds within each row
+// of 16 lanes (quad xor 1, quad xor 2, half-row mirror, row mirror), then
+// the four row sums by readlane — no LDS round trips (a __shfl_xor butterfly
+// is six ds_bpermute).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm(1,0,3,2)
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm(2,3,0,1)
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // Profiling-only ablations of the fused kernel (product build: 0): bit 0
 // skips the mutFlipBit masks, bit 1 the aspirants' fitness loads, bit 2 the
 // Philox evaluation of the decisions.
@@ -137,9 +152,8 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
             if (has1) __builtin_nontemporal_store(x1, w1 + lane);
         }
         if (EVAL) {
-            uint32_t pc = lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
+            const uint32_t pc =
+                wave_sum_u32(lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u);
             if (lane == 0) {
                 a.cwv[c0] = inv0 ? (double)(pc & 0xFFFFu) * a.w0 : cur.f0;
                 if (has1) a.cwv[c1] = inv1 ? (double)(pc >> 16) * a.w0 : cur.f1;
@@ -364,9 +378,8 @@ __device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, i
             if (h1) __builtin_nontemporal_store(x1, w1 + lane);
         }
         if (EVAL) {
-            uint32_t pc = lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
+            const uint32_t pc =
+                wave_sum_u32(lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u);
             if ((lane >> 1) == q) my_count = (lane & 1) ? (pc >> 16) : (pc & 0xFFFFu);
         }
     }

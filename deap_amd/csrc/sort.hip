@@ -339,9 +339,47 @@ int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool des
 // exactly the stable order: ties by ascending index.  (The previous version
 // bitonic-sorted 4,096-pair slices in LDS and then all candidates in one
 // workgroup: 0.21 ms per selBest of 2^20; profiles/r02h.)
-constexpr int TOPK_MAX = 32;
+constexpr int TOPK_MAX = 128;  // HallOfFame candidate sets are 64+
 constexpr int TOPK_PER = 16;            // pairs per lane
 constexpr int TOPK_SPAN = 64 * TOPK_PER;  // pairs per wave
+
+// (key, index) minimum over a row of 16 lanes through DPP (quad xor 1, quad
+// xor 2, half-row mirror, row mirror: every lane ends with its row's
+// minimum), then over the 4 rows by readlane: wave-uniform result, no LDS
+// round trips (the __shfl_xor butterfly was 18 ds_bpermute per round).
+template <int CTRL>
+__device__ __forceinline__ void dpp_min_step(uint64_t& k, int32_t& i) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)k, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(k >> 32), CTRL, 0xF, 0xF, false);
+    const int32_t oi = __builtin_amdgcn_mov_dpp(i, CTRL, 0xF, 0xF, false);
+    const uint64_t ok = ((uint64_t)hi << 32) | lo;
+    if (ok < k || (ok == k && oi < i)) {
+        k = ok;
+        i = oi;
+    }
+}
+__device__ __forceinline__ void wave_min_pair(uint64_t& k, int32_t& i) {
+    dpp_min_step<0xB1>(k, i);   // quad_perm(1,0,3,2)
+    dpp_min_step<0x4E>(k, i);   // quad_perm(2,3,0,1)
+    dpp_min_step<0x141>(k, i);  // row_half_mirror
+    dpp_min_step<0x140>(k, i);  // row_mirror
+    uint64_t bk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), 0) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 0);
+    int32_t bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const uint64_t rk =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), r) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, r);
+        const int32_t ri = __builtin_amdgcn_readlane(i, r);
+        if (rk < bk || (rk == bk && ri < bi)) {
+            bk = rk;
+            bi = ri;
+        }
+    }
+    k = bk;
+    i = bi;
+}
 
 template <bool FROM_WV>
 __global__ __launch_bounds__(256) void topk_wave_kernel(const double* __restrict__ wv, bool desc,
@@ -381,15 +419,7 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const double* __restrict
                 bk = key[j];
                 bi = idx[j];
             }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t ok = __shfl_xor(bk, o, 64);
-            const int32_t oi = __shfl_xor(bi, o, 64);
-            if (ok < bk || (ok == bk && oi < bi)) {
-                bk = ok;
-                bi = oi;
-            }
-        }
+        wave_min_pair(bk, bi);
 #pragma unroll
         for (int j = 0; j < TOPK_PER; ++j)
             if (idx[j] == bi && key[j] == bk) {

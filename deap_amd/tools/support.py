@@ -366,9 +366,9 @@ class HallOfFame:
         from .selection import selBest
         order = selBest(pop, K).to(torch.int64)
         idx = torch.cat([order, torch.zeros(1, dtype=torch.int64, device=order.device)])
-        dev = (pop.genes_view()[idx], pop.wvalues[: len(pop)][idx], pop.valid[: len(pop)][idx])
-        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (idx,) + dev]
-        for h, t in zip(host, (idx,) + dev):
+        dev = (idx, pop.genes_view()[idx], pop.wvalues[: len(pop)][idx], pop.valid[: len(pop)][idx])
+        host = self._staging(dev)
+        for h, t in zip(host, dev):
             h.copy_(t, non_blocking=True)
         done = torch.cuda.Event()
         done.record()
@@ -378,6 +378,20 @@ class HallOfFame:
             o, g, w, v = (h.numpy() for h in host)
             return o, g, w, v
         return wait
+
+    def _staging(self, dev):
+        """Pinned host buffers for one candidate gather, two sets used in
+        turn: eaSimple has at most one gather in flight while the next is
+        queued, and reusing our own buffers keeps pinned allocations (which
+        can synchronise the device) out of the generation loop."""
+        import torch
+        sets = self.__dict__.setdefault("_pinned", [None, None])
+        i = self.__dict__["_pinned_turn"] = 1 - self.__dict__.get("_pinned_turn", 1)
+        cur = sets[i]
+        if cur is None or any(h.shape[0] < t.shape[0] or h.shape[1:] != t.shape[1:] or
+                              h.dtype != t.dtype for h, t in zip(cur, dev)):
+            cur = sets[i] = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in dev]
+        return [h[: t.shape[0]] for h, t in zip(cur, dev)]
 
     def _try_candidates(self, pop, K, idx, graw, wv, valid):
         """One round of the candidate loop over the gathered rows; commits and
@@ -457,7 +471,8 @@ class HallOfFame:
 
     def __getstate__(self):
         state = dict(self.__dict__)
-        state.pop("_garr", None)
+        for k in ("_garr", "_pinned", "_pinned_turn"):
+            state.pop(k, None)
         return state
 
     def _loop_rows(self, pop, rows, genes, wv, ok, fits):

@@ -201,7 +201,7 @@ def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
 
 
 @pytest.mark.parametrize("n,k", [(200, 1), (4097, 15), (100000, 32), (1 << 20, 15),
-                                 ((1 << 21) - 3, 7)])
+                                 ((1 << 21) - 3, 7), (1 << 20, 64), (300001, 128)])
 def test_sel_best_topk_path_matches_stable_sort(gpu, n, k):
     """selBest / selWorst of a single objective with small k take the
     two-launch top-k path; the result is the reference's stable order
