@@ -177,12 +177,14 @@ def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
     tb.register("mate", tools.cxBlend, alpha=0.5)
     tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
     res = {}
-    for label in ("plain", "stats+hof"):
+    # plain twice (the first eaSimple call of a process may pay allocations):
+    # the faster plain run is the reference
+    for label in ("plain", "stats+hof", "plain2"):
         st = RandomStream(5)
         pop = tools.initPopulation(n=n, dim=dim, low=-5.12, high=5.12, gtype="f64",
                                    weights=(-1.0,), stream=st)
         kw = {}
-        if label != "plain":
+        if label == "stats+hof":
             kw = {"stats": _stats_registered(), "halloffame": tools.HallOfFame(10)}
         algorithms.eaSimple(pop, tb, 0.5, 0.2, 2, verbose=False, stream=st, **kw)  # warm-up
         torch.cuda.synchronize()
@@ -190,14 +192,14 @@ def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
         pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 10, verbose=False, stream=st, **kw)
         torch.cuda.synchronize()
         res[label] = (time.perf_counter() - t0) / 10 * 1e3
-        if label != "plain":
+        if label == "stats+hof":
             mins = log.select("min")
             assert all(np.isfinite(m) for m in mins) and len(kw["halloffame"]) == 10
             best = kw["halloffame"][0].fitness.values[0]
             assert best <= min(mins) + 1e-9
-    print("eaSimple ms/gen at 2^20: plain %.3f, with stats+hof %.3f" % (res["plain"],
-                                                                        res["stats+hof"]))
-    assert res["stats+hof"] < 1.5 * res["plain"] + 2.0
+    plain = min(res["plain"], res["plain2"])
+    print("eaSimple ms/gen at 2^20: plain %.3f, with stats+hof %.3f" % (plain, res["stats+hof"]))
+    assert res["stats+hof"] < 1.5 * plain + 2.0
 
 
 @pytest.mark.parametrize("n,k", [(200, 1), (4097, 15), (100000, 32), (1 << 20, 15),
