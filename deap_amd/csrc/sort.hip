@@ -387,7 +387,9 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const double* __restrict
                                                         const int32_t* __restrict__ iidx, int64_t n,
                                                         int k, uint64_t* __restrict__ okey,
                                                         int32_t* __restrict__ oidx,
-                                                        int32_t* __restrict__ out_final) {
+                                                        int32_t* __restrict__ out_final,
+                                                        const int32_t* __restrict__ skip) {
+    if (skip && *skip) return;  // the bucket selection already wrote the result
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t base = wave * TOPK_SPAN;
@@ -437,35 +439,225 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const double* __restrict
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bucket selection (the usual path for n > one wave's span): the keys' range
+// [kmin, kmax] is cut into 2,048 equal buckets (a monotone map of the key),
+// a histogram finds the bucket B holding the k-th key, every element of a
+// bucket <= B (at most TK_CAP of them) is compacted and ranked by (key,
+// index) among the others: rank < k goes to out[rank].  A few full-width
+// passes instead of k sequential extraction rounds (0.33 ms for k = 64 at
+// 2^20, profiles/r02 bookkeeping run).  When more than TK_CAP elements share
+// the buckets <= B (massive ties) the wave passes above run instead; they
+// read the flag and return at once otherwise.
+constexpr int TK_BUCKETS = 2048, TK_CAP = 16384, TK_BLOCKS = 64;
+struct TkState {
+    unsigned long long kmin, kmax;
+    int32_t B, ncand, fallback, count;
+};
+__device__ __forceinline__ uint64_t tk_key(const double* wv, int64_t i, bool best) {
+    const uint64_t q = ordered_key(wv[i]);
+    return best ? ~q : q;
+}
+__device__ __forceinline__ int tk_bucket(uint64_t key, const TkState& st) {
+    const uint64_t width = (st.kmax - st.kmin) / TK_BUCKETS + 1;
+    return (int)((key - st.kmin) / width);
+}
+__global__ __launch_bounds__(256) void tk_minmax_kernel(const double* __restrict__ wv, int64_t n,
+                                                        bool best, TkState* st) {
+    uint64_t mn = ~0ull, mx = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = tk_key(wv, i, best);
+        mn = key < mn ? key : mn;
+        mx = key > mx ? key : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    __shared__ uint64_t smn[4], smx[4];
+    if ((threadIdx.x & 63) == 0) {
+        smn[threadIdx.x >> 6] = mn;
+        smx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            mn = smn[w] < mn ? smn[w] : mn;
+            mx = smx[w] > mx ? smx[w] : mx;
+        }
+        atomicMin(&st->kmin, (unsigned long long)mn);
+        atomicMax(&st->kmax, (unsigned long long)mx);
+    }
+}
+__global__ __launch_bounds__(256) void tk_hist_kernel(const double* __restrict__ wv, int64_t n,
+                                                      bool best, const TkState* st,
+                                                      int32_t* __restrict__ part) {
+    __shared__ int32_t h[TK_BUCKETS];
+    for (int b = threadIdx.x; b < TK_BUCKETS; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const TkState s = *st;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[tk_bucket(tk_key(wv, i, best), s)], 1);
+    __syncthreads();
+    for (int b = threadIdx.x; b < TK_BUCKETS; b += blockDim.x)
+        part[(int64_t)blockIdx.x * TK_BUCKETS + b] = h[b];
+}
+// one workgroup of 1024: bucket totals, their inclusive scan, the boundary
+__global__ __launch_bounds__(1024) void tk_bound_kernel(const int32_t* __restrict__ part, int nparts,
+                                                        int64_t k, TkState* st) {
+    __shared__ int32_t tot[TK_BUCKETS];
+    __shared__ int32_t wsum[16];
+    constexpr int PER = TK_BUCKETS / 1024;
+    int32_t c[PER];
+    int32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int b = threadIdx.x * PER + j;
+        int32_t t = 0;
+        for (int q = 0; q < nparts; ++q) t += part[(int64_t)q * TK_BUCKETS + b];
+        run += t;
+        c[j] = run;  // inclusive within the thread's buckets
+    }
+    // scan of the per-thread totals
+    int32_t x = run;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int32_t off = 0;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    const int32_t excl = off + x - run;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) tot[threadIdx.x * PER + j] = excl + c[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int b = threadIdx.x * PER + j;
+        const int32_t prev = b ? tot[b - 1] : 0;
+        if (prev < k && tot[b] >= k) {  // exactly one bucket
+            st->B = b;
+            st->ncand = tot[b];
+            st->fallback = tot[b] > TK_CAP ? 1 : 0;
+        }
+    }
+}
+__global__ __launch_bounds__(256) void tk_compact_kernel(const double* __restrict__ wv, int64_t n,
+                                                         bool best, TkState* st,
+                                                         uint64_t* __restrict__ ckey,
+                                                         int32_t* __restrict__ cidx) {
+    if (st->fallback) return;
+    const TkState s = *st;
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        uint64_t key = 0;
+        bool in = false;
+        if (i < n) {
+            key = tk_key(wv, i, best);
+            in = tk_bucket(key, s) <= s.B;
+        }
+        const uint64_t m = __ballot(in);
+        if (!m) continue;
+        int32_t base = 0;
+        if (lane == 0) base = atomicAdd(&st->count, __popcll(m));
+        base = __shfl(base, 0, 64);
+        if (in) {
+            const int32_t slot = base + __popcll(m & ((1ull << lane) - 1));
+            ckey[slot] = key;
+            cidx[slot] = (int32_t)i;
+        }
+    }
+}
+// rank of each candidate by (key, index) among all candidates; rank < k -> out
+__global__ __launch_bounds__(256) void tk_rank_kernel(const uint64_t* __restrict__ ckey,
+                                                      const int32_t* __restrict__ cidx,
+                                                      const TkState* st, int64_t k,
+                                                      int32_t* __restrict__ out) {
+    if (st->fallback) return;
+    const int c = st->ncand;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((int)(blockIdx.x * blockDim.x) >= c) return;  // whole workgroup idle
+    const uint64_t ki = i < c ? ckey[i] : ~0ull;
+    const int32_t ii = i < c ? cidx[i] : INT32_MAX;
+    __shared__ uint64_t tk[1024];
+    __shared__ int32_t ti[1024];
+    int32_t rank = 0;
+    for (int t0 = 0; t0 < c; t0 += 1024) {
+        __syncthreads();
+        for (int j = threadIdx.x; j < 1024; j += blockDim.x) {
+            tk[j] = t0 + j < c ? ckey[t0 + j] : ~0ull;
+            ti[j] = t0 + j < c ? cidx[t0 + j] : INT32_MAX;
+        }
+        __syncthreads();
+        const int m = c - t0 < 1024 ? c - t0 : 1024;
+        for (int j = 0; j < m; ++j) rank += (tk[j] < ki || (tk[j] == ki && ti[j] < ii)) ? 1 : 0;
+    }
+    if (i < c && rank < k) out[rank] = ii;
+}
+__global__ void tk_flip_kernel(TkState* st) { st->fallback = !st->fallback; }
+__global__ void tk_init_kernel(TkState* st) {
+    st->kmin = ~0ull;
+    st->kmax = 0;
+    st->B = 0;
+    st->ncand = 0;
+    st->fallback = 0;
+    st->count = 0;
+}
+
 static int sel_topk(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx, bool best) {
     const int64_t n = pop->n;
     auto waves = [](int64_t m) { return (m + TOPK_SPAN - 1) / TOPK_SPAN; };
-    const int64_t c1 = waves(n) * k;  // candidates after the first pass
-    const size_t kb = align_up((size_t)c1 * 8, 256), ib = align_up((size_t)c1 * 4, 256);
-    char* w = (char*)scratch_slot(ctx, 3, 2 * (kb + ib));
-    if (!w) return DM_ERR_NOMEM;
-    uint64_t* key[2] = {(uint64_t*)w, (uint64_t*)(w + kb + ib)};
-    int32_t* idx[2] = {(int32_t*)(w + kb), (int32_t*)(w + 2 * kb + ib)};
     hipStream_t s = ctx->stream;
-    auto grid = [&](int64_t m) { return dim3((unsigned)((waves(m) + 3) / 4)); };
     if (n <= TOPK_SPAN) {
         topk_wave_kernel<true><<<1, 64, 0, s>>>(pop->wvalues, best, nullptr, nullptr, n, (int)k,
-                                                nullptr, nullptr, out_idx);
+                                                nullptr, nullptr, out_idx, nullptr);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
+    const int64_t c1 = waves(n) * k;  // candidates after the first wave pass
+    const size_t kb = align_up((size_t)c1 * 8, 256), ib = align_up((size_t)c1 * 4, 256);
+    const size_t pb = align_up((size_t)TK_BLOCKS * TK_BUCKETS * 4, 256);
+    const size_t cb = align_up((size_t)TK_CAP * 8, 256) + align_up((size_t)TK_CAP * 4, 256);
+    char* w = (char*)scratch_slot(ctx, 3, 2 * (kb + ib) + pb + cb + 256);
+    if (!w) return DM_ERR_NOMEM;
+    uint64_t* key[2] = {(uint64_t*)w, (uint64_t*)(w + kb + ib)};
+    int32_t* idx[2] = {(int32_t*)(w + kb), (int32_t*)(w + 2 * kb + ib)};
+    char* t = w + 2 * (kb + ib);
+    int32_t* part = (int32_t*)t;
+    uint64_t* ckey = (uint64_t*)(t + pb);
+    int32_t* cidx = (int32_t*)(t + pb + align_up((size_t)TK_CAP * 8, 256));
+    TkState* st = (TkState*)(t + pb + cb);
+    const int32_t* skip = &st->fallback;  // 0 after a bucket selection: wave passes skip
+    // bucket selection
+    tk_init_kernel<<<1, 1, 0, s>>>(st);
+    tk_minmax_kernel<<<TK_BLOCKS * 4, 256, 0, s>>>(pop->wvalues, n, best, st);
+    tk_hist_kernel<<<TK_BLOCKS, 256, 0, s>>>(pop->wvalues, n, best, st, part);
+    tk_bound_kernel<<<1, 1024, 0, s>>>(part, TK_BLOCKS, k, st);
+    tk_compact_kernel<<<TK_BLOCKS * 4, 256, 0, s>>>(pop->wvalues, n, best, st, ckey, cidx);
+    tk_rank_kernel<<<TK_CAP / 256, 256, 0, s>>>(ckey, cidx, st, k, out_idx);
+    // wave passes: only when the buckets <= B hold more than TK_CAP elements
+    tk_flip_kernel<<<1, 1, 0, s>>>(st);  // skip = !fallback
+    auto grid = [&](int64_t m) { return dim3((unsigned)((waves(m) + 3) / 4)); };
     topk_wave_kernel<true><<<grid(n), 256, 0, s>>>(pop->wvalues, best, nullptr, nullptr, n, (int)k,
-                                                   key[0], idx[0], nullptr);
+                                                   key[0], idx[0], nullptr, skip);
     int64_t m = c1;
     int cur = 0;
     while (m > TOPK_SPAN) {
         topk_wave_kernel<false><<<grid(m), 256, 0, s>>>(nullptr, best, key[cur], idx[cur], m, (int)k,
-                                                        key[cur ^ 1], idx[cur ^ 1], nullptr);
+                                                        key[cur ^ 1], idx[cur ^ 1], nullptr, skip);
         m = waves(m) * k;
         cur ^= 1;
     }
     topk_wave_kernel<false><<<1, 64, 0, s>>>(nullptr, best, key[cur], idx[cur], m, (int)k, nullptr,
-                                             nullptr, out_idx);
+                                             nullptr, out_idx, skip);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

@@ -18,7 +18,12 @@ tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
 sizes = {"alone": [1 << 20], "tiny": [1 << 20, 1 << 12], "big": [1 << 20, 1 << 20],
          "pad": [1 << 20], "many": [1 << 20] * 4, "bigrev": [1 << 20, 1 << 20],
          "isl": [1 << 20], "seed": [1 << 20], "swap": [1 << 20, 1 << 20],
-         "swapoff": [1 << 20, 1 << 20], "realloc": [1 << 20], "realloc1g": [1 << 20]}[mode]
+         "swapoff": [1 << 20, 1 << 20], "realloc": [1 << 20], "realloc1g": [1 << 20], "dummy": [1 << 20]}[mode]
+if mode == "dummy":  # an unused population (and its offspring buffer) allocated first
+    _st = RandomStream(3, island=9)
+    _d = tools.initPopulation(n=int(float(sys.argv[2])) if len(sys.argv) > 2 else 1 << 20, dim=1000,
+                              low=-1, high=1, gtype="f64", weights=(-1.0,), stream=_st)
+    _d2 = _d.like(len(_d), capacity=_d.capacity)
 order = [1, 0] if mode == "bigrev" else None
 if mode == "pad":  # a dummy allocation first: does the placement of the buffers matter?
     _pad = torch.empty((int(float(sys.argv[2])) if len(sys.argv) > 2 else 17 << 30,),
