@@ -1025,7 +1025,14 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
             DM_LAUNCH_CHECK();
         }
-        batch = std::min(batch * 2, 32);
+        // next batch from what is left: fronts grow along the peel, so the
+        // remaining individuals / the mean front size so far bounds the fronts
+        // still needed (each launch past `done` returns at once but costs
+        // ~10 us; each extra status check a round trip)
+        const double mean = (double)hst->sorted / (double)(hst->nfronts + 1);
+        const double left = (double)(hst->N - hst->sorted);
+        const int need = mean > 0 ? (int)std::ceil(left / mean) : 32;
+        batch = std::max(2, std::min(need + 2, 32));
     }
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones
     ufront.resize(nf + 1);
