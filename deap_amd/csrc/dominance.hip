@@ -10,29 +10,24 @@
 //    (full-rate VALU compares) instead of fp64 values.  A NaN compares neither
 //    way with anything and has no rank: populations holding one take the fp64
 //    kernels of nsga2.hip.
-// 2. Dominance.  A wave owns SD_WPW 64-v blocks (ranks in VGPRs, lane = v) and
-//    sweeps the u rows of the blocks I <= J below them (ranks by scalar loads,
-//    u wave-uniform).  One pair of compare masks per (u, 64 v) gives both
-//    directions: D[u][J] = ANY(x > y) & ~ANY(x < y) is parked in lane u%64
-//    (v_writelane), and "v dominates u" is shifted lane-locally into the
-//    transposed word D[v][I] — the lower triangle of the matrix comes from the
-//    same compares as the upper one.  Dominator counts accumulate as int16
-//    partials per (v-group, u) and per (u-chunk, v), reduced afterwards.
-//    D is stored in 64 x 8-word tiles (tile (I, G): rows 64I..64I+63, words
-//    8G..8G+7, 64 B per row): a wave's direct stores (64 rows x 32 B) and its
-//    transposed stores (64 rows x 64 B, after 8 u-blocks) are contiguous, and
-//    a row segment read by the peel is one 64-B line.
+// 2. Dominance.  Rows are ordered by objective 0 (q order), so a row can only
+//    dominate the rows before it: tri_dom_kernel computes the lower triangle
+//    only (section 2 below), D[a][b] one bit, with b's dominator count as
+//    int16 partials per (A-group, b) summed by tri_count.  D is stored in
+//    tiles of 64 rows x 16 words (tword): one 128-byte line per row and
+//    1024-v segment.
 // 3. Fronts.  Front 0 = count 0 in U order (nsga2.hip).  Then per front a
-//    peel kernel transposes 64 x 64 bit blocks of the members' rows and
-//    decrements the dominator counts atomically; the wave whose decrement
-//    reaches zero appends v to the next front's candidates and every wave
-//    raises v's (front, last releasing position) with a 64-bit atomicMax.
-//    One workgroup then orders the candidates by (last releasing position,
-//    U index) — the order the reference's peel loop appends them in
-//    (emo.py:106-115) — with a bitonic sort in LDS, writes
-//    the front, its ranks and its individual count, and decides termination
-//    on the device.  The host only checks a status word every few fronts.
+//    peel kernel reads the members' row lines (whole lines), transposes the
+//    64 x 64-bit blocks with DPP / permlane moves (transpose.hpp) and
+//    subtracts the dominator counts; a v whose count reaches zero joins the
+//    next front's candidates with the key (last releasing position, U index).
+//    One workgroup then orders the candidates by that key — the order the
+//    reference's peel loop appends them in (emo.py:106-115, SURVEY.md
+//    §8a-a21) — writes the front, its ranks and its individual count, and
+//    decides termination on the device.  The host only checks a status word
+//    every few fronts.
 #include "sort.hpp"
+#include "transpose.hpp"
 
 namespace dm {
 
@@ -113,11 +108,13 @@ __host__ __device__ __forceinline__ int32_t icomp(const int4& r, int c) {
     return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w;
 }
 
-// word w of row u in the tiled layout: tiles of 64 rows x 4 words (2 KB),
-// NQ = 4-word groups per row.  A wave's store of 4 words of its 64 rows is one
-// contiguous 2 KB; a peel read of 4 words of one row is 32 contiguous bytes.
+// word w of row u in the tiled layout: tiles of 64 rows x TW = 16 words (one
+// 128-byte line per row, 8 KB), NQ = 16-word groups per row.  A wave's store
+// of 4 words of its 64 rows is 64 pieces of 32 bytes that fill the tile's
+// lines over four such stores; a peel read of a row segment is one whole line.
+constexpr int TW = 16;
 __host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NQ) {
-    return ((((u >> 6) * NQ + (w >> 2)) << 6) + (u & 63)) * 4 + (w & 3);
+    return ((((u >> 6) * NQ + w / TW) << 6) + (u & 63)) * TW + (w % TW);
 }
 
 // nseg[g]: 8-block segments of v the rows of A-group g reach (every v whose
@@ -362,21 +359,59 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
 }
 
 // count[sigma[q]] (U order, front 0) = countq[q] (q order, the peel) = sum
-// over the A-groups reaching q's segment of part[g][q]
-__global__ void tri_count_kernel(const int16_t* __restrict__ part, const int32_t* __restrict__ nseg,
-                                 const int32_t* __restrict__ sigma, int64_t U, int64_t Upad,
-                                 int64_t ngroups, int32_t* __restrict__ count,
-                                 int32_t* __restrict__ countq) {
+// over the A-groups reaching q's segment of part[g][q].  The column sums are
+// split over TC_CHUNKS ranges of g (grid y) so that enough loads are in
+// flight (a column of segment 0 has ngroups partials): a thread sums 4
+// adjacent q (one 8-byte load per g, 8 in flight) into tmp[chunk][q], and
+// tri_count_sum_kernel adds the chunks.
+constexpr int TC_CHUNKS = 4;
+__global__ __launch_bounds__(256) void tri_count_part_kernel(const int16_t* __restrict__ part,
+                                                             const int32_t* __restrict__ nseg,
+                                                             int64_t U, int64_t Upad, int64_t ngroups,
+                                                             int32_t* __restrict__ tmp) {
+    const int64_t q0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (q0 >= U) return;
+    const int32_t sq = (int32_t)(q0 >> 9);
+    int64_t lo = 0, hi = ngroups;  // first g with nseg[g] > sq
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (nseg[mid] > sq) hi = mid;
+        else lo = mid + 1;
+    }
+    const int64_t ch = (ngroups + TC_CHUNKS - 1) / TC_CHUNKS;
+    const int64_t g0 = std::max<int64_t>(lo, blockIdx.y * ch);
+    const int64_t g1 = std::min<int64_t>(ngroups, (blockIdx.y + 1) * ch);
+    int32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const uint2* col = reinterpret_cast<const uint2*>(part + q0);  // Upad % 64 == 0: aligned
+    const int64_t rs = Upad / 4;                                    // row stride in uint2
+    auto add = [&](uint2 x) {
+        c0 += (int16_t)(x.x & 0xFFFF);
+        c1 += (int16_t)(x.x >> 16);
+        c2 += (int16_t)(x.y & 0xFFFF);
+        c3 += (int16_t)(x.y >> 16);
+    };
+    int64_t g = g0;
+    for (; g + 8 <= g1; g += 8) {
+        uint2 x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = col[(g + i) * rs];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) add(x[i]);
+    }
+    for (; g < g1; ++g) add(col[g * rs]);
+    int32_t* out = tmp + blockIdx.y * U + q0;
+    out[0] = c0;
+    if (q0 + 1 < U) out[1] = c1;
+    if (q0 + 2 < U) out[2] = c2;
+    if (q0 + 3 < U) out[3] = c3;
+}
+__global__ void tri_count_sum_kernel(const int32_t* __restrict__ tmp, const int32_t* __restrict__ sigma,
+                                     int64_t U, int32_t* __restrict__ count,
+                                     int32_t* __restrict__ countq) {
     DGRID_LOOP(q, U) {
-        const int32_t sq = (int32_t)(q >> 9);
-        int64_t lo = 0, hi = ngroups;  // first g with nseg[g] > sq
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (nseg[mid] > sq) hi = mid;
-            else lo = mid + 1;
-        }
         int32_t cnt = 0;
-        for (int64_t g = lo; g < ngroups; ++g) cnt += part[g * Upad + q];
+#pragma unroll
+        for (int c = 0; c < TC_CHUNKS; ++c) cnt += tmp[c * U + q];
         count[sigma[q]] = cnt;
         countq[q] = cnt;
     }
@@ -403,100 +438,51 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
     const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), m, 64);
     return ((uint64_t)hi << 32) | lo;
 }
-// 64x64 bit transposes across the wave (in lane i bit j = A[i][j]; out lane j
-// bit i = A[i][j]) of N words at once, stage by stage so that the lane
-// exchanges of all N words are in flight together, without branches: the
-// stage of distance s swaps 2s-bit blocks between lanes i and i^s.  s = 32
-// moves whole 32-bit halves; s = 16 and 8 recombine bytes with one v_perm;
-// s = 4, 2, 1 rotate the partner's half and merge with one bit-field insert,
-// the per-lane selectors and masks computed once.
-struct Transposer {
-    uint32_t sel16, sel8, m4, m2, m1, r4, r2, r1;
-    bool low32;
-    __device__ explicit Transposer(int lane) {
-        sel16 = (lane & 16) ? 0x03020706u : 0x05040100u;
-        sel8 = (lane & 8) ? 0x03070105u : 0x06020400u;
-        m4 = (lane & 4) ? ~0x0F0F0F0Fu : 0x0F0F0F0Fu;
-        m2 = (lane & 2) ? ~0x33333333u : 0x33333333u;
-        m1 = (lane & 1) ? ~0x55555555u : 0x55555555u;
-        r4 = (lane & 4) ? 4u : 28u;
-        r2 = (lane & 2) ? 2u : 30u;
-        r1 = (lane & 1) ? 1u : 31u;
-        low32 = (lane & 32) == 0;
-    }
-    template <int N>
-    __device__ __forceinline__ void run(uint32_t (&lo)[N], uint32_t (&hi)[N]) const {
-        {  // s = 32: lanes < 32 take the partner's low half as their high half
-            uint32_t r[N];
-#pragma unroll
-            for (int w = 0; w < N; ++w) r[w] = __shfl_xor(low32 ? hi[w] : lo[w], 32, 64);
-#pragma unroll
-            for (int w = 0; w < N; ++w) {
-                hi[w] = low32 ? r[w] : hi[w];
-                lo[w] = low32 ? lo[w] : r[w];
-            }
-        }
-        bytes<N>(lo, hi, 16, sel16);
-        bytes<N>(lo, hi, 8, sel8);
-        bits<N>(lo, hi, 4, m4, r4);
-        bits<N>(lo, hi, 2, m2, r2);
-        bits<N>(lo, hi, 1, m1, r1);
-    }
-    template <int N>
-    __device__ __forceinline__ static void bytes(uint32_t (&lo)[N], uint32_t (&hi)[N], int s,
-                                                 uint32_t sel) {
-        uint32_t rl[N], rh[N];
-#pragma unroll
-        for (int w = 0; w < N; ++w) {
-            rl[w] = __shfl_xor(lo[w], s, 64);
-            rh[w] = __shfl_xor(hi[w], s, 64);
-        }
-#pragma unroll
-        for (int w = 0; w < N; ++w) {
-            lo[w] = __builtin_amdgcn_perm(rl[w], lo[w], sel);
-            hi[w] = __builtin_amdgcn_perm(rh[w], hi[w], sel);
-        }
-    }
-    template <int N>
-    __device__ __forceinline__ static void bits(uint32_t (&lo)[N], uint32_t (&hi)[N], int s,
-                                                uint32_t m, uint32_t rot) {
-        uint32_t rl[N], rh[N];
-#pragma unroll
-        for (int w = 0; w < N; ++w) {
-            rl[w] = __shfl_xor(lo[w], s, 64);
-            rh[w] = __shfl_xor(hi[w], s, 64);
-        }
-#pragma unroll
-        for (int w = 0; w < N; ++w) {
-            const uint32_t tl = __builtin_amdgcn_alignbit(rl[w], rl[w], rot);
-            const uint32_t th = __builtin_amdgcn_alignbit(rh[w], rh[w], rot);
-            lo[w] = (m & lo[w]) | (~m & tl);
-            hi[w] = (m & hi[w]) | (~m & th);
-        }
-    }
-};
-
-constexpr int PEEL_WAVES = 8;   // waves of a peel workgroup (they split the front's members)
-constexpr int PEEL_BATCH = 2;   // member chunks per wave in flight
-
-// One workgroup (8 waves, two per CU resident) owns one 8-word row segment s
-// (v in [512 s, 512 s + 512), q order): its waves take interleaved 64-member
-// slices of the front, transpose the members' row segments, and the per-wave
+#ifndef DM_PEEL_WAVES
+#define DM_PEEL_WAVES 8
+#endif
+constexpr int PEEL_WAVES = DM_PEEL_WAVES;  // waves of a peel workgroup (they split the front's members)
+#ifndef DM_PEEL_BATCH
+#define DM_PEEL_BATCH 2
+#endif
+constexpr int PEEL_BATCH = DM_PEEL_BATCH;  // member chunks per wave in flight
+constexpr int PEEL_WORDS = TW;  // words of a row segment (one line)
+// One workgroup (8 waves) owns one row segment s of D: PEEL_WORDS = 16 words,
+// v in [1024 s, 1024 s + 1024) in q order, one 128-byte line of a row.  Its
+// waves take interleaved 64-member chunks of the front, load each member's
+// line (whole lines: the reads of a front's random rows fetch no bytes of
+// other rows), transpose the 64 x 64-bit blocks, and the per-wave
 // (dominators, last position) of each v are reduced in LDS.  v is written by
 // this workgroup only, so countq needs no atomics; a v whose count reaches
 // zero is released: its rank, its sort key (last releasing position, U index),
 // its row and its individual count are recorded here, so the ordering kernel
-// only sorts.
-__global__ __launch_bounds__(512) void peel_owned_kernel(const uint64_t* __restrict__ D,
+// only sorts.  A row's reach (mrow.y) counts 512-v halves: the words of a half
+// past it were never stored and read as zero.
+// Slices of the front's members for segment s (grid y = K): a row reaches the
+// segments up to its own, so segment s is read by about (1 - s/NS) of the
+// members and the low segments carry the most work; they are split over up
+// to K workgroups (at least PEEL_SLICE_MIN members each).
+#ifndef DM_PEEL_SLICES
+#define DM_PEEL_SLICES 4
+#endif
+constexpr int PEEL_SLICES = DM_PEEL_SLICES;
+constexpr int64_t PEEL_SLICE_MIN = 1024;
+__device__ __forceinline__ int64_t peel_slices(int64_t F, int64_t s, int64_t NS, int64_t K) {
+    const int64_t byload = (K * (NS - s) + NS - 1) / NS;
+    return std::max<int64_t>(1, std::min<int64_t>(byload, F / PEEL_SLICE_MIN));
+}
+__global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint64_t* __restrict__ D,
                                                          int64_t NQ,
                                                          const int2* __restrict__ mrow,
                                                          const int32_t* __restrict__ gsize,
                                                          const int32_t* __restrict__ sigma,
                                                          FrontState* st, int32_t* countq,
+                                                         unsigned long long* lastq,
                                                          uint64_t* ckey, int32_t* cq,
                                                          int32_t* rankU) {
-    __shared__ int32_t sdec[PEEL_WAVES][512];
-    __shared__ int32_t slast[PEEL_WAVES][512];
+    constexpr int PW = PEEL_WORDS, PV = PW * 64;
+    __shared__ int32_t sdec[PEEL_WAVES][PV];
+    __shared__ int32_t slast[PEEL_WAVES][PV];
     __shared__ int32_t sF, sust, sstop, snf;
     if (threadIdx.x == 0) {
         sF = st->F;
@@ -506,13 +492,19 @@ __global__ __launch_bounds__(512) void peel_owned_kernel(const uint64_t* __restr
     }
     __syncthreads();
     if (sstop) return;
-    const int64_t F = sF, U = st->U, s = blockIdx.x;
-    const int2* members = mrow + sust;  // (row in q order, segments it reaches)
+    const int64_t U = st->U, s = blockIdx.x;
+    // members of this workgroup's slice [j0s, F)
+    const int64_t nsl = peel_slices(sF, s, gridDim.x, gridDim.y);
+    if ((int64_t)blockIdx.y >= nsl) return;
+    const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
+    const int64_t j0s = blockIdx.y * slen;
+    const int64_t F = std::min<int64_t>(sF, j0s + slen);
+    const int2* members = mrow + sust;  // (row in q order, 512-v halves it reaches)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const Transposer tr(lane);
-    int32_t dec[8], last[8];
+    const TransposerX tr(lane);
+    int32_t dec[PW], last[PW];
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < PW; ++w) {
         dec[w] = 0;
         last[w] = -1;
     }
@@ -521,28 +513,21 @@ __global__ __launch_bounds__(512) void peel_owned_kernel(const uint64_t* __restr
     int2 mr[PEEL_BATCH];
 #pragma unroll
     for (int b = 0; b < PEEL_BATCH; ++b) {
-        const int64_t j = (int64_t)wave * 64 + b * STEP + lane;
+        const int64_t j = j0s + (int64_t)wave * 64 + b * STEP + lane;
         mr[b] = j < F ? members[j] : make_int2(0, 0);
     }
-    for (int64_t jb = (int64_t)wave * 64; jb < F; jb += STEP * PEEL_BATCH) {
-        uint64_t seg[PEEL_BATCH][8];
-        bool has[PEEL_BATCH];
+    for (int64_t jb = j0s + (int64_t)wave * 64; jb < F; jb += STEP * PEEL_BATCH) {
+        uint4 seg[PEEL_BATCH][PW / 2];
+        bool has[PEEL_BATCH][2];
 #pragma unroll
         for (int b = 0; b < PEEL_BATCH; ++b) {
-            has[b] = s < mr[b].y;  // words past the reach of the row are not stored (zero)
-            if (has[b]) {
+            const uint4* q = reinterpret_cast<const uint4*>(D + tword(mr[b].x, s * PW, NQ));
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint4* q = reinterpret_cast<const uint4*>(D + tword(mr[b].x, s * 8 + 4 * h, NQ));
-                    const uint4 x0 = q[0], x1 = q[1];
-                    seg[b][4 * h] = ((uint64_t)x0.y << 32) | x0.x;
-                    seg[b][4 * h + 1] = ((uint64_t)x0.w << 32) | x0.z;
-                    seg[b][4 * h + 2] = ((uint64_t)x1.y << 32) | x1.x;
-                    seg[b][4 * h + 3] = ((uint64_t)x1.w << 32) | x1.z;
-                }
-            } else {
+            for (int h = 0; h < 2; ++h) {
+                has[b][h] = 2 * s + h < mr[b].y;
 #pragma unroll
-                for (int w = 0; w < 8; ++w) seg[b][w] = 0;
+                for (int i = 0; i < PW / 4; ++i)
+                    seg[b][h * (PW / 4) + i] = has[b][h] ? q[h * (PW / 4) + i] : make_uint4(0, 0, 0, 0);
             }
         }
 #pragma unroll
@@ -553,60 +538,111 @@ __global__ __launch_bounds__(512) void peel_owned_kernel(const uint64_t* __restr
 #pragma unroll
         for (int b = 0; b < PEEL_BATCH; ++b) {
             const int64_t j0 = jb + b * STEP;
-            if (__ballot(has[b]) == 0) continue;
-            uint32_t lo[8], hi[8];
 #pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                lo[w] = (uint32_t)seg[b][w];
-                hi[w] = (uint32_t)(seg[b][w] >> 32);
-            }
-            tr.run<8>(lo, hi);  // lane v: bit i <-> member j0+i dominates v
+            for (int h = 0; h < 2; ++h) {
+                if (__ballot(has[b][h]) == 0) continue;  // no member of the chunk reaches the half
+                uint32_t lo[8], hi[8];
 #pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                dec[w] += __popc(lo[w]) + __popc(hi[w]);
-                const int32_t top = hi[w] ? 63 - __clz(hi[w]) : (lo[w] ? 31 - __clz(lo[w]) : -1);
-                if (top >= 0) last[w] = (int32_t)(j0 + top);
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 x = seg[b][h * 4 + i];
+                    lo[2 * i] = x.x;
+                    hi[2 * i] = x.y;
+                    lo[2 * i + 1] = x.z;
+                    hi[2 * i + 1] = x.w;
+                }
+                tr.run<8>(lo, hi);  // lane v: bit i <-> member j0+i dominates v
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    dec[h * 8 + w] += __popc(lo[w]) + __popc(hi[w]);
+                    const int32_t top = hi[w] ? 63 - __clz(hi[w]) : (lo[w] ? 31 - __clz(lo[w]) : -1);
+                    if (top >= 0) last[h * 8 + w] = (int32_t)(j0 + top);
+                }
             }
         }
     }
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < PW; ++w) {
         sdec[wave][w * 64 + lane] = dec[w];
         slast[wave][w * 64 + lane] = last[w];
     }
     __syncthreads();
-    const int t = threadIdx.x;
-    int32_t d = 0, l = -1;
+    // release: one atomic per workgroup on the shared counters (a
+    // same-address atomic per wave serialised ~6 ns each over thousands of
+    // waves on the large fronts)
+    constexpr int IT = PV / (PEEL_WAVES * 64);
+    __shared__ int32_t wcnt[IT][PEEL_WAVES];
+    __shared__ int64_t wgs[IT][PEEL_WAVES];
+    __shared__ int32_t sbase;
+    bool fresh[IT];
+    int32_t lk[IT], vu[IT];
+    unsigned long long fm[IT];
 #pragma unroll
-    for (int wv = 0; wv < PEEL_WAVES; ++wv) {
-        d += sdec[wv][t];
-        l = max(l, slast[wv][t]);
-    }
-    const int64_t v = s * 512 + t;  // q order
-    bool fresh = false;
-    if (v < U && d > 0) {
-        const int32_t left = countq[v] - d;
-        countq[v] = left;
-        fresh = left == 0;
-    }
-    const unsigned long long fm = __ballot(fresh);
-    if (fm) {
-        const int first = __ffsll(fm) - 1;
-        int32_t base = 0;
-        if (lane == first) base = atomicAdd(&st->ncand, __popcll(fm));
-        base = __shfl(base, first, 64);
-        int64_t gs = 0;
-        if (fresh) {
-            const int32_t vu = sigma[v];
-            const int32_t slot = base + __popcll(fm & ((1ull << lane) - 1));
-            ckey[slot] = ((uint64_t)(uint32_t)l << 32) | (uint32_t)vu;
-            cq[slot] = (int32_t)v;
-            rankU[vu] = snf + 1;
-            gs = gsize[vu];
+    for (int it = 0; it < IT; ++it) {
+        const int t = threadIdx.x + it * PEEL_WAVES * 64;
+        int32_t d = 0, l = -1;
+#pragma unroll
+        for (int wv = 0; wv < PEEL_WAVES; ++wv) {
+            d += sdec[wv][t];
+            l = max(l, slast[wv][t]);
         }
+        const int64_t v = s * PV + t;  // q order
+        fresh[it] = false;
+        if (v < U && d > 0) {
+            if (nsl == 1) {
+                const int32_t left = countq[v] - d;
+                countq[v] = left;
+                fresh[it] = left == 0;
+            } else {
+                // several slices: publish the last position, then subtract;
+                // the subtraction that reaches zero is ordered after every
+                // slice's max (each waits for its max before subtracting)
+                const unsigned long long key = ((unsigned long long)(snf + 1) << 32) | (uint32_t)l;
+                __hip_atomic_fetch_max(lastq + v, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int32_t old = __hip_atomic_fetch_add(countq + v, -d, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (old == d) {
+                    fresh[it] = true;
+                    l = (int32_t)(uint32_t)__hip_atomic_fetch_max(lastq + v, key, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        lk[it] = l;
+        vu[it] = fresh[it] ? sigma[v] : 0;
+        fm[it] = __ballot(fresh[it]);
+        int64_t gs = fresh[it] ? gsize[vu[it]] : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
-        if (lane == first) atomicAdd((unsigned long long*)&st->pending, (unsigned long long)gs);
+        if (lane == 0) {
+            wcnt[it][wave] = __popcll(fm[it]);
+            wgs[it][wave] = gs;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t tot = 0;
+        int64_t gtot = 0;
+        for (int it = 0; it < IT; ++it)
+            for (int wv = 0; wv < PEEL_WAVES; ++wv) {
+                const int32_t c = wcnt[it][wv];
+                wcnt[it][wv] = tot;
+                tot += c;
+                gtot += wgs[it][wv];
+            }
+        sbase = tot ? atomicAdd(&st->ncand, tot) : 0;
+        if (gtot) atomicAdd((unsigned long long*)&st->pending, (unsigned long long)gtot);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        if (!fresh[it]) continue;
+        const int64_t v = s * PV + threadIdx.x + it * PEEL_WAVES * 64;
+        const int32_t slot = sbase + wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
+        ckey[slot] = ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it];
+        cq[slot] = (int32_t)v;
+        rankU[vu[it]] = snf + 1;
     }
 }
 
@@ -876,7 +912,7 @@ __global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, i
 // Workspace of the fast path: the buffers that live from the ranks to the
 // last front, then the scratch shared by the rank sorts and the peel loop.
 struct FastLayout {
-    int64_t NB, NG, NQ, ngroups, Upad;
+    int64_t NB, NG, NQ, ngroups, Upad;  // NG: 512-v segments (tri_dom), NQ: TW-word lines (peel)
     size_t part, S, sigma, pos, nseg, toff, counter, mrow, countq, cq, work, total;
 };
 static size_t ranks_work_bytes(int64_t n) {
@@ -884,14 +920,14 @@ static size_t ranks_work_bytes(int64_t n) {
            radix_sort_temp_bytes(n) + scan_temp_bytes(n);
 }
 static size_t fronts_work_bytes(int64_t U) {
-    return align_up(sizeof(FrontState), 256) + 2 * align_up((size_t)U * 8, 256) +
+    return align_up(sizeof(FrontState), 256) + 3 * align_up((size_t)U * 8, 256) +
            2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
 }
 static FastLayout fast_layout(int64_t n, int64_t U) {
     FastLayout L;
     L.NB = (U + 63) / 64;
     L.NG = (L.NB + 7) / 8;
-    L.NQ = (L.NB + 3) / 4;
+    L.NQ = (L.NB + TW - 1) / TW;
     L.ngroups = (L.NB + TD_WPW - 1) / TD_WPW;
     L.Upad = L.NB * 64;
     size_t off = 0;
@@ -916,8 +952,8 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
 }
 size_t fast_dom_bytes(int64_t n, int64_t U) { return fast_layout(n, U).total; }
 int64_t fast_dom_words(int64_t U) {
-    const int64_t NB = (U + 63) / 64, NG = (NB + 7) / 8;
-    return NB * 64 * NG * 8;
+    const int64_t NB = (U + 63) / 64, NQ = (NB + TW - 1) / TW;
+    return NB * 64 * NQ * TW;
 }
 
 // Ranks (objective 0 from the population's lexicographic order perm, whose
@@ -968,8 +1004,13 @@ int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t 
         default: tri_dom_kernel<4><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
     }
     DM_LAUNCH_CHECK();
-    tri_count_kernel<<<dg1(U), 256, 0, s>>>(part, nseg, sigma, U, L.Upad, L.ngroups, count,
-                                            (int32_t*)(ws + L.countq));
+    // the rank sorts' keys / ktmp (2 n x 8 bytes) hold the TC_CHUNKS column sums
+    static_assert(TC_CHUNKS * 4 <= 16, "tri_count scratch exceeds keys + ktmp");
+    int32_t* ctmp = (int32_t*)keys;
+    const int64_t cthreads = (U + 3) / 4;
+    tri_count_part_kernel<<<dim3((unsigned)((cthreads + 255) / 256), TC_CHUNKS), 256, 0, s>>>(
+        part, nseg, U, L.Upad, L.ngroups, ctmp);
+    tri_count_sum_kernel<<<dg1(U), 256, 0, s>>>(ctmp, sigma, U, count, (int32_t*)(ws + L.countq));
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -982,7 +1023,6 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted) {
     hipStream_t s = ctx->stream;
     const FastLayout L = fast_layout(n, U);
-    const int64_t NG = L.NG;
     const int32_t* sigma = (const int32_t*)(ws + L.sigma);
     const int32_t* pos = (const int32_t*)(ws + L.pos);
     const int32_t* nseg = (const int32_t*)(ws + L.nseg);
@@ -1000,7 +1040,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
     p += align_up((size_t)U * 4, 256);
     int32_t* vtmp = (int32_t*)p;
     p += align_up((size_t)U * 4, 256);
+    // sliced peels: per v the max (front + 1, last releasing position)
+    unsigned long long* lastq = (unsigned long long*)p;
+    p += align_up((size_t)U * 8, 256);
     void* rtemp = p;
+    DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     member_rows_kernel<<<dg1(F0), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
     FrontState* hst = (FrontState*)pinned(ctx, sizeof(FrontState));
@@ -1008,8 +1052,8 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
     int batch = 4;
     for (;;) {
         for (int b = 0; b < batch; ++b) {
-            peel_owned_kernel<<<(unsigned)NG, 512, 0, s>>>(D, L.NQ, mrow, gsize, sigma, st, countq,
-                                                           ckey, cq, rankU);
+            peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
+                D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
         }
         DM_LAUNCH_CHECK();
