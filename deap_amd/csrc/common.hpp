@@ -55,6 +55,7 @@ struct dm_ctx {
     void* pinned = nullptr;  // small host staging area for host-synchronising calls
     size_t pinned_bytes = 0;
     int num_cus = 256;
+    int peel_hint = 4;  // fronts the last fast sortNondominated peeled (first status batch)
     double* zig = nullptr;  // ziggurat tables (device), see zig_normal
     // nevals counters (kEvalSpreadWords, zero between launches; see
     // evals_fold): a kernel's workgroups add their counts to 64 counters 128 B

@@ -466,7 +466,10 @@ constexpr int PEEL_WORDS = TW;  // words of a row segment (one line)
 #define DM_PEEL_SLICES 4
 #endif
 constexpr int PEEL_SLICES = DM_PEEL_SLICES;
-constexpr int64_t PEEL_SLICE_MIN = 1024;
+#ifndef DM_PEEL_SLICE_MIN
+#define DM_PEEL_SLICE_MIN 1024
+#endif
+constexpr int64_t PEEL_SLICE_MIN = DM_PEEL_SLICE_MIN;
 __device__ __forceinline__ int64_t peel_slices(int64_t F, int64_t s, int64_t NS, int64_t K) {
     const int64_t byload = (K * (NS - s) + NS - 1) / NS;
     return std::max<int64_t>(1, std::min<int64_t>(byload, F / PEEL_SLICE_MIN));
@@ -885,13 +888,16 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
     }
 }
 
-__global__ void member_rows_kernel(const int32_t* ulist, int64_t F, const int32_t* pos,
+__global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, const int32_t* pos,
                                    const int32_t* nseg, int2* mrow) {
+    const int64_t F = *Fp;
     DGRID_LOOP(j, F) mrow[j] = member_row(ulist[j], pos, nseg);
 }
 
-__global__ void front_init_kernel(FrontState* st, int32_t F0, int64_t sorted0, int64_t N, int64_t U,
-                                  int32_t* fstarts) {
+__global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int64_t* sorted0p,
+                                  int64_t N, int64_t U, int32_t* fstarts) {
+    const int32_t F0 = *F0p;
+    const int64_t sorted0 = *sorted0p;
     st->F = F0;
     st->ustart = 0;
     st->nfronts = 0;
@@ -1015,10 +1021,13 @@ int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t 
     return DM_OK;
 }
 
-// Fronts 1.. after front 0 (ulist[0, F0), rankU set): peel on the device,
-// checking the status every few fronts.  Fills ufront (front starts in ulist,
-// host) and *sorted (individuals).  ws: the fast_dom_build workspace.
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0, int64_t sorted0,
+// Fronts 1.. after front 0 (ulist[0, *F0), rankU set): peel on the device,
+// checking the status every few fronts.  F0 and sorted0 (front 0's unique
+// fitnesses and individuals) stay on the device.  Fills ufront (front starts
+// in ulist, host; fstarts on the device) and *sorted (individuals).  ws: the
+// fast_dom_build workspace.
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
+                const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted) {
     hipStream_t s = ctx->stream;
@@ -1046,10 +1055,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
     void* rtemp = p;
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
-    member_rows_kernel<<<dg1(F0), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
+    member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
     FrontState* hst = (FrontState*)pinned(ctx, sizeof(FrontState));
     if (!hst) return DM_ERR_NOMEM;
-    int batch = 4;
+    // first status check after as many fronts as the previous call needed
+    int batch = std::max(2, std::min(ctx->peel_hint + 1, 32));
     for (;;) {
         for (int b = 0; b < batch; ++b) {
             peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
@@ -1079,6 +1089,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0
         batch = std::max(2, std::min(need + 2, 32));
     }
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones
+    ctx->peel_hint = hst->nfronts;
     ufront.resize(nf + 1);
     DM_HIP(hipMemcpyAsync(ufront.data(), fstarts, (size_t)(nf + 1) * 4, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));

@@ -33,7 +33,8 @@ int64_t fast_dom_words(int64_t U);
 int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t n,
                    const int32_t* perm, const int32_t* segin, const int32_t* uidx,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, int32_t F0, int64_t sorted0,
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
+                const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted);
 
@@ -373,6 +374,20 @@ __global__ void sum_gsize_kernel(const int32_t* members, int64_t F, const int32_
     }
     if (threadIdx.x == 0 && sh[0]) atomicAdd((unsigned long long*)total, (unsigned long long)sh[0]);
 }
+__global__ void sum_gsize_dev_kernel(const int32_t* members, const int32_t* Fp, const int32_t* gsize,
+                                     int64_t* total) {
+    __shared__ int64_t sh[256];
+    const int64_t F = *Fp;
+    int64_t acc = 0;
+    GRID_LOOP(j, F) acc += gsize[members[j]];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && sh[0]) atomicAdd((unsigned long long*)total, (unsigned long long)sh[0]);
+}
 
 // ---------------------------------------------------------------------------
 // 4. expansion to individuals
@@ -531,26 +546,32 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     if ((rc = exclusive_scan_i32(s, flag, fpos, U, ftotal, ustemp))) return rc;
     compact_kernel<<<g1(U), 256, 0, s>>>(flag, fpos, U, ulist, nullptr, nullptr, rankU, 0);
     DM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
-    DM_HIP(hipMemcpyAsync(hostv, ftotal, 4, hipMemcpyDeviceToHost, s));
-    DM_HIP(hipStreamSynchronize(s));
-    int64_t F = hostv[0];
-    std::vector<int32_t> ufront{0};
-    int64_t ustart = 0;  // start of the current front in ulist
-    sum_gsize_kernel<<<g1(F), 256, 0, s>>>(ulist, F, gsize, dtotal);
-    int64_t* hostd = (int64_t*)(hostv + 8);
-    DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
-    DM_HIP(hipStreamSynchronize(s));
-    int64_t sorted_inds = hostd[0];
-    ufront.push_back((int32_t)F);
     const int64_t N = std::min<int64_t>(n, k);
+    std::vector<int32_t> ufront{0};
+    int64_t F = 0, sorted_inds = 0;
+    int64_t ustart = 0;  // start of the current front in ulist
     int32_t rnk = 0;
-    if (fast && !first_only && sorted_inds < N && F < U && F > 0) {
+    int64_t* hostd = (int64_t*)(hostv + 8);
+    const bool device_fronts = fast && !first_only;
+    if (device_fronts) {
+        // front 0's size and individual count stay on the device: the peel's
+        // first kernel reads them (no host round trip)
+        sum_gsize_dev_kernel<<<g1(U), 256, 0, s>>>(ulist, ftotal, gsize, dtotal);
         int64_t total = 0;
         // ufs doubles as the device front-start array
-        if ((rc = fast_fronts(ctx, D, n, U, (int32_t)F, sorted_inds, N, gsize, ulist, rankU, count,
-                              ufs, fwork, ufront, &total)))
+        if ((rc = fast_fronts(ctx, D, n, U, ftotal, dtotal, N, gsize, ulist, rankU, count, ufs,
+                              fwork, ufront, &total)))
             return rc;
         sorted_inds = total;
+    } else {
+        DM_HIP(hipMemcpyAsync(hostv, ftotal, 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        F = hostv[0];
+        sum_gsize_kernel<<<g1(F), 256, 0, s>>>(ulist, F, gsize, dtotal);
+        DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        sorted_inds = hostd[0];
+        ufront.push_back((int32_t)F);
     }
     while (!fast && !first_only && sorted_inds < N && ustart + F < U && F > 0) {
         // peel front `rnk` (ulist[ustart, ustart+F)) -> front rnk+1
@@ -591,8 +612,9 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     }
     const int32_t nfronts = (int32_t)ufront.size() - 1;
     const int64_t T = ufront.back();  // unique fits in emitted fronts
-    // expansion
-    DM_HIP(hipMemcpyAsync(ufs, ufront.data(), ufront.size() * 4, hipMemcpyHostToDevice, s));
+    // expansion (the device peel already wrote ufs)
+    if (!device_fronts)
+        DM_HIP(hipMemcpyAsync(ufs, ufront.data(), ufront.size() * 4, hipMemcpyHostToDevice, s));
     member_sizes_kernel<<<g1(T), 256, 0, s>>>(ulist, T, gsize, flag);
     if ((rc = exclusive_scan_i32(s, flag, outpos, T, ftotal, ustemp))) return rc;
     expand_kernel<<<g1(T), 256, 0, s>>>(ulist, T, outpos, useg, gsize, perm, order);
@@ -602,7 +624,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         // individuals outside the emitted fronts keep rankU = -1
         ind_rank_kernel<<<g1(n), 256, 0, s>>>(ui, rankU, n, rank);
     }
-    DM_HIP(hipStreamSynchronize(s));  // ufront host vector goes out of scope
+    if (!device_fronts) DM_HIP(hipStreamSynchronize(s));  // ufront host vector goes out of scope
     res->nsorted = sorted_inds;
     res->nfronts = nfronts;
     DM_LAUNCH_CHECK();
