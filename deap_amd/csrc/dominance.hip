@@ -1056,8 +1056,13 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
-    FrontState* hst = (FrontState*)pinned(ctx, sizeof(FrontState));
-    if (!hst) return DM_ERR_NOMEM;
+    // status word and the first front starts come back together: when the
+    // peel is done they are usually all that is needed (one round trip)
+    char* hbuf = (char*)pinned(ctx, 2048);
+    if (!hbuf) return DM_ERR_NOMEM;
+    FrontState* hst = (FrontState*)hbuf;
+    int32_t* hfs = (int32_t*)(hbuf + 256);
+    const int64_t npre = std::min<int64_t>((2048 - 256) / 4, U + 2);
     // first status check after as many fronts as the previous call needed
     int batch = std::max(2, std::min(ctx->peel_hint + 1, 32));
     for (;;) {
@@ -1068,6 +1073,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
         }
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
+        DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));
         DM_HIP(hipStreamSynchronize(s));
         if (hst->done) break;
         if (hst->overflow) {
@@ -1091,8 +1097,12 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones
     ctx->peel_hint = hst->nfronts;
     ufront.resize(nf + 1);
-    DM_HIP(hipMemcpyAsync(ufront.data(), fstarts, (size_t)(nf + 1) * 4, hipMemcpyDeviceToHost, s));
-    DM_HIP(hipStreamSynchronize(s));
+    if (nf + 1 <= npre) {
+        std::copy(hfs, hfs + nf + 1, ufront.begin());
+    } else {
+        DM_HIP(hipMemcpyAsync(ufront.data(), fstarts, (size_t)(nf + 1) * 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+    }
     *sorted = hst->sorted;
     return DM_OK;
 }

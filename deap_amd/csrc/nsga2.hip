@@ -445,7 +445,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
                         radix_sort_temp_bytes(n) + scan_temp_bytes(n) + 8192;
     char* base = (char*)scratch(ctx, need);
     if (!base) return DM_ERR_NOMEM;
-    int32_t* hostv = (int32_t*)pinned(ctx, 64);
+    int32_t* hostv = (int32_t*)pinned(ctx, 2048);  // the size fast_fronts asks for: no realloc
     if (!hostv) return DM_ERR_NOMEM;
     Bump bp{base};
     uint64_t* keys = bp.take<uint64_t>(n);
