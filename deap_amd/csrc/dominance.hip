@@ -429,6 +429,7 @@ struct FrontState {
     int32_t ncand;     // candidates of the next front appended by the peel
     int64_t sorted;    // individuals in the emitted fronts
     int64_t pending;   // individuals of the released candidates (gsize sums)
+    int64_t lastinds;  // individuals of the last emitted front
     int64_t N;         // min(n, k)
     int64_t U;
 };
@@ -876,6 +877,7 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
         const int32_t nstart = snstart, r = st->nfronts;
         const int64_t sorted = st->sorted + st->pending;
         st->sorted = sorted;
+        st->lastinds = st->pending;
         st->pending = 0;
         st->ustart = nstart;
         st->F = n;
@@ -905,6 +907,7 @@ __global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int6
     st->overflow = 0;
     st->ncand = 0;
     st->sorted = sorted0;
+    st->lastinds = sorted0;
     st->pending = 0;
     st->N = N;
     st->U = U;
@@ -1029,7 +1032,8 @@ int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t 
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
-                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted) {
+                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
+                int64_t* last_inds) {
     hipStream_t s = ctx->stream;
     const FastLayout L = fast_layout(n, U);
     const int32_t* sigma = (const int32_t*)(ws + L.sigma);
@@ -1104,6 +1108,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
         DM_HIP(hipStreamSynchronize(s));
     }
     *sorted = hst->sorted;
+    *last_inds = hst->lastinds;
     return DM_OK;
 }
 

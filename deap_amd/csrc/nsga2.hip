@@ -36,7 +36,8 @@ int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t 
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
-                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted);
+                int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
+                int64_t* last_inds);
 
 // ---------------------------------------------------------------------------
 // Workspace bump allocator over the context scratch
@@ -421,6 +422,7 @@ __global__ void front_start_kernel(const int32_t* ufront_start, int32_t nfronts,
 struct SortResult {
     int64_t nsorted = 0;
     int32_t nfronts = 0;
+    int64_t last_inds = 0;  // individuals of the last emitted front
 };
 
 static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, bool first_only,
@@ -553,6 +555,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     int32_t rnk = 0;
     int64_t* hostd = (int64_t*)(hostv + 8);
     const bool device_fronts = fast && !first_only;
+    int64_t last_inds = 0;
     if (device_fronts) {
         // front 0's size and individual count stay on the device: the peel's
         // first kernel reads them (no host round trip)
@@ -560,7 +563,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         int64_t total = 0;
         // ufs doubles as the device front-start array
         if ((rc = fast_fronts(ctx, D, n, U, ftotal, dtotal, N, gsize, ulist, rankU, count, ufs,
-                              fwork, ufront, &total)))
+                              fwork, ufront, &total, &last_inds)))
             return rc;
         sorted_inds = total;
     } else {
@@ -571,6 +574,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
         DM_HIP(hipStreamSynchronize(s));
         sorted_inds = hostd[0];
+        last_inds = hostd[0];
         ufront.push_back((int32_t)F);
     }
     while (!fast && !first_only && sorted_inds < N && ustart + F < U && F > 0) {
@@ -605,6 +609,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         DM_HIP(hipMemcpyAsync(hostd, dtotal, 8, hipMemcpyDeviceToHost, s));
         DM_HIP(hipStreamSynchronize(s));
         sorted_inds += hostd[0];
+        last_inds = hostd[0];
         ustart = nstart;
         F = F2;
         ++rnk;
@@ -627,6 +632,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     if (!device_fronts) DM_HIP(hipStreamSynchronize(s));  // ufront host vector goes out of scope
     res->nsorted = sorted_inds;
     res->nfronts = nfronts;
+    res->last_inds = last_inds;
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -789,17 +795,15 @@ extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weight
     if (rc) return rc;
     rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd);
     if (rc) return rc;
-    // host copy of front starts (small)
-    std::vector<int32_t> fs(r.nfronts + 1);
-    DM_HIP(hipMemcpyAsync(fs.data(), fstart, fs.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-    DM_HIP(hipStreamSynchronize(ctx->stream));
-    const int64_t chosen = r.nfronts > 0 ? fs[r.nfronts - 1] : 0;
+    // fronts before the last one are taken whole (emo.py:38-40); the sort
+    // reports the emitted individuals and the last front's size on the host
+    const int64_t chosen = r.nfronts > 0 ? r.nsorted - r.last_inds : 0;
     if (chosen > 0)
         DM_HIP(hipMemcpyAsync(out_idx, order, (size_t)std::min(chosen, k) * 4,
                               hipMemcpyDeviceToDevice, ctx->stream));
     const int64_t rem = k - chosen;
     if (rem > 0 && r.nfronts > 0) {
-        const int64_t L = fs[r.nfronts] - chosen;  // last front size
+        const int64_t L = r.last_inds;  // last front size
         char* base = (char*)scratch(ctx, 2 * align_up((size_t)L * 8, 256) +
                                              2 * align_up((size_t)L * 4, 256) +
                                              radix_sort_temp_bytes(L) + 4096);
