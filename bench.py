@@ -44,9 +44,16 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py "
+                         "starts torch.distributed.run with this many ranks itself")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (gloo: CPU launcher test only)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="N > 1 launcher check without a GPU: rendezvous, deme ownership and "
+                         "the migRing hop plan of every rank, no kernels")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c5", "c5x"])
@@ -60,7 +67,53 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1234)
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """``--gpus N`` (N > 1) started as a plain ``python bench.py``: run
+    ``torch.distributed.run`` with N ranks as a CHILD process (nothing here
+    imports torch or touches a GPU, and nothing execs), relay its output line
+    by line (progress reaches the caller while the ranks run), check that
+    rank 0's JSON line reports ``n_gpus == N`` and exit with the children's
+    status.  The same command therefore measures 1, 2, 4 or 8 GPUs."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    result = None
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            result = s
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        sys.stderr.write("bench.py: torch.distributed.run with %d ranks failed (exit %d)\n"
+                         % (n, rc))
+        return rc or 1
+    if result is None:
+        sys.stderr.write("bench.py: rank 0 printed no result line\n")
+        return 1
+    got = json.loads(result).get("n_gpus")
+    if got != n:
+        sys.stderr.write("bench.py: expected n_gpus == %d in the result, got %r\n" % (n, got))
+        return 1
+    print(result, flush=True)
+    return 0
 
 
 def cpu_model():
@@ -74,24 +127,60 @@ def cpu_model():
     return "unknown"
 
 
-def host_workers():
-    """Worker processes for the CPU baseline: every CPU this process may run
-    on (sched_getaffinity), capped at the 16-CPU share the GPU box grants one
-    GPU (its os.cpu_count() reports the whole machine)."""
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup (v2 ``cpu.max`` "quota period", v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``), or None when unlimited or
+    unreadable."""
+    import math
     try:
-        avail = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def host_workers():
+    """Worker processes for the CPU baseline = every core this process is
+    granted: the CPUs it may run on (sched_getaffinity), limited by the cgroup
+    CPU quota when one is set; with no quota, by the per-job thread grant the
+    environment states (OMP_NUM_THREADS — the GPU box sets it to its 16-CPU
+    share per GPU, while os.cpu_count() there reports the whole machine).
+    Returns (workers, detail)."""
+    try:
+        visible = len(os.sched_getaffinity(0))
     except AttributeError:
-        avail = os.cpu_count() or 1
-    return max(1, min(avail, int(os.environ.get("DM_CPU_WORKERS", "16")))), avail
+        visible = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    env = os.environ.get("DM_CPU_WORKERS") or os.environ.get("OMP_NUM_THREADS")
+    if quota is not None:
+        workers, source = min(visible, quota), "cgroup cpu quota"
+    elif env and env.isdigit() and int(env) > 0:
+        workers, source = min(visible, int(env)), ("DM_CPU_WORKERS" if os.environ.get(
+            "DM_CPU_WORKERS") else "OMP_NUM_THREADS (per-job CPU grant)")
+    else:
+        workers, source = visible, "sched_getaffinity"
+    return max(1, workers), {"cpus_visible": visible, "cgroup_quota": quota,
+                             "cores_source": source}
 
 
 def cpu_baseline(problem, sample):
     from oracle import deap_port
-    workers, avail = host_workers()
+    workers, detail = host_workers()
     dim = CONFIGS_DIM[problem]
     rate, secs, used = deap_port.run(problem, n=sample, dim=dim, ngen=2, workers=workers)
     return {"value": rate, "unit": "individual-generations/sec", "cores": used, "kind": "port",
-            "cpu_model": cpu_model(), "cpus_visible": avail,
+            "cpu_model": cpu_model(), **detail,
             "sample": "DEAP-faithful eaSimple (oracle/deap_port.py, bit-exact with the reference on "
                       "tests/golden/port.npz: array genomes, deepcopy clone, Pool(%d).map "
                       "evaluate), pop %d x %d genes, 2 timed generations (%.1f s)"
@@ -116,23 +205,73 @@ def load_traffic(config):
         return None
 
 
-def main():
-    args = parse()
+def deme_split(args, world, rank):
+    """Demes per rank: ``--islands I`` splits I demes evenly over the ranks
+    (strong scaling, C4 literally), otherwise ``--islands-per-gpu`` demes per
+    rank (weak scaling; the default N-GPU run is one 2^20 island per GPU)."""
+    if args.islands:
+        if args.islands % world:
+            raise SystemExit("--islands must be a multiple of the GPU count")
+        per, scaling = args.islands // world, "strong"
+    else:
+        per, scaling = args.islands_per_gpu, "weak"
+    return per, scaling, per * world, list(range(rank * per, (rank + 1) * per))
+
+
+def dry_run(args, world, rank):
+    """Launcher / distributed-setup check without a GPU (``--dry-run``, used
+    by tests/test_bench_launcher.py over gloo): every rank joins the process
+    group, agrees on the deme owners (islands.owner_map, the all_gather the
+    real run does) and computes its migRing hops with the C ABI's planner
+    (``dm_mig_plan``, host-only); rank 0 prints them in the bench line."""
+    import torch.distributed as dist
+    from deap_amd import islands
+    if world > 1:
+        dist.init_process_group(args.backend)
+    per, scaling, n_demes, ids = deme_split(args, world, rank)
+    owner = islands.owner_map(ids, n_demes, world, None)
+    plan = islands.mig_plan(n_demes, None, owner, rank)
+    plans = [None] * world
+    if world > 1:
+        dist.all_gather_object(plans, plan)
+    else:
+        plans = [plan]
+    if rank == 0:
+        print(json.dumps({"metric": METRICS[args.config], "value": None, "n_gpus": world,
+                          "dry_run": True, "scaling": scaling, "islands": n_demes,
+                          "owner": [owner[d] for d in range(n_demes)], "hops": plans}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return launch_ranks(args.gpus, argv)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s" % (args.gpus,
+                                                                    os.environ["WORLD_SIZE"]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if args.config == "c5":
-        return bench_nsga2(args)
+        return bench_nsga2(args, world, rank, local)
     if args.config == "c5x":
-        return bench_nsga2_example(args)
+        return bench_nsga2_example(args, world, rank, local)
     import ctypes
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(args.backend, device_id=torch.device("cuda", local)
+                                if args.backend == "nccl" else None)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -141,14 +280,7 @@ def main():
 
     problem, gtype, dim, cx, mut, weights, bpi = CONFIGS[args.config]
     n = args.pop
-    if args.islands:
-        if args.islands % world:
-            raise SystemExit("--islands must be a multiple of the GPU count")
-        per, scaling = args.islands // world, "strong"
-    else:
-        per, scaling = args.islands_per_gpu, "weak"
-    n_demes = per * world
-    ids = list(range(rank * per, (rank + 1) * per))
+    per, scaling, n_demes, ids = deme_split(args, world, rank)
     low, high = {"rastrigin": (-5.12, 5.12), "rosenbrock": (-2.048, 2.048),
                  "onemax": (0, 1)}[problem]
     streams = [RandomStream(args.seed, island=d) for d in ids]
@@ -277,6 +409,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        from deap_amd import islands
+        islands.close_comms()
         dist.destroy_process_group()
 
 
@@ -286,8 +420,8 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
     tests/golden/nsga2*.npz, speed within +-20 % of the reference in
     tests/golden/port_nsga2_calibration.json) on host individuals.
     nd='standard' is O(M N^2) Python: timed on random subsets of the 2N
-    fitnesses at 512 / 1,024 / 2,048 and extrapolated to 2N with the fitted
-    power law (declared); nd='log' (DEAP's fastest ranks) is timed at the full
+    fitnesses at 1,024 / 2,048 / 4,096 / 8,192 and extrapolated to 2N with the
+    power law fitted on them (declared); nd='log' (DEAP's fastest ranks) is timed at the full
     2N.  One core (DEAP's selection is serial).  The variation/evaluation of a
     generation costs seconds on the CPU against hours of selection and is left
     out."""
@@ -296,17 +430,17 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
     rng = np.random.default_rng(7)
     n2 = len(wv2)
     pts = []
-    for n in (512, 1024, 2048):
+    for n in (1024, 2048, 4096, 8192):
         rows = rng.choice(n2, n, replace=False)
         pts.append((n, deap_port.time_sel_nsga2(wv2[rows], weights, n // 2, "standard")))
     slope = float(np.polyfit(np.log([p[0] for p in pts]), np.log([p[1] for p in pts]), 1)[0])
     t_std = pts[-1][1] * (n2 / pts[-1][0]) ** slope
     out = {"value": round(pop / t_std, 4), "unit": "individual-generations/sec", "cores": 1,
            "kind": "port", "cpu_model": cpu_model(),
-           "sample": "selNSGA2(2N -> N, nd='standard') of the port at 2N = 512/1024/2048 "
-                     "(%.2f/%.2f/%.2f s), extrapolated to 2N = %d with the fitted law N^%.2f: "
-                     "%.0f s per generation (declared extrapolation)"
-                     % (pts[0][1], pts[1][1], pts[2][1], n2, slope, t_std),
+           "sample": "selNSGA2(2N -> N, nd='standard') of the port at 2N = "
+                     "1024/2048/4096/8192 (%s s), extrapolated to 2N = %d with the law N^%.2f "
+                     "fitted on those points: %.0f s per generation (declared extrapolation)"
+                     % ("/".join("%.2f" % p[1] for p in pts), n2, slope, t_std),
            "law_exponent": round(slope, 3), "standard_s_per_gen": round(t_std, 1)}
     if with_log:
         t_log = deap_port.time_sel_nsga2(wv2, weights, n2 // 2, "log")
@@ -316,7 +450,45 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
     return out
 
 
-def bench_nsga2(args):
+def replica_setup(args, world, local):
+    """C5 / C5x at N > 1: replicas only (no exchange step), one
+    process per GPU; the process group is used for the barrier and the
+    max-over-ranks time only."""
+    import torch
+    import torch.distributed as dist
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group(args.backend, device_id=device if args.backend == "nccl" else None)
+    return device
+
+
+def replica_barrier(world):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def replica_max(x, world, device):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def replica_finish(world):
+    import torch.distributed as dist
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_nsga2(args, world=1, rank=0, local=0):
     """Config C5: NSGA-II on DTLZ2, M=3, D=12 fp64, pop 2^17.
     A step is one eaMuPlusLambda generation (deap/algorithms.py:316-329): varOr
     of lambda = N offspring (cxBlend / mutGaussian) with the invalid ones
@@ -324,16 +496,22 @@ def bench_nsga2(args):
     the chosen rows.  The dominant stage is the all-pairs dominance pass of
     sortNondominated, VALU-bound: roofline = pairwise fitness comparisons per
     second (M compares per ordered pair, U(U-1) ordered pairs of unique fits)
-    against the fp64 VALU compare rate (256 CU x 4 SIMD x 16 lanes x 2.4 GHz).
+    against the 32-bit integer VALU rate: the dominance kernel compares dense
+    integer ranks (MI355X_MICROARCH.md: 4 SIMD x 32 lanes per CU per cycle ->
+    256 x 128 x 2.4 GHz = 78.6 T lane-ops/s), and SURVEY.md §8d counts one
+    M-objective compare per UNORDERED pair of unique fitnesses, M*U(U-1)/2.
+    ``roofline`` is tri_dom_kernel's own average duration (HIP events the
+    library records around its launches, dm_ctx_set_timing_target), and
+    ``selection`` the same count over the whole selNSGA2.
     Replicas only at N > 1 (no exchange)."""
+    import ctypes
     import torch
-    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd import _lib, algorithms, base, benchmarks, tools
     from deap_amd.ops import RandomStream
-    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
-    torch.cuda.set_device(device)
+    device = replica_setup(args, world, local)
     n = args.pop if args.pop != 1 << 20 else 1 << 17
     m, dim = 3, 12
-    stream = RandomStream(args.seed)
+    stream = RandomStream(args.seed, island=rank)
     pop = tools.initPopulation(n=n, dim=dim, low=0.0, high=1.0, gtype="f64",
                                weights=(-1.0,) * m, device=device, stream=stream)
     tb = base.Toolbox()
@@ -345,64 +523,83 @@ def bench_nsga2(args):
     step = algorithms.MuPlusLambdaStep(pop, tb, n, n, 0.6, 0.3)
     for _ in range(args.warmup):
         step.step(stream)
-    torch.cuda.synchronize()
+    replica_barrier(world)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
     t0 = time.perf_counter()
     for s in range(args.steps):
         ev[2 * s].record()
         step.step(stream)
         ev[2 * s + 1].record()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    replica_barrier(world)
+    elapsed = replica_max(time.perf_counter() - t0, world, device)
     gen_ms = sum(ev[2 * s].elapsed_time(ev[2 * s + 1]) for s in range(args.steps)) / args.steps
     # stage breakdown outside the timed region: selNSGA2 alone on 2N rows
     # (current parents + one varOr batch of offspring)
     comb = step.combined
     sel_ms = []
     two = pop.like(2 * n, capacity=2 * n)
-    from deap_amd import _lib
-    import ctypes
-    _lib.call("dm_gather", comb.ctx.bind(), ctypes.byref(comb.c_pop()), None,
-              ctypes.byref(two.c_pop(0, n)))
+    ctx = comb.ctx.bind()
+    _lib.call("dm_gather", ctx, ctypes.byref(comb.c_pop()), None, ctypes.byref(two.c_pop(0, n)))
     off = algorithms.varOr(comb, tb, n, 0.6, 0.3, evaluate=True, stream=stream)
-    _lib.call("dm_gather", comb.ctx.bind(), ctypes.byref(off.c_pop()), None,
-              ctypes.byref(two.c_pop(n, n)))
-    for _ in range(4):
+    _lib.call("dm_gather", ctx, ctypes.byref(off.c_pop()), None, ctypes.byref(two.c_pop(n, n)))
+    reps = 5
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_DOMINANCE)
+    _lib.call("dm_ctx_set_timing", ctx, reps)
+    for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        idx = tools.selNSGA2(two, n)
+        tools.selNSGA2(two, n)
         b.record()
         torch.cuda.synchronize()
         sel_ms.append(a.elapsed_time(b))
-    sel_ms = sorted(sel_ms[1:])[1]
+    times = (ctypes.c_float * reps)()
+    cnt = ctypes.c_int32(0)
+    _lib.call("dm_ctx_kernel_times", ctx, times, reps, ctypes.byref(cnt))
+    _lib.call("dm_ctx_set_timing", ctx, 0)
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_GENERATION)
+    assert cnt.value == reps, "expected one dominance kernel per selection, got %d" % cnt.value
+    dom_ms = sorted(times[1:])[(reps - 1) // 2]
+    sel_ms = sorted(sel_ms[1:])[(reps - 1) // 2]
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
     uniq = int(torch.unique(wv, dim=0).shape[0])
-    cmp_per_sel = float(m) * uniq * (uniq - 1)
-    valu_peak = 256 * 4 * 16 * 2.4e9 / 1e9  # Gop/s of fp64 compares
-    achieved = cmp_per_sel / (sel_ms * 1e-3) / 1e9
+    cmp_per_sel = float(m) * uniq * (uniq - 1) / 2.0
+    valu_peak = 256 * 4 * 32 * 2.4e9 / 1e9  # Gop/s of 32-bit integer VALU lane ops
+    achieved = cmp_per_sel / (dom_ms * 1e-3) / 1e9
+    sel_achieved = cmp_per_sel / (sel_ms * 1e-3) / 1e9
     out = {"metric": "individual-generations/sec @pop=2^17 DTLZ2 NSGA-II (C5)",
-           "value": round(n * args.steps / elapsed, 1), "unit": "individual-generations/sec",
-           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "value": round(n * args.steps * world / elapsed, 1),
+           "unit": "individual-generations/sec",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": "C5 NSGA-II DTLZ2 M=3 D=12 eaMuPlusLambda(mu=lambda=N) + "
                                   "selNSGA2(2N->N)", "pop": n, "genes": dim, "objectives": m,
                       "operators": "varOr cxBlend(0.5) mutGaussian(0,0.1,1/D) cxpb=0.6 mutpb=0.3",
-                      "parallelism": "replicas1"},
+                      "parallelism": "replicas%d" % world},
            "gen_ms_events": round(gen_ms, 4),
            "roofline": {"bound": "valu", "achieved": round(achieved, 1), "peak": valu_peak,
                         "unit": "Gcompare/s", "frac": round(achieved / valu_peak, 4),
-                        "traffic": None, "kernel": "selNSGA2 (dom_build + peel + crowding)",
-                        "kernel_ms": round(sel_ms, 4), "unique_fits": uniq,
-                        "fronts": len(fronts)},
+                        "traffic": None, "kernel": "tri_dom_kernel<3>",
+                        "kernel_ms": round(dom_ms, 4),
+                        "compares_per_launch": cmp_per_sel,
+                        "count": "M*U(U-1)/2 (one M-objective compare per unordered pair of "
+                                 "unique fitnesses, SURVEY.md 8d)",
+                        "peak_basis": "32-bit int VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz",
+                        "unique_fits": uniq, "fronts": len(fronts)},
+           "selection": {"ms": round(sel_ms, 4), "achieved": round(sel_achieved, 1),
+                         "frac": round(sel_achieved / valu_peak, 4),
+                         "what": "whole selNSGA2(2N -> N): ranks, dominance, peel, crowding, "
+                                 "last-front selection"},
            "cpu_baseline": None}
-    if not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_nsga2(wv.cpu().numpy(), (-1.0,) * m, n)
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    replica_finish(world)
 
 
-def bench_nsga2_example(args):
+def bench_nsga2_example(args, world=1, rank=0, local=0):
     """DEAP's canonical NSGA-II loop (examples/ga/nsga2.py:94-114) on DTLZ2,
     M=3, D=12 fp64, pop 2^17.  A step is one generation: selTournamentDCD(pop, N)
     -> clone + cxSimulatedBinaryBounded(eta 20, cxpb 0.9) + mutPolynomialBounded
@@ -415,11 +612,10 @@ def bench_nsga2_example(args):
     import torch
     from deap_amd import _lib, algorithms, base, benchmarks, tools
     from deap_amd.ops import RandomStream
-    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
-    torch.cuda.set_device(device)
+    device = replica_setup(args, world, local)
     n = args.pop if args.pop != 1 << 20 else 1 << 17
     m, dim = 3, 12
-    stream = RandomStream(args.seed)
+    stream = RandomStream(args.seed, island=rank)
     pop = tools.initPopulation(n=n, dim=dim, low=0.0, high=1.0, gtype="f64",
                                weights=(-1.0,) * m, device=device, stream=stream)
     tb = base.Toolbox()
@@ -460,37 +656,40 @@ def bench_nsga2_example(args):
 
     for _ in range(args.warmup):
         one_gen(False)
-    torch.cuda.synchronize()
+    replica_barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_gen(True)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    replica_barrier(world)
+    elapsed = replica_max(time.perf_counter() - t0, world, device)
     vms = sorted(a.elapsed_time(b) for a, b in var_ms)
     v_ms = sum(vms) / len(vms)
     var_bytes = (n // 2) * (4 * dim * 8) + n * (4 + 2 * m * 8 + 2)
     achieved = var_bytes / (v_ms * 1e-3) / 1e9
     out = {"metric": "individual-generations/sec @pop=2^17 DTLZ2 NSGA-II example loop (C5x)",
-           "value": round(n * args.steps / elapsed, 1), "unit": "individual-generations/sec",
-           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "value": round(n * args.steps * world / elapsed, 1),
+           "unit": "individual-generations/sec",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": "C5x examples/ga/nsga2.py loop: selTournamentDCD + "
                                   "cxSimulatedBinaryBounded + mutPolynomialBounded + "
                                   "selNSGA2(2N->N)", "pop": n, "genes": dim, "objectives": m,
-                      "parallelism": "replicas1"},
+                      "parallelism": "replicas%d" % world},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
                         "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
                         "kernel": "bounded_vary_kernel (varBounded)",
                         "kernel_ms": round(v_ms, 5)},
            "cpu_baseline": None}
-    if not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the loop's CPU cost is its selNSGA2 (selTournamentDCD and the bounded
         # operators of 2^17 individuals take seconds): the C5 baseline applies
         out["cpu_baseline"] = cpu_baseline_nsga2(two.wvalues[:2 * n].cpu().numpy(), (-1.0,) * m,
                                                  n, with_log=False)
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    replica_finish(world)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -150,22 +150,74 @@ def load(path, device=None, individual_class=None, capacity=None):
     return out
 
 
+def _reference_tools():
+    """DEAP's own ``deap.tools`` when it is importable (a user switching from
+    the reference has it), else None."""
+    try:
+        from deap import tools as ref_tools  # noqa: F401  (the user's DEAP)
+    except ImportError:
+        return None
+    return ref_tools
+
+
+def to_reference_types(halloffame, logbook, tools_module):
+    """Rebuild a hall of fame and a logbook as ``tools_module.HallOfFame`` /
+    ``tools_module.Logbook`` objects (DEAP's classes when exporting for DEAP:
+    unpickling them then needs DEAP only, not deap_amd).  The hall keeps its
+    order (insertion worst first re-creates equal-fitness order exactly,
+    support.py:550-560); the logbook keeps header, records, chapters and the
+    stream position."""
+    hof = lb = None
+    if halloffame is not None:
+        hof = tools_module.HallOfFame(halloffame.maxsize, halloffame.similar)
+        for ind in reversed(list(halloffame)):
+            hof.insert(ind)
+    if logbook is not None:
+        lb = _copy_logbook(logbook, tools_module.Logbook)
+    return hof, lb
+
+
+def _copy_logbook(src, cls):
+    lb = cls()
+    lb.header = list(src.header) if src.header is not None else None
+    lb.extend(dict(r) for r in src)
+    lb.buffindex = src.buffindex
+    for name, ch in src.chapters.items():
+        lb.chapters[name] = _copy_logbook(ch, cls)
+    return lb
+
+
 def export_reference_dict(population, generation=None, halloffame=None, logbook=None,
-                          stream=None, individual_class=None):
+                          stream=None, individual_class=None, tools_module=None):
     """The checkpoint dict of the reference's tutorial
     (doc/tutorials/advanced/checkpoint.rst:21-65):
     ``dict(population=..., generation=..., halloffame=..., logbook=...,
-    rndstate=...)`` with the population materialised as host individuals
-    (``individual_class`` — e.g. a DEAP ``creator.Individual`` — or plain
-    lists carrying a ``fitness``; ``fitness.wvalues`` set for valid rows), the
-    hall of fame and logbook as given, and ``rndstate`` = the counter-based
-    stream state ``(seed, island, counter)`` (the device does not draw from
-    Python's ``random``; the tuple resumes the same stream through
-    :func:`import_reference_dict`).  A user who pickles it, as the tutorial
-    does, gets a file that their DEAP code can read."""
+    rndstate=random.getstate())``.
+
+    * ``population``: host individuals (``individual_class`` — e.g. DEAP's
+      ``creator.Individual`` — or plain lists carrying a ``fitness``;
+      ``fitness.wvalues`` set for valid rows);
+    * ``halloffame`` / ``logbook``: DEAP's ``tools.HallOfFame`` /
+      ``tools.Logbook`` holding the same entries when DEAP is importable (or
+      ``tools_module``'s classes), otherwise the deap_amd objects (same API);
+    * ``rndstate``: ``random.getstate()`` — what the tutorial passes to
+      ``random.setstate`` (checkpoint.rst:32);
+    * ``device_stream``: the counter-based device stream ``(seed, island,
+      counter)`` that :func:`import_reference_dict` resumes bit-exactly (the
+      device never draws from Python's ``random``)."""
+    import random
+    tm = tools_module if tools_module is not None else _reference_tools()
+    if tm is not None:
+        halloffame, logbook = to_reference_types(halloffame, logbook, tm)
     return {"population": population.to_individuals(individual_class),
             "generation": generation, "halloffame": halloffame, "logbook": logbook,
-            "rndstate": tuple(stream.getstate()) if stream is not None else None}
+            "rndstate": random.getstate(),
+            "device_stream": tuple(stream.getstate()) if stream is not None else None}
+
+
+def _stream_triple(v):
+    return (isinstance(v, (tuple, list)) and len(v) == 3
+            and all(isinstance(x, int) for x in v))
 
 
 def import_reference_dict(cp, weights=None, gtype=None, device=None, capacity=None):
@@ -175,20 +227,24 @@ def import_reference_dict(cp, weights=None, gtype=None, device=None, capacity=No
     ``weights`` default to the first individual's ``fitness.weights``; genome
     type by ``gtype`` or inferred (DevicePopulation.from_individuals).
     Returns a dict with ``population`` (DevicePopulation), ``generation``,
-    ``halloffame``, ``logbook`` and ``stream`` (a RandomStream when ``rndstate``
-    is a ``(seed, island, counter)`` tuple, else None)."""
+    ``halloffame``, ``logbook`` and ``stream`` (a RandomStream from
+    ``device_stream``; a checkpoint written by DEAP itself has none — the run
+    then continues on a fresh stream).  ``rndstate`` is left to the caller's
+    ``random.setstate`` exactly as in the tutorial."""
     from .device import DevicePopulation
     from .ops import RandomStream
     pop = DevicePopulation.from_individuals(list(cp["population"]), weights, gtype, device,
                                             capacity)
     stream = None
-    rs = cp.get("rndstate")
-    if isinstance(rs, (tuple, list)) and len(rs) == 3 and all(isinstance(x, int) for x in rs):
+    ds = cp.get("device_stream")
+    if ds is None and _stream_triple(cp.get("rndstate")):
+        ds = cp["rndstate"]  # round-2 exports kept the stream under rndstate
+    if _stream_triple(ds):
         stream = RandomStream()
-        stream.setstate(tuple(rs))
+        stream.setstate(tuple(ds))
     return {"population": pop, "generation": cp.get("generation"),
             "halloffame": cp.get("halloffame"), "logbook": cp.get("logbook"), "stream": stream}
 
 
 __all__ = ["save", "load", "read_header", "header", "export_reference_dict",
-           "import_reference_dict"]
+           "import_reference_dict", "to_reference_types"]

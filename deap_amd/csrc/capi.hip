@@ -482,6 +482,13 @@ int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches) {
     return DM_OK;
 }
 
+int dm_ctx_set_timing_target(dm_ctx* ctx, int32_t target) {
+    DM_CHECK_ARG(ctx != nullptr && (target == DM_TIME_GENERATION || target == DM_TIME_DOMINANCE),
+                 "bad timing target %d", target);
+    ctx->timing_target = target;
+    return DM_OK;
+}
+
 int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count) {
     DM_CHECK_ARG(ctx != nullptr && count != nullptr && (ms != nullptr || cap == 0), "bad argument");
     const int n = std::min(ctx->tev_used, (int)cap);

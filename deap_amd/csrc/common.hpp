@@ -65,6 +65,7 @@ struct dm_ctx {
     // launch stream around each generation kernel, for bench.py's roofline.
     std::vector<hipEvent_t> tev;
     int tev_used = 0;  // pairs recorded so far
+    int timing_target = 0;  // DM_TIME_GENERATION / DM_TIME_DOMINANCE: which launches
 };
 
 namespace dm {
@@ -107,15 +108,17 @@ __device__ __forceinline__ void evals_fold(long long* spread, int64_t* nevals, l
     *nevals += (int64_t)tot;
 }
 
-// Event pair i around the next generation-kernel launch (no-op when timing is
-// off or every pair has been used).
-inline void timing_begin(dm_ctx* ctx) {
+// Event pair i around the next launch of the timed kind (target: 0 = the
+// generation kernel, 1 = the NSGA-II dominance kernel; no-op when timing is
+// off, another kind is timed, or every pair has been used).
+inline void timing_begin(dm_ctx* ctx, int target = 0) {
     const int i = ctx->tev_used;
-    if (2 * i + 1 < (int)ctx->tev.size()) (void)hipEventRecord(ctx->tev[2 * i], ctx->stream);
+    if (target == ctx->timing_target && 2 * i + 1 < (int)ctx->tev.size())
+        (void)hipEventRecord(ctx->tev[2 * i], ctx->stream);
 }
-inline void timing_end(dm_ctx* ctx) {
+inline void timing_end(dm_ctx* ctx, int target = 0) {
     const int i = ctx->tev_used;
-    if (2 * i + 1 < (int)ctx->tev.size()) {
+    if (target == ctx->timing_target && 2 * i + 1 < (int)ctx->tev.size()) {
         (void)hipEventRecord(ctx->tev[2 * i + 1], ctx->stream);
         ctx->tev_used = i + 1;
     }

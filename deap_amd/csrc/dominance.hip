@@ -972,9 +972,11 @@ int64_t fast_dom_words(int64_t U) {
 // Ranks (objective 0 from the population's lexicographic order perm, whose
 // group starts segin marks; uidx: U index of each group's representative),
 // the dominance words D (fast_dom_words(U)) and count[U] (U order).
-int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t n,
+int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
                    const int32_t* perm, const int32_t* segin, const int32_t* uidx,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws) {
+    hipStream_t s = ctx->stream;
+    const int num_cus = ctx->num_cus;
     const FastLayout L = fast_layout(n, U);
     int4* S = (int4*)(ws + L.S);
     int32_t* sigma = (int32_t*)(ws + L.sigma);
@@ -1011,11 +1013,13 @@ int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t 
     }
     tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
     const unsigned blocks = (unsigned)std::max(1, num_cus) * 8;
+    timing_begin(ctx, DM_TIME_DOMINANCE);
     switch (m) {
         case 2: tri_dom_kernel<2><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
         case 3: tri_dom_kernel<3><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
         default: tri_dom_kernel<4><<<blocks, 256, 0, s>>>(S, U, L.NB, L.NQ, L.ngroups, nseg, toff, counter, D, part); break;
     }
+    timing_end(ctx, DM_TIME_DOMINANCE);
     DM_LAUNCH_CHECK();
     // the rank sorts' keys / ktmp (2 n x 8 bytes) hold the TC_CHUNKS column sums
     static_assert(TC_CHUNKS * 4 <= 16, "tri_count scratch exceeds keys + ktmp");

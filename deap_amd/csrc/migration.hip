@@ -109,7 +109,9 @@ __device__ __forceinline__ bool wave_genome_eq(const char* a, const char* b, int
 }
 
 // bitmap[j][w]: bit r%64 of word r/64 set iff row r equals immigrant j;
-// first[j] = the lowest such row.  A wave owns 64 consecutive rows (one bitmap
+// first[j] = the lowest such row.  dirty (nullable): rows an earlier hop of
+// the same migration overwrote — the immigrant object that was there is no
+// longer in the list, so list.index's identity test cannot hit that row.  A wave owns 64 consecutive rows (one bitmap
 // word per immigrant, written with a plain store), lane = row: the row's
 // fitness / validity are loaded once and compared with a tile of 64
 // immigrants staged in LDS; a fitness match (or an invalid fitness on either
@@ -118,6 +120,7 @@ __global__ __launch_bounds__(256) void match_kernel(const char* genes, const dou
                                                     const uint8_t* valid, int64_t n, int64_t stride,
                                                     int dim, int gtype, int nobj,
                                                     const void* imm_block, int64_t k, int64_t words,
+                                                    const unsigned long long* dirty,
                                                     unsigned long long* bitmap, int32_t* first) {
     Block im = block_view((void*)imm_block, stride, nobj, k);
     __shared__ double swv[64 * DM_MAX_OBJ];
@@ -143,11 +146,12 @@ __global__ __launch_bounds__(256) void match_kernel(const char* genes, const dou
 #pragma unroll
             for (int o = 0; o < DM_MAX_OBJ; ++o) f[o] = (in && o < nobj) ? wv[r * nobj + o] : 0.0;
             const uint8_t vr = in ? valid[r] : 0;
+            const bool clean = !(in && dirty && ((dirty[r >> 6] >> (r & 63)) & 1ull));
             for (int jj = 0; jj < jn; ++jj) {
                 const int64_t j = jt + jj;
                 // list.index tests `is` before `==` (PyObject_RichCompareBool):
                 // the immigrant's own row matches even when its genome holds a NaN
-                const bool self = in && r == ssrc[jj];
+                const bool self = in && clean && r == ssrc[jj];
                 bool eq = self;
                 // fitness prefilter (fit_prefilter, registers unrolled)
                 bool pre = in && !self;
@@ -192,8 +196,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
                                                       const void* em_block, int64_t k,
                                                       int64_t words, unsigned long long* bitmap,
                                                       const uint8_t* E, const int32_t* first,
-                                                      int32_t* slots,
-                                                      int32_t* content, int32_t* err) {
+                                                      int32_t* slots, int32_t* content,
+                                                      unsigned long long* dirty, int32_t* err) {
     Block em = block_view((void*)em_block, stride, nobj, k);
     __shared__ int64_t best;
     __shared__ int32_t placed_slot[4096];
@@ -226,6 +230,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
             if (lane == 0) {
                 valid[slot] = em.valid[j];
                 slots[j] = (int32_t)slot;
+                if (dirty) atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
             }
         }
         return;
@@ -277,7 +282,10 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
         uint4* dst = reinterpret_cast<uint4*>(genes + slot * stride);
         for (int64_t i = threadIdx.x; i < stride / 16; i += blockDim.x) dst[i] = src[i];
         if (threadIdx.x < nobj) wv[slot * nobj + threadIdx.x] = em.wv[j * nobj + threadIdx.x];
-        if (threadIdx.x == 0) valid[slot] = em.valid[j];
+        if (threadIdx.x == 0) {
+            valid[slot] = em.valid[j];
+            if (dirty) atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+        }
         // the row no longer holds its original genome
         for (int64_t jj = j + 1 + threadIdx.x; jj < k; jj += blockDim.x)
             bitmap[jj * words + (slot >> 6)] &= ~(1ull << (slot & 63));
@@ -312,9 +320,12 @@ extern "C" int dm_pack_rows(dm_ctx* ctx, const dm_pop* pop, const int32_t* idx, 
 namespace dm {
 // Placement for one receiving deme, asynchronous: *err (device int32) gets
 // j + 1 when immigrant j is not found (list.index ValueError), else stays 0.
+// dirty (nullable, ceil(n/64) words): rows overwritten by earlier hops into
+// this deme in the same migration (read by the identity test, and the rows
+// this placement overwrites are added).
 static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
                            const void* emigrant_block, int64_t k, int32_t* out_slots,
-                           int32_t* err) {
+                           unsigned long long* dirty, int32_t* err) {
     const int64_t n = pop->n;
     const int64_t words = (n + 63) / 64;
     const size_t bm = align_up((size_t)k * words * 8, 256);
@@ -335,13 +346,12 @@ static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block
         1, std::min<int64_t>((words + 3) / 4, (int64_t)ctx->num_cus * 16));
     match_kernel<<<grid, 256, 0, s>>>((const char*)pop->genes, pop->wvalues, pop->valid, n,
                                       pop->stride, pop->dim, pop->gtype, pop->nobj,
-                                      immigrant_block, k, words, bitmap, first);
+                                      immigrant_block, k, words, dirty, bitmap, first);
     em_im_eq_kernel<<<(unsigned)std::max<int64_t>(1, (k * k + 255) / 256), 256, 0, s>>>(
         emigrant_block, immigrant_block, k, pop->stride, pop->dim, pop->gtype, pop->nobj, E);
     resolve_kernel<<<1, 256, 0, s>>>((char*)pop->genes, pop->wvalues, pop->valid, n, pop->stride,
                                      pop->nobj, emigrant_block, k, words, bitmap, E, first,
-                                     out_slots,
-                                     content, err);
+                                     out_slots, content, dirty, err);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -357,7 +367,8 @@ extern "C" int dm_mig_place(dm_ctx* ctx, dm_pop* pop, const void* immigrant_bloc
     int32_t* err = (int32_t*)scratch_slot(ctx, 4, 256);
     if (!err) return DM_ERR_NOMEM;
     DM_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
-    if ((rc = mig_place_async(ctx, pop, immigrant_block, emigrant_block, k, out_slots, err)))
+    if ((rc = mig_place_async(ctx, pop, immigrant_block, emigrant_block, k, out_slots, nullptr,
+                              err)))
         return rc;
     int32_t herr = 0;
     DM_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -451,10 +462,12 @@ extern "C" int dm_sel_sample(dm_ctx* ctx, int64_t n, int64_t k, dm_rng rng, int3
 // ---------------------------------------------------------------------------
 #include <rccl/rccl.h>
 #include <cstring>
+#include <string>
 
 struct dm_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    int32_t* flag = nullptr;  // device word for mig_agree
 };
 
 namespace dm {
@@ -492,24 +505,35 @@ static int plan_hops(int32_t n_demes, const int32_t* migarray, const int32_t* ow
         }                                                                          \
     } while (0)
 
-static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
-                         const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
-                         const int32_t* owner, int64_t k, int32_t* const* emig_idx,
-                         int32_t* const* immig_idx, int32_t* const* out_slots, int32_t flags) {
-    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+// Every per-rank check of a migration, and the scratch it needs, before any
+// communication: a rank that fails here must not leave its peers waiting in
+// ncclSend / ncclRecv (see mig_agree).
+struct MigPlan {
+    std::vector<int32_t> local_of;
+    std::vector<dm_mig_hop> hops;
+    char* base = nullptr;
+    size_t bb = 0;
+    int nrecv = 0;
+    std::vector<int32_t> hops_into;  // per local deme: hops that place into it
+};
+
+static int mig_prepare(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
+                       const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
+                       const int32_t* owner, int64_t k, int32_t* const* emig_idx, int32_t flags,
+                       MigPlan& P) {
     DM_CHECK_ARG(n_demes >= 1 && n_local >= 0 && n_local <= n_demes, "bad deme counts");
     DM_CHECK_ARG(n_local == 0 || (demes && deme_ids && emig_idx), "null deme arrays");
     DM_CHECK_ARG(k >= 0 && k <= 4096, "k must be in [0, 4096]");
     const int me = comm ? comm->rank : 0;
     // local index of every global deme held here
-    std::vector<int32_t> local_of(n_demes, -1);
+    P.local_of.assign(n_demes, -1);
     for (int32_t i = 0; i < n_local; ++i) {
         DM_CHECK_ARG(deme_ids[i] >= 0 && deme_ids[i] < n_demes, "deme id %d out of range",
                      deme_ids[i]);
-        DM_CHECK_ARG(local_of[deme_ids[i]] < 0, "deme %d listed twice", deme_ids[i]);
+        DM_CHECK_ARG(P.local_of[deme_ids[i]] < 0, "deme %d listed twice", deme_ids[i]);
         if (owner) DM_CHECK_ARG(owner[deme_ids[i]] == me, "deme %d is not owned by rank %d",
                                 deme_ids[i], me);
-        local_of[deme_ids[i]] = i;
+        P.local_of[deme_ids[i]] = i;
         int rc = validate_pop(&demes[i], "deme");
         if (rc) return rc;
         DM_CHECK_ARG(emig_idx[i] != nullptr || k == 0, "null emigrant indices");
@@ -519,8 +543,7 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
         for (int32_t d = 0; d < n_demes; ++d)
             DM_CHECK_ARG(owner[d] >= 0 && (!comm || owner[d] < comm->nranks), "bad owner[%d]", d);
     if (!owner) DM_CHECK_ARG(n_local == n_demes, "without owner every deme must be local");
-    std::vector<dm_mig_hop> hops;
-    int rc = plan_hops(n_demes, migarray, owner, me, flags, hops);
+    int rc = plan_hops(n_demes, migarray, owner, me, flags, P.hops);
     if (rc) return rc;
     if (k == 0 || n_local == 0) return DM_OK;
     // every deme shares one layout (the blocks travel between them)
@@ -528,14 +551,69 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
         DM_CHECK_ARG(demes[i].stride == demes[0].stride && demes[i].dim == demes[0].dim &&
                          demes[i].gtype == demes[0].gtype && demes[i].nobj == demes[0].nobj,
                      "demes differ in layout");
-    const size_t bb = align_up((size_t)block_bytes(&demes[0], k), 256);
-    int nrecv = 0;
-    for (const dm_mig_hop& h : hops) nrecv += h.kind == DM_HOP_RECV;
-    // [emigrant block | immigrant block] per local deme, then one per receive
-    char* base = (char*)scratch_slot(ctx, 4, bb * (2 * (size_t)n_local + nrecv) +
-                                                 align_up((size_t)k * 4, 256) +
-                                                 align_up(hops.size() * 4, 256));
-    if (!base) return DM_ERR_NOMEM;
+    const bool p2p = std::any_of(P.hops.begin(), P.hops.end(),
+                                 [](const dm_mig_hop& h) { return h.kind != DM_HOP_LOCAL; });
+    DM_CHECK_ARG(!p2p || comm != nullptr, "cross-rank hops need an RCCL communicator");
+    P.bb = align_up((size_t)block_bytes(&demes[0], k), 256);
+    P.hops_into.assign(n_local, 0);
+    for (const dm_mig_hop& h : P.hops) {
+        P.nrecv += h.kind == DM_HOP_RECV;
+        if (h.kind != DM_HOP_SEND) ++P.hops_into[P.local_of[h.to]];
+    }
+    // dirty-row bitmaps for demes that receive more than one hop
+    size_t dirty_bytes = 0;
+    for (int32_t i = 0; i < n_local; ++i)
+        if (P.hops_into[i] > 1) dirty_bytes += align_up((size_t)(demes[i].n + 63) / 64 * 8, 256);
+    // [emigrant block | immigrant block] per local deme, then one per receive,
+    // the placement slots, the per-hop status words, the dirty bitmaps
+    P.base = (char*)scratch_slot(ctx, 4, P.bb * (2 * (size_t)n_local + P.nrecv) +
+                                             align_up((size_t)k * 4, 256) +
+                                             align_up(P.hops.size() * 4, 256) + dirty_bytes);
+    if (!P.base) return DM_ERR_NOMEM;
+    return DM_OK;
+}
+
+// All ranks of the communicator agree that every rank prepared its part of
+// the migration (min-reduction of a flag over RCCL on the ctx stream) before
+// any rank posts a send or receive; a rank whose check failed reports its own
+// error, the others a ValueError naming the failure elsewhere.
+static int mig_agree(dm_ctx* ctx, dm_comm* comm, bool ok_here, bool* ok_all) {
+    hipStream_t s = ctx->stream;
+    DM_HIP(hipMemsetAsync(comm->flag, ok_here ? 1 : 0, sizeof(int32_t), s));
+    DM_NCCL(ncclAllReduce(comm->flag, comm->flag, 1, ncclInt32, ncclMin, comm->comm, s));
+    int32_t v = 0;
+    DM_HIP(hipMemcpyAsync(&v, comm->flag, sizeof(v), hipMemcpyDeviceToHost, s));
+    DM_HIP(hipStreamSynchronize(s));
+    *ok_all = v != 0;
+    return DM_OK;
+}
+
+static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
+                         const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
+                         const int32_t* owner, int64_t k, int32_t* const* emig_idx,
+                         int32_t* const* immig_idx, int32_t* const* out_slots, int32_t flags) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    MigPlan P;
+    int rc = mig_prepare(ctx, comm, n_local, demes, deme_ids, n_demes, migarray, owner, k,
+                         emig_idx, flags, P);
+    if (comm && comm->nranks > 1) {
+        std::string mine = rc ? std::string(dm_last_error()) : std::string();
+        bool all = false;
+        int arc = mig_agree(ctx, comm, rc == DM_OK, &all);
+        if (arc) return arc;
+        if (rc) {
+            set_error("%s", mine.c_str());
+            return rc;
+        }
+        DM_CHECK_ARG(all, "migRing: another rank rejected this migration (see its error)");
+    } else if (rc) {
+        return rc;
+    }
+    if (k == 0 || n_local == 0) return DM_OK;
+    const std::vector<dm_mig_hop>& hops = P.hops;
+    const std::vector<int32_t>& local_of = P.local_of;
+    const size_t bb = P.bb;
+    char* base = P.base;
     hipStream_t s = ctx->stream;
     std::vector<char*> emig(n_local), immig(n_local);
     // migration.py:39-46: every deme's emigrants / immigrants first
@@ -551,10 +629,8 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
     }
     // exchange: the incoming block of every hop into a local deme
     std::vector<char*> incoming(hops.size(), nullptr);
-    const bool p2p = std::any_of(hops.begin(), hops.end(),
-                                 [](const dm_mig_hop& h) { return h.kind != DM_HOP_LOCAL; });
-    if (p2p) {
-        DM_CHECK_ARG(comm != nullptr, "cross-rank hops need an RCCL communicator");
+    if (P.nrecv || std::any_of(hops.begin(), hops.end(),
+                               [](const dm_mig_hop& h) { return h.kind == DM_HOP_SEND; })) {
         const size_t bytes = (size_t)block_bytes(&demes[0], k);
         char* rb = base + 2 * (size_t)n_local * bb;
         DM_NCCL(ncclGroupStart());
@@ -574,14 +650,24 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
         if (hops[h].kind == DM_HOP_LOCAL) incoming[h] = emig[local_of[hops[h].from]];
     // migration.py:48-51: placements in from_deme order, asynchronous; one
     // status word per hop, copied back and checked once at the end
-    int32_t* slot_scratch = (int32_t*)(base + 2 * (size_t)n_local * bb + (size_t)nrecv * bb);
-    int32_t* errs = slot_scratch + align_up((size_t)k, 64);
+    int32_t* slot_scratch = (int32_t*)(base + 2 * (size_t)n_local * bb + (size_t)P.nrecv * bb);
+    int32_t* errs = (int32_t*)((char*)slot_scratch + align_up((size_t)k * 4, 256));
+    char* dptr = (char*)errs + align_up(hops.size() * 4, 256);
+    std::vector<unsigned long long*> dirty(n_local, nullptr);
+    for (int32_t i = 0; i < n_local; ++i) {
+        if (P.hops_into[i] <= 1) continue;
+        const size_t db = (size_t)(demes[i].n + 63) / 64 * 8;
+        dirty[i] = (unsigned long long*)dptr;
+        DM_HIP(hipMemsetAsync(dirty[i], 0, db, s));
+        dptr += align_up(db, 256);
+    }
     DM_HIP(hipMemsetAsync(errs, 0, hops.size() * 4, s));
     for (size_t h = 0; h < hops.size(); ++h) {
         if (!incoming[h]) continue;
         const int32_t t = local_of[hops[h].to];
         int32_t* slots = out_slots && out_slots[t] ? out_slots[t] : slot_scratch;
-        if ((rc = mig_place_async(ctx, &demes[t], immig[t], incoming[h], k, slots, errs + h)))
+        if ((rc = mig_place_async(ctx, &demes[t], immig[t], incoming[h], k, slots, dirty[t],
+                                  errs + h)))
             return rc;
     }
     std::vector<int32_t> herr(hops.size(), 0);
@@ -654,6 +740,12 @@ extern "C" int dm_comm_init(dm_ctx* ctx, int32_t nranks, int32_t rank, const uin
     }
     c->nranks = nranks;
     c->rank = rank;
+    if (hipMalloc(&c->flag, 256) != hipSuccess) {
+        set_error("hipMalloc of the communicator's flag word failed");
+        ncclCommDestroy(c->comm);
+        delete c;
+        return DM_ERR_NOMEM;
+    }
     *out = c;
     return DM_OK;
 }
@@ -661,6 +753,7 @@ extern "C" int dm_comm_init(dm_ctx* ctx, int32_t nranks, int32_t rank, const uin
 extern "C" int dm_comm_destroy(dm_comm* comm) {
     if (!comm) return DM_OK;
     ncclResult_t r = comm->comm ? ncclCommDestroy(comm->comm) : ncclSuccess;
+    if (comm->flag) (void)hipFree(comm->flag);
     delete comm;
     if (r != ncclSuccess) {
         set_error("ncclCommDestroy failed: %s", ncclGetErrorString(r));

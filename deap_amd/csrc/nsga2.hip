@@ -30,7 +30,7 @@ int sort_by_fitness(dm_ctx* ctx, const double* wv, int nobj, int64_t n, bool des
 // device-driven peel
 size_t fast_dom_bytes(int64_t n, int64_t U);
 int64_t fast_dom_words(int64_t U);
-int fast_dom_build(hipStream_t s, int num_cus, const double* wv, int m, int64_t n,
+int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
                    const int32_t* perm, const int32_t* segin, const int32_t* uidx,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
@@ -523,7 +523,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
     unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
     if (fast) {
-        if ((rc = fast_dom_build(s, ctx->num_cus, wv, m, n, perm, segin, uidx, ufit, U, D, count,
+        if ((rc = fast_dom_build(ctx, wv, m, n, perm, segin, uidx, ufit, U, D, count,
                                  fwork)))
             return rc;
     } else if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {

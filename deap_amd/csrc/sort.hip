@@ -17,9 +17,14 @@ constexpr int RS_BINS = 256;
 constexpr int RS_MAX_PASSES = 8;
 constexpr int RS_HIST_BLOCKS = 512;
 
+// temp layout: global digit histograms | one tile-id counter per pass |
+// look-back status words
+constexpr size_t RS_GHIST_BYTES = (RS_MAX_PASSES * RS_BINS * 4 + 255) / 256 * 256;
+constexpr size_t RS_TICKET_BYTES = 256;
+
 size_t radix_sort_temp_bytes(int64_t n) {
     const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
-    return align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256) +
+    return RS_GHIST_BYTES + RS_TICKET_BYTES +
            align_up((size_t)tiles * RS_MAX_PASSES * RS_BINS * 4, 256);
 }
 
@@ -49,11 +54,17 @@ constexpr uint32_t RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_COUNT = (1u << 30
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
     uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n, int shift,
-    const int32_t* __restrict__ ghist, uint32_t* status) {
+    const int32_t* __restrict__ ghist, uint32_t* status, uint32_t* ticket) {
     __shared__ int32_t cnt[RS_ROUNDS][RS_THREADS / 64][RS_BINS];
     __shared__ int32_t gofs[RS_BINS];
+    __shared__ uint32_t tile_id;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t tile = blockIdx.x;
+    // tile ids in the order workgroups START (an atomic ticket, not blockIdx):
+    // every tile a workgroup waits on in the look-back below is then already
+    // running, whatever order the dispatcher launches workgroups in
+    if (tid == 0) tile_id = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = tile_id;
     const int64_t base = tile * RS_TILE;
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r)
@@ -149,10 +160,10 @@ int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* key
     const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
     const int passes = std::min(RS_MAX_PASSES, (end_bit - begin_bit + 7) / 8);
     int32_t* ghist = (int32_t*)temp;
-    uint32_t* status = (uint32_t*)((char*)temp + align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256));
+    uint32_t* ticket = (uint32_t*)((char*)temp + RS_GHIST_BYTES);
+    uint32_t* status = (uint32_t*)((char*)temp + RS_GHIST_BYTES + RS_TICKET_BYTES);
     DM_HIP(hipMemsetAsync(temp, 0,
-                          align_up((size_t)RS_MAX_PASSES * RS_BINS * 4, 256) +
-                              (size_t)passes * tiles * RS_BINS * 4,
+                          RS_GHIST_BYTES + RS_TICKET_BYTES + (size_t)passes * tiles * RS_BINS * 4,
                           s));
     const unsigned hb = (unsigned)std::min<int64_t>(RS_HIST_BLOCKS, (n + RS_THREADS * 8 - 1) / (RS_THREADS * 8));
     rs_hist_kernel<<<hb, RS_THREADS, 0, s>>>(keys, n, begin_bit, passes, ghist);
@@ -163,7 +174,8 @@ int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* key
     for (int p = 0; p < passes; ++p) {
         rs_pass_kernel<<<(unsigned)tiles, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n,
                                                              begin_bit + 8 * p, ghist + p * RS_BINS,
-                                                             status + (size_t)p * tiles * RS_BINS);
+                                                             status + (size_t)p * tiles * RS_BINS,
+                                                             ticket + p);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

@@ -63,9 +63,12 @@ def migRingDistributed(demes, deme_ids, n_demes, k, selection, replacement=None,
                        "emigrants": [e.cpu().numpy().copy() for e in e_idx],
                        "immigrants": [None if i is None else i.cpu().numpy().copy()
                                       for i in i_idx]})
-    if _uses_rccl(demes, group) or (world == 1 and force_p2p):
-        comm = rccl_comm(demes[0], group) if demes else None
-        _mig_ring_rccl(comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_idx,
+    if _uses_rccl(group) or (world == 1 and force_p2p):
+        # every rank takes this route (the choice depends on the backend only)
+        # and joins the communicator, a rank without demes included
+        ctx = demes[0].ctx if demes else _current_ctx()
+        comm = rccl_comm(ctx, group)
+        _mig_ring_rccl(ctx, comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_idx,
                        force_p2p)
         return
     # host-staged route (gloo / CPU backends)
@@ -81,10 +84,17 @@ def migRingDistributed(demes, deme_ids, n_demes, k, selection, replacement=None,
             place(local[to], immig[to], received[(frm, to)], k)
 
 
-def _uses_rccl(demes, group):
-    if not dist.is_initialized() or not demes:
-        return False
-    return dist.get_backend(group) == "nccl" and demes[0].device.type == "cuda"
+def _uses_rccl(group):
+    """RCCL route iff the process group's backend is nccl (= RCCL on ROCm).
+    Decided from the backend alone so that every rank — one that holds no
+    deme included — takes the same route (the communicator set-up and the
+    exchange are collective)."""
+    return dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+
+def _current_ctx():
+    from .device import Context
+    return Context.get()
 
 
 def route_blocks(emig, make_recv, owner, migarray, me, group=None):
@@ -190,12 +200,22 @@ class RcclComm:
 _COMMS = {}
 
 
-def rccl_comm(pop, group=None):
-    key = (id(group), pop.device.index, dist.is_initialized())
+def rccl_comm(ctx, group=None):
+    """The communicator of (process group, device), created on first use
+    (collective: every rank of the group calls this in the same migration)."""
+    key = (id(group), ctx.device.index, dist.is_initialized())
     c = _COMMS.get(key)
     if c is None:
-        c = _COMMS[key] = RcclComm(pop.ctx, group)
+        c = _COMMS[key] = RcclComm(ctx, group)
     return c
+
+
+def close_comms():
+    """Destroy every communicator this process created (before
+    ``dist.destroy_process_group``)."""
+    while _COMMS:
+        _, c = _COMMS.popitem()
+        c.close()
 
 
 def _ptr_array(tensors):
@@ -205,7 +225,8 @@ def _ptr_array(tensors):
     return arr
 
 
-def _mig_ring_rccl(comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_idx, force_p2p):
+def _mig_ring_rccl(ctx, comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_idx,
+                   force_p2p):
     n_local = len(demes)
     pops = (_lib.DevicePop * max(n_local, 1))(*[p.c_pop() for p in demes])
     ids = (ctypes.c_int32 * max(n_local, 1))(*deme_ids)
@@ -213,8 +234,7 @@ def _mig_ring_rccl(comm, demes, deme_ids, n_demes, migarray, owner, k, e_idx, i_
     own = (ctypes.c_int32 * n_demes)(*[owner[d] for d in range(n_demes)])
     e_idx = [e.to(torch.int32).contiguous() for e in e_idx]
     i_idx = [None if i is None else i.to(torch.int32).contiguous() for i in i_idx]
-    ctx = demes[0].ctx.bind() if demes else None
-    _lib.call("dm_mig_ring_rccl", ctx, comm.handle, n_local, pops, ids, n_demes, mig, own, int(k),
+    _lib.call("dm_mig_ring_rccl", ctx.bind(), comm.handle, n_local, pops, ids, n_demes, mig, own, int(k),
               _ptr_array(e_idx), _ptr_array(i_idx), None,
               _lib.DM_MIG_FORCE_P2P if force_p2p else 0)
 
@@ -261,7 +281,10 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
     for name, v in zip(("k", "selection", "replacement", "migarray"), mig_a):
         mig_kw[name] = v
     steps = [GenerationStep(d, toolbox, cxpb, mutpb) for d in demes]
-    nev = torch.zeros((len(demes), ngen + 1), dtype=torch.int64, device=demes[0].device)
+    # a rank may hold no deme (any split, owner_map): it still joins every
+    # migration, which is collective
+    dev = demes[0].device if demes else torch.device("cuda", torch.cuda.current_device())
+    nev = torch.zeros((len(demes), ngen + 1), dtype=torch.int64, device=dev)
     logbook = Logbook()
     logbook.header = ["gen", "deme", "evals"] + (stats.fields if stats else [])
     recs = []
@@ -291,7 +314,8 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
                     and not force_p2p:
                 mig_op(demes, stream=streams[0], record=record, **mig_kw)
             else:
-                migRingDistributed(demes, deme_ids, n_demes, stream=streams[0], group=group,
+                migRingDistributed(demes, deme_ids, n_demes,
+                                   stream=streams[0] if streams else None, group=group,
                                    record=record, force_p2p=force_p2p, **mig_kw)
             if callback is not None:
                 callback(gen, "migration", demes)
@@ -322,4 +346,4 @@ def mig_plan(n_demes, migarray, owner, me, force_p2p=False):
 
 
 __all__ = ["migRingDistributed", "eaSimpleDemes", "route_blocks", "owner_map", "mig_plan",
-           "RcclComm"]
+           "RcclComm", "close_comms"]

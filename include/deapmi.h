@@ -153,6 +153,11 @@ int dm_ctx_sync(dm_ctx* ctx);  /* hipStreamSynchronize on the ctx stream */
  * recorded. */
 int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches);
 int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count);
+/* Which launches the event pairs bracket: DM_TIME_GENERATION (default, the
+ * dm_generation kernel) or DM_TIME_DOMINANCE (the integer-rank dominance
+ * kernel of dm_sort_nondominated / dm_sel_nsga2). */
+enum dm_time_target { DM_TIME_GENERATION = 0, DM_TIME_DOMINANCE = 1 };
+int dm_ctx_set_timing_target(dm_ctx* ctx, int32_t target);
 
 /* ---- RNG (test + init) ---------------------------------------------------- */
 /* Raw Philox4x32-10 blocks: out[i*4..i*4+3] = philox(ctr_i, key) with

@@ -120,3 +120,35 @@ def test_hall_of_fame_on_host_lists():
     hof.update(pop)
     # value pinned against the reference HallOfFame (bisect_right insertion)
     assert [list(i) for i in hof] == [[4], [2]]
+
+
+def test_checkpoint_reference_types_keep_order_and_chapters():
+    """export_reference_dict hands DEAP a tools.HallOfFame / tools.Logbook
+    (checkpoint.rst:21-65): to_reference_types rebuilds them through the
+    given module's classes — here deap_amd.tools, which mirrors DEAP's API —
+    with equal-fitness entries in the same order, the same similar() and the
+    logbook's records, header, chapters and stream position."""
+    import operator
+    from deap_amd import checkpoint, tools
+    creator.create("FMaxC", base.Fitness, weights=(1.0,))
+    creator.create("IndC", list, fitness=creator.FMaxC)
+    pop = []
+    for genes, v in (([1], 1.0), ([2], 5.0), ([3], 5.0), ([4], 4.0), ([5], 5.0)):
+        ind = creator.IndC(genes)
+        ind.fitness.values = (v,)
+        pop.append(ind)
+    hof = tools.HallOfFame(4)
+    hof.update(pop)
+    log = tools.Logbook()
+    log.header = ["gen", "fit"]
+    log.record(gen=0, fit={"max": 1.0})
+    log.record(gen=1, fit={"max": 2.0})
+    _ = log.stream
+    h2, l2 = checkpoint.to_reference_types(hof, log, tools)
+    assert type(h2) is tools.HallOfFame and type(l2) is tools.Logbook
+    assert [list(i) for i in h2] == [list(i) for i in hof]
+    assert h2.maxsize == 4 and h2.similar is operator.eq
+    assert list(l2) == list(log) and l2.header == log.header and l2.buffindex == log.buffindex
+    assert l2.chapters["fit"].select("max") == [1.0, 2.0]
+    h3, l3 = checkpoint.to_reference_types(None, None, tools)
+    assert h3 is None and l3 is None

@@ -1,0 +1,145 @@
+"""Islands across processes with the real device kernels (the
+device pack / placement under a multi-rank ``migRingDistributed`` had only
+run with host stand-ins).
+
+Two processes share the one GPU of the test box (RCCL refuses two ranks on
+one device, so the process group is ``gloo`` and the emigrant blocks are
+host-staged by ``route_blocks``; every pack, selection and placement is the
+device kernel of ``libdeapmi.so``).  Each rank runs ``eaSimpleDemes`` on its
+share of 4 OneMax demes with migRing every 5 generations
+(``examples/ga/onemax_multidemic.py:79-93``, ``deap/tools/migration.py:4-51``).
+Philox streams are keyed by the deme id, so the split over ranks cannot
+change a single bit: the result must equal the one-process run, which
+``test_gpu_islands.py`` replays in the oracle.  Splits include a rank that
+holds no deme (it must still join every migration)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_DEMES, N, DIM, NGEN, K = 4, 96, 100, 12, 5
+
+
+def _toolbox():
+    from deap_amd import base, benchmarks, tools
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.onemax)
+    tb.register("mate", tools.cxTwoPoint)
+    tb.register("mutate", tools.mutFlipBit, indpb=0.05)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("migrate", tools.migRing, k=K, selection=tools.selBest)
+    return tb
+
+
+def _evolve(ids, n_demes=N_DEMES, migarray=None):
+    from deap_amd import islands, tools
+    from deap_amd.ops import RandomStream
+    streams = [RandomStream(64, island=d) for d in ids]
+    demes = [tools.initPopulation(n=N, dim=DIM, low=0, high=1, gtype="bits", weights=(1.0,),
+                                  stream=s) for s in streams]
+    tb = _toolbox()
+    if migarray is not None:
+        tb.register("migrate", tools.migRing, k=K, selection=tools.selBest, migarray=migarray)
+    demes, log = islands.eaSimpleDemes(demes, tb, 0.5, 0.2, NGEN, mig_every=5, deme_ids=ids,
+                                       n_demes=n_demes, streams=streams)
+    return {d: p.to_numpy() for d, p in zip(ids, demes)}, log
+
+
+def _worker(rank, world, port, ids_by_rank, migarray, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        got, log = _evolve(ids_by_rank[rank], migarray=migarray)
+        q.put((rank, {d: (g, wv) for d, (g, wv, _) in got.items()},
+               [(r["gen"], r["deme"], r["evals"]) for r in log]))
+    except BaseException as e:  # report instead of leaving the parent waiting
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("ids_by_rank,migarray", [
+    ([[0, 1], [2, 3]], None),          # even split, ring crosses ranks twice
+    ([[0, 2], [1, 3]], None),          # interleaved: every hop is cross-rank
+    ([[0, 1, 2, 3], []], None),        # rank 1 holds no deme
+    ([[3], [0, 1, 2]], [2, 3, 1, 0]),  # uneven split, another permutation
+])
+def test_two_ranks_equal_one_process(gpu, ids_by_rank, migarray):
+    import torch.multiprocessing as mp
+    want, want_log = _evolve(list(range(N_DEMES)), migarray=migarray)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ids_by_rank, migarray, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got, logs = {}, []
+    try:
+        for _ in procs:
+            rank, part, log = q.get(timeout=100)
+            assert isinstance(part, dict), "rank %d failed: %s" % (rank, part)
+            got.update(part)
+            logs.extend(log)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    assert sorted(got) == list(range(N_DEMES))
+    for d in range(N_DEMES):
+        assert np.array_equal(got[d][0], want[d][0]), "deme %d genomes" % d
+        assert np.array_equal(got[d][1], want[d][1]), "deme %d fitness" % d
+    assert sorted(logs) == sorted((r["gen"], r["deme"], r["evals"]) for r in want_log)
+
+
+def test_second_hop_into_a_deme_has_no_identity_match(gpu):
+    """migarray [1, 1, 0]: deme 1 receives twice.  Its immigrant row 2 holds a
+    NaN genome, so list.index finds it only by identity.  The first hop
+    (0 -> 1) overwrites that row; on the second hop (1 -> 1) the immigrant
+    object is no longer in the list and ``populations[1].index(immigrant)``
+    raises ValueError (deap/tools/migration.py:48-51, restated below with
+    Python lists of the same objects).  The device must not match the
+    overwritten row by its old identity."""
+    import torch
+    from deap_amd import tools
+    from deap_amd.device import DevicePopulation
+
+    genes = [np.arange(12, dtype=np.float64).reshape(3, 4) + 100 * d for d in range(3)]
+    genes[1][2, 0] = np.nan
+    demes = [DevicePopulation.from_numpy(g, (1.0,), wvalues=g[:, 1:2] if d != 1 else
+                                         np.array([[0.], [1.], [5.]]), valid=np.ones(3))
+             for d, g in enumerate(genes)]
+    # the reference's loop over host objects
+    host = [[list(r) for r in g] for g in genes]
+    em = [[host[0][2]], [host[1][2]], [host[2][2]]]   # selBest(k=1) of each deme
+    ref_err = None
+    try:
+        for frm, to in enumerate([1, 1, 0]):
+            for i, imm in enumerate(em[to]):
+                host[to][host[to].index(imm)] = em[frm][i]
+    except ValueError as e:
+        ref_err = e
+    assert ref_err is not None
+
+    # selBest(k=1) picks row 2 of every deme (the largest weighted fitness)
+    with pytest.raises(ValueError):
+        tools.migRing(demes, 1, tools.selBest, migarray=[1, 1, 0])
+    # the first hop was applied before the failing lookup, as in the reference
+    g1, _, _ = demes[1].to_numpy()
+    assert np.array_equal(g1[2], genes[0][2])
+    del torch

@@ -614,9 +614,15 @@ def test_checkpoint_reference_dict_round_trip(gpu):
                                      stream=stream2)
     before = pop2.to_numpy()
     cp = checkpoint.export_reference_dict(pop2, 2, hof, log2, stream2)
-    assert set(cp) == {"population", "generation", "halloffame", "logbook", "rndstate"}
+    assert set(cp) == {"population", "generation", "halloffame", "logbook", "rndstate",
+                       "device_stream"}
     assert len(cp["population"]) == 513 and all(i.fitness.valid for i in cp["population"])
     cp = pickle.loads(pickle.dumps(cp))
+    # the tutorial's resume line (checkpoint.rst:32) accepts rndstate
+    import random
+    state = random.getstate()
+    random.setstate(cp["rndstate"])
+    random.setstate(state)
     back = checkpoint.import_reference_dict(cp, device=pop2.device)
     for a, b in zip(before, back["population"].to_numpy()):
         assert np.array_equal(a, b)
