@@ -166,7 +166,17 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
             // one launch: decisions drawn inside the burst kernel (+ the
             // nevals reduction of its per-workgroup partials)
             const bool count = ec != EC_NONE && a.nevals && !std::getenv("DM_BITS_NOCOUNT");
+            // tournaments read the parents' fitness through int16 keys (one
+            // coalesced pass, timed with the generation kernel)
+            static const bool no_keys = std::getenv("DM_BITS_NOKEYS") != nullptr;
+            const bool keys = sel == DM_SEL_TOURNAMENT && a.w0 != 0.0 && !no_keys;
+            if (keys) {
+                int16_t* kb = (int16_t*)scratch(ctx, (size_t)a.np * 2 + 16);
+                if (!kb) return DM_ERR_NOMEM;
+                a.pkeys = kb;
+            }
             timing_begin(ctx);
+            if (keys) launch_fit_keys(a, (int16_t*)a.pkeys, ctx->stream);
             launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
                                   ctx->stream);
             timing_end(ctx);

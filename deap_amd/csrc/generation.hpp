@@ -37,6 +37,9 @@ struct GenArgs {
     float flip_inv_log2;  // 1 / log2(1 - indpb) for geometric skips
     int32_t eval_fn;
     double w0;  // ev.weights[0]
+    // C2 fitness keys (fit_key_kernel, generation_pipe_bits.hip): the parents'
+    // wvalues as exact int16 multiples of |w0| (or FIT_KEY_NONE), nullable
+    const int16_t* pkeys;
     dm_eval ev;
     Rng rng;
     const double* zig;

@@ -187,6 +187,60 @@ __global__ __launch_bounds__(256) void gen_bits_burst_kernel(GenArgs a, const Pa
 // Same Philox counters as pair_plan_kernel / gen_bits_kernel: bit-identical
 // children (tests/test_gpu_parity.py::test_native_hot_kernel_equals_replay_kernel).
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Parent fitness keys.  The tournaments read t random parent fitnesses per
+// child; as 8-B loads from the 8 MiB wvalues array (2^20 rows) each pulls a
+// whole line past the 4 MiB L2 of its XCD (PMC: 1.31x the algorithmic bytes,
+// profiles/r02x).  OneMax fitnesses are small integers times the weight, so
+// one coalesced pass writes every parent's wvalue as an int16 q with
+// wv == q * |w0| EXACTLY (2 MiB, L2-resident), or FIT_KEY_NONE when the row
+// is invalid or its value is not such a multiple.  The tournament rebuilds
+// the exact fp64 wvalue from the key (falls back to wvalues / valid for
+// FIT_KEY_NONE), so the comparisons are the reference's own
+// (Fitness.__gt__ on wvalues, selection.py:68), not an approximation.
+// ---------------------------------------------------------------------------
+constexpr int16_t FIT_KEY_NONE = -32768;
+
+__global__ __launch_bounds__(256) void fit_key_kernel(const double* __restrict__ wv,
+                                                      const uint8_t* __restrict__ valid, int64_t n,
+                                                      double scale, int16_t* __restrict__ keys) {
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i0 >= n) return;
+    int16_t k[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        k[j] = FIT_KEY_NONE;
+        const int64_t i = i0 + j;
+        if (i < n && valid[i]) {
+            const double v = wv[i];
+            const double q = rint(v / scale);
+            if (fabs(q) <= 32767.0 && q * scale == v) k[j] = (int16_t)q;
+        }
+    }
+    if (i0 + 3 < n) {
+        *reinterpret_cast<uint64_t*>(keys + i0) =
+            (uint64_t)(uint16_t)k[0] | ((uint64_t)(uint16_t)k[1] << 16) |
+            ((uint64_t)(uint16_t)k[2] << 32) | ((uint64_t)(uint16_t)k[3] << 48);
+    } else {
+        for (int j = 0; j < 4 && i0 + j < n; ++j) keys[i0 + j] = k[j];
+    }
+}
+
+void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s) {
+    const int64_t threads = (a.np + 3) / 4;
+    fit_key_kernel<<<dim3((unsigned)((threads + 255) / 256)), 256, 0, s>>>(
+        a.pwv, a.pvalid, a.np, fabs(a.w0), keys);
+}
+
+// wvalue of parent k: from its key when it has one (exact), else wvalues
+__device__ __forceinline__ double parent_fit(const GenArgs& a, int32_t k) {
+    if (a.pkeys) {
+        const int16_t q = a.pkeys[k];
+        if (q != FIT_KEY_NONE) return (double)q * fabs(a.w0);
+    }
+    return a.pwv[k];
+}
+
 // Decision draws of one group (PP pairs) of a wave, before the tournament:
 // the Philox words of every lane and the aspirants' fitness loads in flight.
 struct BitsDraw {
@@ -247,10 +301,10 @@ __device__ __forceinline__ BitsDraw bits_draw(const GenArgs& a, int64_t p0, int 
     // selection lanes: both aspirants of the call and their fitness
     if (draw && lane < CXL) {
         d.k0 = (int32_t)bounded64(w.x, w.y, np);
-        d.f0 = (DM_BITS_ABLATE & 2) ? (double)(d.k0 & 255) : a.pwv[d.k0];
+        d.f0 = (DM_BITS_ABLATE & 2) ? (double)(d.k0 & 255) : parent_fit(a, d.k0);
         if (2 * (int)sub + 1 < t) {
             d.k1 = (int32_t)bounded64(w.z, w.w, np);
-            d.f1 = (DM_BITS_ABLATE & 2) ? (double)(d.k1 & 255) : a.pwv[d.k1];
+            d.f1 = (DM_BITS_ABLATE & 2) ? (double)(d.k1 & 255) : parent_fit(a, d.k1);
         }
     }
     // crossover lanes CXL..CXL+PP-1: flag and cxTwoPoint cuts of pair L - CXL
@@ -310,7 +364,8 @@ __device__ __forceinline__ void bits_resolve(const GenArgs& a, const BitsDraw& d
     // the winner's validity is only needed for the fitness store: loaded with
     // the rows, off the decision chain (one random byte per child, not t)
     g.v = 1;
-    if (live && !(g.cx_c || g.mut)) g.v = a.pvalid[k];
+    if (live && !(g.cx_c || g.mut))
+        g.v = (a.pkeys && a.pkeys[k] != FIT_KEY_NONE) ? 1u : a.pvalid[k];
     const int64_t npairs = (a.nc + 1) / 2;
     const bool lw = lane < a.words64;
 #pragma unroll

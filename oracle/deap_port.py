@@ -330,8 +330,9 @@ def assign_crowding_dist(individuals):
         individuals[i].fitness.crowding_dist = d
 
 
-def sel_nsga2(individuals, k, nd="standard"):
-    """emo.py:15-50."""
+def sel_nsga2(individuals, k, nd="standard", return_fronts=False):
+    """emo.py:15-50.  ``return_fronts``: also return the sorted fronts (test
+    use: one sort serves both checks)."""
     if nd == "standard":
         fronts = sort_nondominated(individuals, k)
     elif nd == "log":
@@ -345,7 +346,7 @@ def sel_nsga2(individuals, k, nd="standard"):
     if rest > 0:
         last = sorted(fronts[-1], key=lambda ind: ind.fitness.crowding_dist, reverse=True)
         chosen.extend(last[:rest])
-    return chosen
+    return (chosen, fronts) if return_fronts else chosen
 
 
 # Fortin et al. (2013), generalised reduced run-time non-dominated sort, as

@@ -159,3 +159,66 @@ def test_sort_nondominated_objective0_ties(gpu, monkeypatch):
     ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
     assert fast == ref
     assert sum(len(f) for f in fast) == n
+
+
+def _shell_fitness(n, m, seed, levels=12):
+    """Directions on the positive unit sphere scaled by one of a few radii:
+    fronts of thousands of members (the member-slice peel path, >= 1,024
+    members per 1,024-v segment)."""
+    rng = np.random.default_rng(seed)
+    d = np.abs(rng.normal(size=(n, m)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return d * (1.0 + 0.02 * rng.integers(0, levels, size=(n, 1)))
+
+
+@pytest.mark.parametrize("n,m,kind", [(1 << 18, 3, "sphere"), (40000, 3, "shells"),
+                                      (40000, 2, "shells")])
+def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
+    """C5 at its benched size against a reference-pinned restatement (VERDICT r2
+    item 2): ``oracle/deap_port.py``'s Fortin log sort and selNSGA2 (bit-exact
+    with the reference on tests/golden/nsga2*.npz, test_support_port.py) on
+    the same 2N fitnesses (deap/tools/emo.py:15-50, 53-117, 234-276):
+
+    * device ``sortLogNondominated`` fronts == the port's, member for member;
+    * device ``selNSGA2(nd='log')`` chosen order == the port's;
+    * every device ``sortNondominated`` front (integer-rank dominance tiles +
+      device peel, the benched path) == the port's front as a set (the ranks
+      are identical; only the order inside a front differs between the two
+      reference sorts);
+    * the standard selNSGA2's crowding distances == the port's, bitwise, and
+      its chosen set == the port's whenever the crowding value at the cut of
+      the last front is not tied across the cut."""
+    from deap_amd import tools
+    from oracle import deap_port
+    k = n // 2
+    wv = -(_sphere_fitness(n, m, 500 + m) if kind == "sphere" else _shell_fitness(n, m, 600 + m))
+    weights = (-1.0,) * m
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=weights, gtype="f64", wvalues=wv,
+                           valid=np.ones(n))
+    # the port on host individuals (row index kept by identity)
+    inds = deap_port.nsga2_population(wv, weights)
+    row = {id(ind): i for i, ind in enumerate(inds)}
+    ref_chosen, ref_fronts = deap_port.sel_nsga2(inds, k, "log", return_fronts=True)
+    ref_fronts = [[row[id(x)] for x in f] for f in ref_fronts]
+    ref_chosen = [row[id(x)] for x in ref_chosen]
+    ref_crowd = np.array([getattr(x.fitness, "crowding_dist", np.nan) for x in inds])
+    if kind == "shells":
+        assert max(len(f) for f in ref_fronts) > 1024, [len(f) for f in ref_fronts]
+    # log sort: exact order
+    got_log = [f.cpu().numpy().tolist() for f in tools.sortLogNondominated(pop, k)]
+    assert [len(f) for f in got_log] == [len(f) for f in ref_fronts]
+    assert got_log == ref_fronts
+    assert tools.selNSGA2(pop, k, nd="log").cpu().numpy().tolist() == ref_chosen
+    # standard sort (the benched path): same fronts as sets
+    got_std = [f.cpu().numpy() for f in tools.sortNondominated(pop, k)]
+    assert len(got_std) == len(ref_fronts)
+    for i, (a, b) in enumerate(zip(got_std, ref_fronts)):
+        assert len(a) == len(b) and set(a.tolist()) == set(b), "front %d" % i
+    chosen = tools.selNSGA2(pop, k).cpu().numpy()
+    crowd = pop.crowding_dist[:n].cpu().numpy()
+    assert np.array_equal(crowd[chosen], ref_crowd[chosen])
+    last = np.array(ref_fronts[-1])
+    need = k - sum(len(f) for f in ref_fronts[:-1])
+    cut = np.sort(ref_crowd[last])[::-1]
+    if need < len(last) and cut[need - 1] != cut[need]:
+        assert set(chosen.tolist()) == set(ref_chosen)

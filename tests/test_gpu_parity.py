@@ -892,3 +892,48 @@ def test_nsga2_example_loop_steps_replay_in_oracle(gpu):
                                valid=np.ones(n, np.uint8))
         pop.crowding_dist = comb.crowding_dist[torch.from_numpy(chosen).long().cuda()].contiguous()
         assert np.allclose(pop.crowding_dist.cpu().numpy(), [ecrowd[i] for i in chosen])
+
+
+@pytest.mark.parametrize("weight", [1.0, -2.5])
+def test_bits_tournament_keys_fall_back_exactly(gpu, weight):
+    """The C2 hot kernel reads parent fitness through int16 keys (exact
+    multiples of |w0|, generation_pipe_bits.hip fit_key_kernel).  Parents
+    whose wvalues are not such multiples (fractions, beyond int16, NaN, -0.0)
+    or whose fitness is invalid take the wvalues / valid fallback: one
+    generation of the native kernel must still equal the dump-mode replay
+    kernel (which reads wvalues directly) bit for bit — genomes, fitness,
+    validity of the clones."""
+    import ctypes
+    import torch
+    from deap_amd import algorithms, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim = 4099, 300
+    sel = np.random.default_rng(5).permutation(n)
+    outs = []
+    for mode in ("native", "dump"):
+        stream = RandomStream(91)
+        pop = tools.initPopulation(n=n, dim=dim, low=0, high=1, gtype="bits", weights=(weight,),
+                                   stream=stream)
+        benchmarks.onemax(pop)
+        wv = pop.wvalues[:n, 0].cpu().numpy().copy()
+        wv[sel[:300]] += 0.25 * weight                    # not a multiple of |w0|
+        wv[sel[300:320]] = 40000.0 * weight               # beyond int16
+        wv[sel[320:330]] = np.nan
+        wv[sel[330:400]] = -0.0
+        valid = np.ones(n, np.uint8)
+        valid[sel[400:500]] = 0                           # invalid parents
+        pop.wvalues[:n, 0].copy_(torch.from_numpy(wv))
+        pop.valid[:n].copy_(torch.from_numpy(valid))
+        tb = _toolbox("twopoint", "flipbit", 0.05, 0.5, evaluate="onemax", tournsize=3)
+        step = algorithms.GenerationStep(pop, tb, 0.5, 0.2)
+        off = pop.like(n, capacity=n)
+        nev = torch.zeros(1, dtype=torch.int64, device=pop.device)
+        decs = [] if mode == "dump" else None
+        step.step(pop, off, stream, ctypes.c_void_p(nev.data_ptr()), mode, decs, 0)
+        outs.append((off.to_numpy(), int(nev.item())))
+    (g1, wv1, ok1), n1 = outs[0]
+    (g2, wv2, ok2), n2 = outs[1]
+    assert np.array_equal(g1, g2)
+    assert np.array_equal(ok1, ok2)
+    assert np.array_equal(wv1, wv2, equal_nan=True)
+    assert n1 == n2
