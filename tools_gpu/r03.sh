@@ -37,6 +37,23 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
       for pmc in FETCH_SIZE WRITE_SIZE; do
         step pmc_${cfg}_$pmc 180 rocprofv3 --pmc $pmc -d $OUT/pmc_${cfg}_$pmc -o run --output-format csv -- python3 bench.py --config $cfg --steps 6 --warmup 1 --no-cpu-baseline
       done ;;
+    alloc)
+      for m in torch raw contig arena; do step alloc_${m}1 240 python tools_gpu/alloc_probe.py $m 1; done
+      step alloc_torch4 300 python tools_gpu/alloc_probe.py torch 4
+      step alloc_arena4 300 python tools_gpu/alloc_probe.py arena 4 ;;
+    counters) step counters 120 rocprofv3 -L ;;
+    pmc_alloc)
+      i=0
+      for pmc in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_TCC_READ_REQ_LATENCY_sum" \
+                 "TCP_TCC_READ_REQ_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE" \
+                 "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum"; do
+        i=$((i+1))
+        step pmc_alloc_$i 240 rocprofv3 --pmc $pmc -d $OUT/pmc_alloc_$i -o run --output-format csv -- python3 tools_gpu/alloc_probe.py torch 4 6
+      done ;;
+    c2ab)
+      step c2_keys 200 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline
+      step c2_nokeys 200 env DM_BITS_NOKEYS=1 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
+    pmc_c5sq) step pmc_c5sq 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS -d $OUT/pmc_c5sq -o run --output-format csv -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
