@@ -183,8 +183,20 @@ __device__ __forceinline__ int32_t writelane(int32_t old, int32_t val) {
     return old;
 }
 
+// Dominator counts.  DM_TD_TCOUNT = 1 (default): after each 64-row block the
+// group's words (lane a: bit j <-> a dominates row j of the block) are
+// transposed across the wave (TransposerX, DPP / permlane moves) so that lane
+// j holds the dominators of row j and counts them with v_bcnt — per block and
+// A-block one transpose (~31 VALU) instead of 64 s_bcnt1 + s_add on the SALU
+// and a v_writelane per row (r02: 1.16e9 SALU beside 1.36e9 VALU
+// instructions per launch, profiles/r03b).  0: the per-row SALU count.
+#ifndef DM_TD_TCOUNT
+#define DM_TD_TCOUNT 1
+#endif
+
 // one row b (ranks y) against the group's lanes: shift the dominance bits
-// into tw, return b's dominator count over the group
+// into tw, return b's dominator count over the group (0 when counted by
+// transposes)
 template <int M, bool STRICT>
 __device__ __forceinline__ int32_t td_row(const int4 y4, const int32_t (&x)[TD_WPW][M],
                                           uint32_t (&tw)[TD_WPW]) {
@@ -212,7 +224,7 @@ __device__ __forceinline__ int32_t td_row(const int4 y4, const int32_t (&x)[TD_W
             msk = __ballot(mn >= 0) & __ballot(mx > 0);
         }
         tw[k] = add2_carry(tw[k], tw[k], msk);
-#ifndef DM_TD_NOCOUNT
+#if !defined(DM_TD_NOCOUNT) && !DM_TD_TCOUNT
         cnt += __popcll(msk);
 #endif
     }
@@ -230,10 +242,15 @@ __device__ __forceinline__ void td_half(const int4* L, const int32_t (&x)[TD_WPW
 #pragma unroll
         for (int i = 0; i < 4; ++i) nxt[i] = L[JTOP - J4 - 4 - i];
     }
-    cpark = writelane<JTOP - J4>(cpark, td_row<M, STRICT>(cur[0], x, tw));
-    cpark = writelane<JTOP - J4 - 1>(cpark, td_row<M, STRICT>(cur[1], x, tw));
-    cpark = writelane<JTOP - J4 - 2>(cpark, td_row<M, STRICT>(cur[2], x, tw));
-    cpark = writelane<JTOP - J4 - 3>(cpark, td_row<M, STRICT>(cur[3], x, tw));
+    if constexpr (DM_TD_TCOUNT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) (void)td_row<M, STRICT>(cur[i], x, tw);
+    } else {
+        cpark = writelane<JTOP - J4>(cpark, td_row<M, STRICT>(cur[0], x, tw));
+        cpark = writelane<JTOP - J4 - 1>(cpark, td_row<M, STRICT>(cur[1], x, tw));
+        cpark = writelane<JTOP - J4 - 2>(cpark, td_row<M, STRICT>(cur[2], x, tw));
+        cpark = writelane<JTOP - J4 - 3>(cpark, td_row<M, STRICT>(cur[3], x, tw));
+    }
     if constexpr (J4 + 4 < 32) td_half<M, STRICT, JTOP, J4 + 4>(L, x, tw, cpark, nxt);
 }
 template <int M, bool STRICT, int JTOP>
@@ -257,7 +274,7 @@ __device__ void td_partial_half(const int4* L, int jtop, int nb,
             continue;
         }
         const int32_t cnt = td_row<M, STRICT>(L[j], x, tw);
-        cpark = (int)(threadIdx.x & 63) == j ? cnt : cpark;
+        if constexpr (!DM_TD_TCOUNT) cpark = (int)(threadIdx.x & 63) == j ? cnt : cpark;
     }
 }
 
@@ -272,6 +289,7 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
                                                       int16_t* __restrict__ part) {
     __shared__ int4 sbuf[4][64];  // per wave: the ranks of the current v block
     const int lane = threadIdx.x & 63;
+    const TransposerX tr(lane);
     int4* L = sbuf[threadIdx.x >> 6];
     const int64_t Upad = NB * 64;
     const int32_t total = toff[ngroups];
@@ -331,6 +349,18 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
             } else {
                 td_partial_half<M, false>(L, 63, nb, x, th, cpark);
                 td_partial_half<M, false>(L, 31, nb, x, tl, cpark);
+            }
+            if constexpr (DM_TD_TCOUNT) {
+                uint32_t lo[TD_WPW], hi[TD_WPW];
+#pragma unroll
+                for (int k = 0; k < TD_WPW; ++k) {
+                    lo[k] = tl[k];
+                    hi[k] = th[k];
+                }
+                tr.run<TD_WPW>(lo, hi);  // lane j: bit a <-> lane a dominates row j
+                cpark = 0;
+#pragma unroll
+                for (int k = 0; k < TD_WPW; ++k) cpark += __popc(lo[k]) + __popc(hi[k]);
             }
             part[g * Upad + B * 64 + lane] = (int16_t)cpark;
             const int bq = (int)(B & 3);
@@ -479,33 +509,71 @@ __device__ __forceinline__ int64_t peel_slices(int64_t F, int64_t s, int64_t NS,
     const int64_t byload = (K * (NS - s) + NS - 1) / NS;
     return std::max<int64_t>(1, std::min<int64_t>(byload, F / PEEL_SLICE_MIN));
 }
-__global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint64_t* __restrict__ D,
-                                                         int64_t NQ,
-                                                         const int2* __restrict__ mrow,
-                                                         const int32_t* __restrict__ gsize,
-                                                         const int32_t* __restrict__ sigma,
-                                                         FrontState* st, int32_t* countq,
-                                                         unsigned long long* lastq,
-                                                         uint64_t* ckey, int32_t* cq,
-                                                         int32_t* rankU) {
-    constexpr int PW = PEEL_WORDS, PV = PW * 64;
-    __shared__ int32_t sdec[PEEL_WAVES][PV];
-    __shared__ int32_t slast[PEEL_WAVES][PV];
-    __shared__ int32_t sF, sust, sstop, snf;
-    if (threadIdx.x == 0) {
-        sF = st->F;
-        sust = st->ustart;
-        snf = st->nfronts;
-        sstop = st->done | st->overflow;
+// Data one phase of the persistent peel hands to another crosses workgroups
+// on different XCDs, whose L2s are not coherent with each other: those
+// accesses are agent-scope relaxed loads / stores (sc1, served coherently)
+// when COH; plain otherwise (separate launches: the kernel boundary makes
+// them visible).
+template <bool COH, typename T>
+__device__ __forceinline__ T cld(const T* p) {
+    if constexpr (COH)
+        return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return *p;
+}
+template <bool COH, typename T>
+__device__ __forceinline__ void cst(T* p, T v) {
+    if constexpr (COH)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+template <bool COH>
+__device__ __forceinline__ int2 cld2(const int2* p) {
+    if constexpr (COH) {
+        const unsigned long long x = __hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(const_cast<int2*>(p)), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        return make_int2((int32_t)(uint32_t)x, (int32_t)(uint32_t)(x >> 32));
+    } else {
+        return *p;
     }
-    __syncthreads();
-    if (sstop) return;
-    const int64_t U = st->U, s = blockIdx.x;
+}
+template <bool COH>
+__device__ __forceinline__ void cst2(int2* p, int2 v) {
+    if constexpr (COH)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                           (unsigned long long)(uint32_t)v.x | ((unsigned long long)(uint32_t)v.y << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+constexpr int PEEL_PV = PEEL_WORDS * 64;                 // v of a row segment
+constexpr int PEEL_IT = PEEL_PV / (PEEL_WAVES * 64);      // v per thread
+struct PeelLds {
+    int32_t sdec[PEEL_WAVES][PEEL_PV];
+    int32_t slast[PEEL_WAVES][PEEL_PV];
+};
+struct PeelSmall {
+    int32_t wcnt[PEEL_IT][PEEL_WAVES];
+    int64_t wgs[PEEL_IT][PEEL_WAVES];
+    int32_t sbase;
+};
+
+// Slice y of the nsl slices of row segment s for the front of sF unique
+// fitnesses starting at sust in ulist / mrow (front number snf).
+template <bool COH>
+__device__ void peel_segment(const uint64_t* __restrict__ D, int64_t NQ, const int2* mrow,
+                             const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
+                             FrontState* st, int32_t* countq, unsigned long long* lastq,
+                             uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t sF,
+                             int32_t sust, int32_t snf, int64_t s, int64_t y, int64_t nsl,
+                             PeelLds& L, PeelSmall& S) {
+    constexpr int PW = PEEL_WORDS, PV = PEEL_PV;
     // members of this workgroup's slice [j0s, F)
-    const int64_t nsl = peel_slices(sF, s, gridDim.x, gridDim.y);
-    if ((int64_t)blockIdx.y >= nsl) return;
     const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
-    const int64_t j0s = blockIdx.y * slen;
+    const int64_t j0s = y * slen;
     const int64_t F = std::min<int64_t>(sF, j0s + slen);
     const int2* members = mrow + sust;  // (row in q order, 512-v halves it reaches)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -522,7 +590,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint6
 #pragma unroll
     for (int b = 0; b < PEEL_BATCH; ++b) {
         const int64_t j = j0s + (int64_t)wave * 64 + b * STEP + lane;
-        mr[b] = j < F ? members[j] : make_int2(0, 0);
+        mr[b] = j < F ? cld2<COH>(members + j) : make_int2(0, 0);
     }
     for (int64_t jb = j0s + (int64_t)wave * 64; jb < F; jb += STEP * PEEL_BATCH) {
         uint4 seg[PEEL_BATCH][PW / 2];
@@ -541,7 +609,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint6
 #pragma unroll
         for (int b = 0; b < PEEL_BATCH; ++b) {
             const int64_t j = jb + (PEEL_BATCH + b) * STEP + lane;
-            mr[b] = j < F ? members[j] : make_int2(0, 0);
+            mr[b] = j < F ? cld2<COH>(members + j) : make_int2(0, 0);
         }
 #pragma unroll
         for (int b = 0; b < PEEL_BATCH; ++b) {
@@ -570,35 +638,31 @@ __global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint6
     }
 #pragma unroll
     for (int w = 0; w < PW; ++w) {
-        sdec[wave][w * 64 + lane] = dec[w];
-        slast[wave][w * 64 + lane] = last[w];
+        L.sdec[wave][w * 64 + lane] = dec[w];
+        L.slast[wave][w * 64 + lane] = last[w];
     }
     __syncthreads();
     // release: one atomic per workgroup on the shared counters (a
     // same-address atomic per wave serialised ~6 ns each over thousands of
     // waves on the large fronts)
-    constexpr int IT = PV / (PEEL_WAVES * 64);
-    __shared__ int32_t wcnt[IT][PEEL_WAVES];
-    __shared__ int64_t wgs[IT][PEEL_WAVES];
-    __shared__ int32_t sbase;
-    bool fresh[IT];
-    int32_t lk[IT], vu[IT];
-    unsigned long long fm[IT];
+    bool fresh[PEEL_IT];
+    int32_t lk[PEEL_IT], vu[PEEL_IT];
+    unsigned long long fm[PEEL_IT];
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < PEEL_IT; ++it) {
         const int t = threadIdx.x + it * PEEL_WAVES * 64;
         int32_t d = 0, l = -1;
 #pragma unroll
         for (int wv = 0; wv < PEEL_WAVES; ++wv) {
-            d += sdec[wv][t];
-            l = max(l, slast[wv][t]);
+            d += L.sdec[wv][t];
+            l = max(l, L.slast[wv][t]);
         }
         const int64_t v = s * PV + t;  // q order
         fresh[it] = false;
         if (v < U && d > 0) {
             if (nsl == 1) {
-                const int32_t left = countq[v] - d;
-                countq[v] = left;
+                const int32_t left = cld<COH>(countq + v) - d;
+                cst<COH>(countq + v, left);
                 fresh[it] = left == 0;
             } else {
                 // several slices: publish the last position, then subtract;
@@ -624,45 +688,73 @@ __global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint6
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
         if (lane == 0) {
-            wcnt[it][wave] = __popcll(fm[it]);
-            wgs[it][wave] = gs;
+            S.wcnt[it][wave] = __popcll(fm[it]);
+            S.wgs[it][wave] = gs;
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t tot = 0;
         int64_t gtot = 0;
-        for (int it = 0; it < IT; ++it)
+        for (int it = 0; it < PEEL_IT; ++it)
             for (int wv = 0; wv < PEEL_WAVES; ++wv) {
-                const int32_t c = wcnt[it][wv];
-                wcnt[it][wv] = tot;
+                const int32_t c = S.wcnt[it][wv];
+                S.wcnt[it][wv] = tot;
                 tot += c;
-                gtot += wgs[it][wv];
+                gtot += S.wgs[it][wv];
             }
-        sbase = tot ? atomicAdd(&st->ncand, tot) : 0;
+        S.sbase = tot ? atomicAdd(&st->ncand, tot) : 0;
         if (gtot) atomicAdd((unsigned long long*)&st->pending, (unsigned long long)gtot);
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < PEEL_IT; ++it) {
         if (!fresh[it]) continue;
         const int64_t v = s * PV + threadIdx.x + it * PEEL_WAVES * 64;
-        const int32_t slot = sbase + wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
-        ckey[slot] = ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it];
-        cq[slot] = (int32_t)v;
-        rankU[vu[it]] = snf + 1;
+        const int32_t slot = S.sbase + S.wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
+        cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
+        cst<COH>(cq + slot, (int32_t)v);
+        cst<COH>(rankU + vu[it], snf + 1);
     }
+    __syncthreads();  // the LDS is reused by the caller's next task
+}
+
+__global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint64_t* __restrict__ D,
+                                                         int64_t NQ,
+                                                         const int2* __restrict__ mrow,
+                                                         const int32_t* __restrict__ gsize,
+                                                         const int32_t* __restrict__ sigma,
+                                                         FrontState* st, int32_t* countq,
+                                                         unsigned long long* lastq,
+                                                         uint64_t* ckey, int32_t* cq,
+                                                         int32_t* rankU) {
+    __shared__ PeelLds L;
+    __shared__ PeelSmall S;
+    __shared__ int32_t sF, sust, sstop, snf;
+    if (threadIdx.x == 0) {
+        sF = st->F;
+        sust = st->ustart;
+        snf = st->nfronts;
+        sstop = st->done | st->overflow;
+    }
+    __syncthreads();
+    if (sstop) return;
+    const int64_t s = blockIdx.x;
+    const int64_t nsl = peel_slices(sF, s, gridDim.x, gridDim.y);
+    if ((int64_t)blockIdx.y >= nsl) return;
+    peel_segment<false>(D, NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU, st->U, sF,
+                        sust, snf, s, blockIdx.y, nsl, L, S);
 }
 
 constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
 
-// Bitonic sort of P = 1024 * E keys held E per thread (element i = tid*E + e),
+// Bitonic sort of P = NT * E keys held E per thread (element i = tid*E + e),
 // ascending: compare-exchanges of stride < E stay in registers, strides below
 // 64 E go through lane shuffles, only the longer ones through LDS (one
 // barrier per stage), so a 2,048-key sort needs 18 barriers instead of 66.
-template <int E>
+template <int NT, int E>
 __device__ void block_bitonic(uint64_t (&k)[E], uint64_t* lds) {
-    constexpr int P = 1024 * E;
+    constexpr int P = NT * E;
     const int tid = threadIdx.x, lane = tid & 63;
     for (int size = 2; size <= P; size <<= 1) {
         int stride = size >> 1;
@@ -671,7 +763,7 @@ __device__ void block_bitonic(uint64_t (&k)[E], uint64_t* lds) {
             for (int e = 0; e < E; ++e) lds[tid * E + e] = k[e];
             __syncthreads();
             for (; stride >= 64 * E; stride >>= 1) {
-                for (int q = tid; q < P / 2; q += 1024) {
+                for (int q = tid; q < P / 2; q += NT) {
                     const int a = 2 * q - (q & (stride - 1));
                     const int b = a + stride;
                     const bool up = (a & size) == 0;
@@ -722,100 +814,102 @@ __device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const 
     return make_int2(r, nseg[r / (64 * TD_WPW)]);
 }
 
-template <int E>
+template <int NT, int E, bool COH>
 __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2* mout,
                              const int32_t* pos, const int32_t* nseg, uint64_t* lds) {
     uint64_t k[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = threadIdx.x * E + e;
-        k[e] = i < n ? ckey[i] : ~0ull;
+        k[e] = i < n ? cld<COH>(ckey + i) : ~0ull;
     }
-    block_bitonic<E>(k, lds);
+    block_bitonic<NT, E>(k, lds);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = threadIdx.x * E + e;
         if (i < n) {
             const int32_t u = (int32_t)(uint32_t)k[e];
-            out[i] = u;
-            mout[i] = member_row(u, pos, nseg);
+            cst<COH>(out + i, u);
+            cst2<COH>(mout + i, member_row(u, pos, nseg));
         }
     }
 }
 
-// Orders the released candidates by (last releasing position, U index),
-// appends them to ulist as the next front and updates the state.
-// presorted: ckey already ordered (the host's radix-sort fallback for fronts
-// larger than ORDER_CAP).
+template <int CAP>
+union OrderLds {
+    uint64_t keys[CAP];
+    struct {
+        int32_t base[CAP + 1];
+        int32_t tmp[CAP];
+    } cs;
+};
+struct OrderScalars {
+    int32_t sn, sgo, snstart, sF, smax;
+};
+
 // Orders the released candidates by (last releasing position l, U index) and
-// appends them to ulist / mrow as the next front.  Counting sort: l < F (the
-// current front's size), so the candidates are binned by l in LDS and ranked
-// inside their bin by U index; a bin of more than ORDER_BIN_MAX candidates
-// (or too many candidates) takes the bitonic sort of the whole key.
-// presorted: ckey already ordered (the host's radix-sort fallback).
+// appends them to ulist / mrow as the next front, then updates the state
+// (one workgroup of NT threads).  Counting sort: l < F (the current front's
+// size), so the candidates are binned by l in LDS and ranked inside their bin
+// by U index; a bin of more than ORDER_BIN_MAX candidates (or too many
+// candidates) takes the bitonic sort of the whole key.  More than CAP
+// candidates: overflow, the host's radix sort orders them (presorted: ckey
+// already ordered).
 constexpr int ORDER_BIN_MAX = 64;
-__global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const uint64_t* ckey,
-                                                           const int32_t* cq, int32_t* ulist,
-                                                           int2* mrow, const int32_t* pos,
-                                                           const int32_t* nseg, int32_t* fstarts,
-                                                           int presorted) {
-    __shared__ union {
-        uint64_t keys[ORDER_CAP];
-        struct {
-            int32_t base[ORDER_CAP + 1];
-            int32_t tmp[ORDER_CAP];
-        } cs;
-    } lds;
-    __shared__ int32_t part[1024];
-    __shared__ int32_t sn, sgo, snstart, sF, smax;
+template <int NT, int CAP, bool COH>
+__device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t* cq,
+                            int32_t* ulist, int2* mrow, const int32_t* pos, const int32_t* nseg,
+                            int32_t* fstarts, int presorted, OrderLds<CAP>& lds, int32_t* part,
+                            OrderScalars& sc) {
     const int tid = threadIdx.x;
     if (tid == 0) {
-        sgo = !(st->done || (st->overflow && !presorted));
-        sn = st->ncand;
-        snstart = st->ustart + st->F;
-        sF = st->F;
-        smax = 0;
+        const int32_t done = cld<COH>(&st->done), ovf = cld<COH>(&st->overflow);
+        sc.sgo = !(done || (ovf && !presorted));
+        sc.sn = cld<COH>(&st->ncand);
+        sc.snstart = cld<COH>(&st->ustart) + cld<COH>(&st->F);
+        sc.sF = cld<COH>(&st->F);
+        sc.smax = 0;
     }
     __syncthreads();
-    if (!sgo) return;
-    const int32_t n = sn;
+    if (!sc.sgo) return;
+    const int32_t n = sc.sn;
     if (n == 0) {  // nothing released: the reference's `if F2 == 0: break`
-        if (tid == 0) st->done = 1;
+        if (tid == 0) cst<COH>(&st->done, 1);
         return;
     }
-    if (!presorted && n > ORDER_CAP) {
-        if (tid == 0) st->overflow = 1;
+    if (!presorted && n > CAP) {
+        if (tid == 0) cst<COH>(&st->overflow, 1);
         return;
     }
-    int32_t* out = ulist + snstart;
-    int2* mout = mrow + snstart;
+    int32_t* out = ulist + sc.snstart;
+    int2* mout = mrow + sc.snstart;
     bool sorted_here = false;
     if (presorted) {
-        for (int i = tid; i < n; i += blockDim.x) {
-            const int32_t u = (int32_t)(uint32_t)ckey[i];
-            out[i] = u;
-            mout[i] = member_row(u, pos, nseg);
+        for (int i = tid; i < n; i += NT) {
+            const int32_t u = (int32_t)(uint32_t)cld<COH>(ckey + i);
+            cst<COH>(out + i, u);
+            cst2<COH>(mout + i, member_row(u, pos, nseg));
         }
         sorted_here = true;
-    } else if (sF <= ORDER_CAP) {
-        constexpr int E = ORDER_CAP / 1024;
-        const int32_t Fr = sF;
-        for (int i = tid; i <= Fr; i += 1024) lds.cs.base[i] = 0;
+    } else if (sc.sF <= CAP) {
+        constexpr int E = CAP / NT;
+        const int32_t Fr = sc.sF;
+        for (int i = tid; i <= Fr; i += NT) lds.cs.base[i] = 0;
         __syncthreads();
         uint64_t key[E];
         int32_t qv[E], slot[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const int i = tid + e * 1024;
+            const int i = tid + e * NT;
             if (i < n) {
-                key[e] = ckey[i];
-                qv[e] = cq[i];
+                key[e] = cld<COH>(ckey + i);
+                qv[e] = cld<COH>(cq + i);
                 slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
             }
         }
         __syncthreads();
         // exclusive prefix of the bin counts: thread t owns C consecutive bins
-        const int C = (Fr + 1023) / 1024;
+        const int C = (Fr + NT - 1) / NT;
         const int b0 = tid * C, b1 = min(Fr, b0 + C);
         int32_t sum = 0, mx = 0;
         for (int b = b0; b < b1; ++b) {
@@ -824,12 +918,12 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
             mx = max(mx, c);
         }
         part[tid] = sum;
-        if (mx > ORDER_BIN_MAX) atomicMax(&smax, mx);
+        if (mx > ORDER_BIN_MAX) atomicMax(&sc.smax, mx);
         __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const int32_t y = tid >= o ? part[tid - o] : 0;
+        for (int o = 1; o < NT; o <<= 1) {
+            const int32_t yv = tid >= o ? part[tid - o] : 0;
             __syncthreads();
-            part[tid] += y;
+            part[tid] += yv;
             __syncthreads();
         }
         int32_t run = part[tid] - sum;
@@ -840,23 +934,23 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
         }
         if (tid == 0) lds.cs.base[Fr] = n;
         __syncthreads();
-        if (smax == 0) {
+        if (sc.smax == 0) {
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const int i = tid + e * 1024;
+                const int i = tid + e * NT;
                 if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
             }
             __syncthreads();
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const int i = tid + e * 1024;
+                const int i = tid + e * NT;
                 if (i < n) {
                     const int32_t l = (int32_t)(key[e] >> 32), vu = (int32_t)(uint32_t)key[e];
                     const int32_t beg = lds.cs.base[l], end = lds.cs.base[l + 1];
                     int32_t r = beg;
                     for (int32_t j = beg; j < end; ++j) r += lds.cs.tmp[j] < vu ? 1 : 0;
-                    out[r] = vu;
-                    mout[r] = make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]);
+                    cst<COH>(out + r, vu);
+                    cst2<COH>(mout + r, make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
                 }
             }
             sorted_here = true;
@@ -865,32 +959,174 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
     }
     if (!sorted_here) {
         uint64_t* keys = lds.keys;
-        if (n <= 1024) {
-            order_sorted<1>(ckey, n, out, mout, pos, nseg, keys);
-        } else if (n <= 2048) {
-            order_sorted<2>(ckey, n, out, mout, pos, nseg, keys);
-        } else if (n <= 4096) {
-            order_sorted<4>(ckey, n, out, mout, pos, nseg, keys);
-        } else if (n <= 8192) {
-            order_sorted<8>(ckey, n, out, mout, pos, nseg, keys);
+        if (n <= NT) {
+            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 2 * NT) {
+            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 4 * NT) {
+            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys);
+        } else if (n <= 8 * NT) {
+            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys);
         } else {
-            order_sorted<16>(ckey, n, out, mout, pos, nseg, keys);
+            static_assert(CAP <= 16 * NT, "order capacity exceeds the bitonic sizes");
+            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys);
         }
     }
     if (tid == 0) {
-        const int32_t nstart = snstart, r = st->nfronts;
-        const int64_t sorted = st->sorted + st->pending;
-        st->sorted = sorted;
-        st->lastinds = st->pending;
-        st->pending = 0;
-        st->ustart = nstart;
-        st->F = n;
-        st->nfronts = r + 1;
-        st->ncand = 0;
-        st->overflow = 0;
-        fstarts[r + 2] = nstart + n;
+        const int32_t nstart = sc.snstart, r = cld<COH>(&st->nfronts);
+        const int64_t pending = (int64_t)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(&st->pending), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t sorted = cld<COH>(&st->sorted) + pending;
+        cst<COH>(&st->sorted, sorted);
+        cst<COH>(&st->lastinds, pending);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&st->pending), 0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cst<COH>(&st->ustart, nstart);
+        cst<COH>(&st->F, n);
+        cst<COH>(&st->nfronts, r + 1);
+        __hip_atomic_store(&st->ncand, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cst<COH>(&st->overflow, 0);
+        cst<COH>(fstarts + r + 2, nstart + n);
         // emo.py:109: continue while pareto_sorted < N (and fronts remain)
-        if (sorted >= st->N || nstart + n >= st->U) st->done = 1;
+        if (sorted >= cld<COH>(&st->N) || nstart + n >= cld<COH>(&st->U)) cst<COH>(&st->done, 1);
+    }
+}
+
+__global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const uint64_t* ckey,
+                                                           const int32_t* cq, int32_t* ulist,
+                                                           int2* mrow, const int32_t* pos,
+                                                           const int32_t* nseg, int32_t* fstarts,
+                                                           int presorted) {
+    __shared__ OrderLds<ORDER_CAP> lds;
+    __shared__ int32_t part[1024];
+    __shared__ OrderScalars sc;
+    order_front<1024, ORDER_CAP, false>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, presorted,
+                                        lds, part, sc);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent peel: ONE cooperative launch peels front after front (VERDICT
+// r2: 58 peel + 58 order launches per selection at ~33 + 8 us each, mostly
+// dispatch and dependent-load latency).  Every workgroup of the co-resident
+// grid takes (segment, slice) tasks of the current front; the workgroup that
+// finishes last orders the released candidates (order_front, NT = the peel's
+// 512 threads, PP_CAP candidates in the peel's LDS) while the others wait for
+// it (front_arrive / front_wait); all read the state and stop together when
+// done (or on an overflow of PP_CAP,
+// which the host's radix sort resolves before relaunching).  Cross-workgroup
+// data moves through sc1 accesses and device atomics (cld / cst), the
+// barrier is an arrival counter; a watchdog turns a barrier that does not
+// complete in ~0.25 s into an error flag instead of a hang.
+// ---------------------------------------------------------------------------
+constexpr int PP_THREADS = PEEL_WAVES * 64;
+constexpr int PP_CAP = 8192;
+struct PersistLds {
+    union {
+        PeelLds peel;
+        OrderLds<PP_CAP> order;
+    } u;
+    PeelSmall ps;
+    OrderScalars os;
+    int32_t part[PP_THREADS];
+    int32_t sF, sust, snf, sstop, ok;
+};
+static_assert(sizeof(PersistLds) <= 80 * 1024, "persistent peel LDS");
+
+// Front barrier of the persistent peel, "last arriver orders": every
+// workgroup arrives once per front (a returning device atomic on bar[0]); the
+// one that completes the count (bar[0] == front * grid) runs the ordering
+// phase itself and then publishes the front number in bar[16]; the others
+// wait for that word.  One barrier per front, no second rendezvous, and the
+// ordering starts the moment the last peel task ends.  Returns -1 when the
+// wait timed out or another workgroup flagged an error (*err set), 1 for the
+// orderer, 0 otherwise.
+__device__ int front_arrive(unsigned* bar, unsigned front, unsigned nwg, int32_t* err,
+                            int32_t& role) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        role = old + 1 == front * nwg ? 1 : 0;
+    }
+    __syncthreads();
+    return role;
+}
+__device__ bool front_wait(unsigned* bar, unsigned front, int32_t* err, int32_t& ok) {
+    if (threadIdx.x == 0) {
+        ok = 1;
+        uint32_t it = 0;
+        while (__hip_atomic_load(bar + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < front) {
+            __builtin_amdgcn_s_sleep(8);
+            if ((++it & 255u) == 0 &&
+                (it > (1u << 19) ||
+                 __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+struct PersistArgs {
+    const uint64_t* D;
+    int64_t NQ;
+    int2* mrow;
+    const int32_t* gsize;
+    const int32_t* sigma;
+    FrontState* st;
+    int32_t* countq;
+    unsigned long long* lastq;
+    uint64_t* ckey;
+    int32_t* cq;
+    int32_t* rankU;
+    int32_t* ulist;
+    const int32_t* pos;
+    const int32_t* nseg;
+    int32_t* fstarts;
+    unsigned* bar;  // zeroed before the launch
+    int32_t* err;   // zeroed before the launch
+};
+
+__global__ __launch_bounds__(PP_THREADS) void peel_persistent_kernel(PersistArgs a) {
+    __shared__ PersistLds L;
+    const unsigned nwg = gridDim.x;
+    const int64_t U = a.st->U;  // set by front_init_kernel (an earlier launch)
+    unsigned epoch = 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            L.sF = cld<true>(&a.st->F);
+            L.sust = cld<true>(&a.st->ustart);
+            L.snf = cld<true>(&a.st->nfronts);
+            L.sstop = cld<true>(&a.st->done) | cld<true>(&a.st->overflow) |
+                      cld<true>(a.err);
+        }
+        __syncthreads();
+        if (L.sstop) break;  // the same state for every workgroup: all stop together
+        const int32_t sF = L.sF, sust = L.sust, snf = L.snf;
+        const int64_t ntask = a.NQ * PEEL_SLICES;
+        for (int64_t t = blockIdx.x; t < ntask; t += nwg) {
+            const int64_t s = t % a.NQ, y = t / a.NQ;
+            const int64_t nsl = peel_slices(sF, s, a.NQ, PEEL_SLICES);
+            if (y >= nsl) continue;
+            peel_segment<true>(a.D, a.NQ, a.mrow, a.gsize, a.sigma, a.st, a.countq, a.lastq,
+                               a.ckey, a.cq, a.rankU, U, sF, sust, snf, s, y, nsl, L.u.peel, L.ps);
+        }
+        ++epoch;
+        if (front_arrive(a.bar, epoch, nwg, a.err, L.ok)) {
+            order_front<PP_THREADS, PP_CAP, true>(a.st, a.ckey, a.cq, a.ulist, a.mrow, a.pos,
+                                                  a.nseg, a.fstarts, 0, L.u.order, L.part, L.os);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(a.bar + 16, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (!front_wait(a.bar, epoch, a.err, L.ok)) {
+            break;
+        }
     }
 }
 
@@ -934,7 +1170,7 @@ static size_t ranks_work_bytes(int64_t n) {
 }
 static size_t fronts_work_bytes(int64_t U) {
     return align_up(sizeof(FrontState), 256) + 3 * align_up((size_t)U * 8, 256) +
-           2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
+           2 * align_up((size_t)U * 4, 256) + 256 + radix_sort_temp_bytes(U);
 }
 static FastLayout fast_layout(int64_t n, int64_t U) {
     FastLayout L;
@@ -1032,6 +1268,29 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
     return DM_OK;
 }
 
+// Integer crowding keys (selNSGA2's fast path): rk[o * T + j] = the dense rank
+// of objective o (weighted-value order, equal values equal ranks) of the
+// emitted individual order[j], from the ranks the dominance pass already
+// holds (S in q order).  assignCrowdingDist's per-objective sorts then run on
+// (front, rank) keys of ~26 bits — 4 radix passes instead of 8 + 1.
+__global__ void rank_keys_kernel(const int4* S, const int32_t* pos, const int32_t* ui,
+                                 const int32_t* order, int64_t T, int m, int32_t* rk) {
+    DGRID_LOOP(j, T) {
+        const int4 r = S[pos[ui[order[j]]]];
+        for (int o = 0; o < m; ++o) rk[o * T + j] = icomp(r, o == 0 ? m - 1 : o - 1);
+    }
+}
+int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, const int32_t* ui,
+                   const int32_t* order, int64_t T, int32_t* rk) {
+    const FastLayout L = fast_layout(n, U);
+    if (T <= 0) return DM_OK;
+    rank_keys_kernel<<<dg1(T), 256, 0, ctx->stream>>>((const int4*)(ws + L.S),
+                                                      (const int32_t*)(ws + L.pos), ui, order, T,
+                                                      m, rk);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
 // Fronts 1.. after front 0 (ulist[0, *F0), rankU set): peel on the device,
 // checking the status every few fronts.  F0 and sorted0 (front 0's unique
 // fitnesses and individuals) stay on the device.  Fills ufront (front starts
@@ -1064,6 +1323,10 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     // sliced peels: per v the max (front + 1, last releasing position)
     unsigned long long* lastq = (unsigned long long*)p;
     p += align_up((size_t)U * 8, 256);
+    // persistent peel: barrier counter and error flag
+    unsigned* bar = (unsigned*)p;
+    int32_t* perr = (int32_t*)(p + 192);  // bar[0]: arrivals, bar[16]: ordered front
+    p += 256;
     void* rtemp = p;
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
@@ -1075,9 +1338,48 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     FrontState* hst = (FrontState*)hbuf;
     int32_t* hfs = (int32_t*)(hbuf + 256);
     const int64_t npre = std::min<int64_t>((2048 - 256) / 4, U + 2);
-    // first status check after as many fronts as the previous call needed
+    // persistent peel (opt-in, DM_PEEL_PERSIST=1): one cooperative launch per
+    // run of fronts (until done, or until a front exceeds PP_CAP candidates).
+    // Measured slower than the launch pair per front on C5 (7.11 vs 6.44 ms
+    // per generation on one box, profiles/r03d): the sc1 member / key traffic
+    // and the barrier polling cost more than the launches they replace.
+    static const bool persist = std::getenv("DM_PEEL_PERSIST") != nullptr;
+    int grid = 0;
+    if (persist) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peel_persistent_kernel,
+                                                         PP_THREADS, 0) == hipSuccess)
+            grid = (int)std::min<int64_t>((int64_t)per_cu * ctx->num_cus, L.NQ * PEEL_SLICES);
+    }
+    while (grid > 0) {
+        DM_HIP(hipMemsetAsync(bar, 0, 256, s));
+        PersistArgs pa{D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU, ulist,
+                       pos, nseg, fstarts, bar, perr};
+        void* kargs[] = {&pa};
+        DM_HIP(hipLaunchCooperativeKernel((const void*)peel_persistent_kernel, dim3((unsigned)grid),
+                                          dim3(PP_THREADS), kargs, 0, s));
+        DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
+        DM_HIP(hipMemcpyAsync(hbuf + 200, perr, 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        if (*(int32_t*)(hbuf + 200)) {
+            set_error("persistent front peel: a grid barrier timed out (grid %d)", grid);
+            return DM_ERR_HIP;
+        }
+        if (hst->done) break;
+        DM_CHECK_ARG(hst->overflow, "persistent front peel stopped before the last front");
+        // a front too large for the in-kernel sort: the radix sort orders its keys
+        const int32_t nc = hst->ncand;
+        DM_HIP(hipMemsetAsync(vals, 0, (size_t)nc * 4, s));
+        int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, nc, 0, 64, rtemp);
+        if (rc) return rc;
+        front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
+        DM_LAUNCH_CHECK();
+    }
+    // multi-launch peel (DM_PEEL_MULTI, or no cooperative grid): first status
+    // check after as many fronts as the previous call needed
     int batch = std::max(2, std::min(ctx->peel_hint + 1, 32));
-    for (;;) {
+    for (; grid == 0;) {
         for (int b = 0; b < batch; ++b) {
             peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
                 D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);

@@ -33,6 +33,8 @@ int64_t fast_dom_words(int64_t U);
 int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
                    const int32_t* perm, const int32_t* segin, const int32_t* uidx,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
+int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, const int32_t* ui,
+                   const int32_t* order, int64_t T, int32_t* rk);
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
@@ -423,11 +425,15 @@ struct SortResult {
     int64_t nsorted = 0;
     int32_t nfronts = 0;
     int64_t last_inds = 0;  // individuals of the last emitted front
+    int64_t U = 0;          // unique fitnesses
+    bool rank_keys = false; // rank_keys filled (fast path)
 };
 
+// rank_keys (nullable, m * n int32): filled with the emitted individuals'
+// per-objective integer ranks when the fast path runs (res->rank_keys).
 static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, bool first_only,
                                   int32_t* order, int32_t* front_start, int32_t* rank,
-                                  SortResult* res) {
+                                  SortResult* res, int32_t* rank_keys = nullptr) {
     hipStream_t s = ctx->stream;
     const int64_t n = pop->n;
     const int m = pop->nobj;
@@ -629,6 +635,13 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         // individuals outside the emitted fronts keep rankU = -1
         ind_rank_kernel<<<g1(n), 256, 0, s>>>(ui, rankU, n, rank);
     }
+    res->U = U;
+    res->rank_keys = false;
+    if (rank_keys && fast && !std::getenv("DM_CROWD_FP")) {
+        if ((rc = fast_rank_keys(ctx, fwork, n, U, m, ui, order, sorted_inds, rank_keys)))
+            return rc;
+        res->rank_keys = true;
+    }
     if (!device_fronts) DM_HIP(hipStreamSynchronize(s));  // ufront host vector goes out of scope
     res->nsorted = sorted_inds;
     res->nfronts = nfronts;
@@ -693,9 +706,22 @@ __global__ void crowd_update_kernel(const double* wv, int m, int obj, Weights wt
     }
 }
 
+// (front, rank) key of objective obj: ascending in the unweighted value
+// (values = wvalues / weights: a negative weight reverses the rank order)
+__global__ void crowd_rank_key_kernel(const int32_t* rk, int64_t U, bool neg, const int32_t* fid,
+                                      const int32_t* pos, int rbits, uint64_t* keys, int64_t T) {
+    GRID_LOOP(j, T) {
+        const int32_t p = pos[j];
+        const uint32_t r = (uint32_t)(neg ? (int32_t)(U - 1) - rk[p] : rk[p]);
+        keys[j] = ((uint64_t)(uint32_t)fid[p] << rbits) | r;
+    }
+}
+
+// rk (nullable): per-objective integer ranks of the T individuals (m x T,
+// sort_nondominated_impl's rank_keys) over U unique fitnesses.
 static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                          const int32_t* order, const int32_t* fstart_dev, int32_t nfronts,
-                         int64_t T, double* crowd) {
+                         int64_t T, double* crowd, const int32_t* rk = nullptr, int64_t U = 0) {
     hipStream_t s = ctx->stream;
     const int m = pop->nobj;
     if (T <= 0 || nfronts <= 0) return DM_OK;
@@ -723,6 +749,27 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
     // position) — one 64-bit sort per objective carried over; the grouping
     // by front (a stable sort by front id) works on a copy.
     iota32_kernel<<<g1(T), 256, 0, s>>>(pos, T);
+    bool zero_w = false;
+    for (int o = 0; o < m; ++o) zero_w = zero_w || weights[o] == 0.0;
+    if (rk && !zero_w) {
+        // sorted by (front, rank_i) carrying the previous objective's order:
+        // within a front lexicographic in (v_i, ..., v_0, position), fronts
+        // grouped — one sort of rbits + fbits bits per objective
+        int rbits = 1;
+        while (rbits < 31 && (1ll << rbits) < U) ++rbits;
+        int kbits = rbits;
+        while (kbits < 64 && (1ll << (kbits - rbits)) <= nfronts) ++kbits;
+        for (int i = 0; i < m; ++i) {
+            crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U, weights[i] < 0.0,
+                                                        fid, pos, rbits, keys, T);
+            int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, kbits, rtemp);
+            if (rc) return rc;
+            crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
+                                                      fstart_dev, T, crowd);
+        }
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
     for (int i = 0; i < m; ++i) {
         crowd_key_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, keys, T);
         int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, 64, rtemp);
@@ -786,14 +833,18 @@ extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weight
     DM_CHECK_ARG(k >= 0, "negative k");
     const int64_t n = pop->n;
     if (n == 0 || k == 0) return DM_OK;
-    // order / front starts outlive the sort's slot-0 workspace: slot 2
-    int32_t* order = (int32_t*)scratch_slot(ctx, 2, (size_t)(2 * n + 2) * 4);
+    // order / front starts / integer crowding keys outlive the sort's slot-0
+    // workspace: slot 2
+    const int m = pop->nobj;
+    int32_t* order = (int32_t*)scratch_slot(ctx, 2, (size_t)(2 * n + 2 + (int64_t)m * n) * 4);
     if (!order) return DM_ERR_NOMEM;
     int32_t* fstart = order + n;
+    int32_t* rkeys = order + 2 * n + 2;
     SortResult r;
-    rc = sort_nondominated_impl(ctx, pop, k, false, order, fstart, nullptr, &r);
+    rc = sort_nondominated_impl(ctx, pop, k, false, order, fstart, nullptr, &r, rkeys);
     if (rc) return rc;
-    rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd);
+    rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd,
+                       r.rank_keys ? rkeys : nullptr, r.U);
     if (rc) return rc;
     // fronts before the last one are taken whole (emo.py:38-40); the sort
     // reports the emitted individuals and the last front's size on the host

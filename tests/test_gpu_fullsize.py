@@ -222,3 +222,96 @@ def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
     cut = np.sort(ref_crowd[last])[::-1]
     if need < len(last) and cut[need - 1] != cut[need]:
         assert set(chosen.tolist()) == set(ref_chosen)
+
+
+def _row_hashes(pop):
+    """int64 hash of every genome row, computed on the device (test
+    infrastructure: a wrapping multiply-add over the row's 64-bit words)."""
+    import torch
+    g = pop.genes[:len(pop)].view(torch.int64)
+    rng = np.random.default_rng(1234)
+    mult = torch.from_numpy(rng.integers(1, 2**62, size=g.shape[1], dtype=np.int64) | 1).to(g.device)
+    out = torch.empty(g.shape[0], dtype=torch.int64, device=g.device)
+    for a in range(0, g.shape[0], 1 << 16):
+        out[a:a + (1 << 16)] = (g[a:a + (1 << 16)] * mult).sum(dim=1)
+    return out.cpu().numpy()
+
+
+def test_c4_migration_at_full_size(gpu):
+    """C4 at its benched size: two demes of 2^20
+    Rastrigin-1000D fp64 after one eaSimple generation each (clones of the
+    tournament winners make equal genomes common), then migRing(k=15,
+    selBest) along the ring 0 -> 1 -> 0 (deap/tools/migration.py:4-51).  The
+    reference loop is replayed on the host over the full demes: for every
+    immigrant, ``list.index`` = the FIRST row whose genome equals it in the
+    deme as the earlier placements left it (candidate rows found through a
+    hash of every row, each confirmed by an exact genome compare), then the
+    emigrant replaces it.  The device result must equal that replay on every
+    row (hashes of all 2^20 rows of both demes; placed rows' genomes and
+    fitness bit for bit), and the emigrants must be a selBest of each deme."""
+    import ctypes
+    import torch
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim, k = N, 1000, 15
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.rastrigin)
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+    tb.register("select", tools.selTournament, tournsize=3)
+    demes = []
+    for d in range(2):
+        st = RandomStream(1234, island=d)
+        p = tools.initPopulation(n=n, dim=dim, low=-5.12, high=5.12, gtype="f64", weights=(-1.0,),
+                                 stream=st)
+        benchmarks.rastrigin(p)
+        off = p.like(n, capacity=n)
+        nev = torch.zeros(1, dtype=torch.int64, device=p.device)
+        algorithms.GenerationStep(p, tb, 0.5, 0.2).step(p, off, st, ctypes.c_void_p(nev.data_ptr()))
+        p.swap_storage(off)
+        del off
+        demes.append(p)
+    torch.cuda.synchronize()
+    em = [tools.selBest(p, k).cpu().numpy().astype(np.int64) for p in demes]
+    wv0 = [p.wvalues[:n, 0].cpu().numpy().copy() for p in demes]
+    for d in range(2):  # selBest: the k largest weighted fitnesses (1e-12 tolerance)
+        assert _rel_close(np.sort(wv0[d][em[d]])[::-1], np.sort(wv0[d])[::-1][:k], 1e-12)
+    h0 = [_row_hashes(p) for p in demes]
+    # host copies of every row a placement can touch: the emigrants and every
+    # row sharing a hash with an immigrant
+    need = [set(em[d].tolist()) | set(np.nonzero(np.isin(h0[d], h0[d][em[d]]))[0].tolist())
+            for d in range(2)]
+    rows = []
+    for d in range(2):
+        idx = sorted(need[d])
+        g, w, _ = demes[d].rows_numpy(idx)
+        rows.append({r: (g[i], w[i, 0]) for i, r in enumerate(idx)})
+    # the reference loop (migarray [1, 0], immigrants = emigrants)
+    cur_h = [h.copy() for h in h0]
+    cur = [dict(r) for r in rows]  # row -> (genome, wvalue) as placements leave it
+    placed = [[], []]
+    for frm, to in enumerate([1, 0]):
+        for j in range(k):
+            target = rows[to][int(em[to][j])][0]
+            slot = None
+            for c in np.nonzero(cur_h[to] == h0[to][em[to][j]])[0]:
+                if np.array_equal(cur[to][int(c)][0], target):
+                    slot = int(c)
+                    break
+            assert slot is not None, "immigrant %d of deme %d not found" % (j, to)
+            src = rows[frm][int(em[frm][j])]
+            cur[to][slot] = src
+            cur_h[to][slot] = h0[frm][em[frm][j]]
+            placed[to].append((slot, src))
+    rec = []
+    tools.migRing(demes, k, tools.selBest, record=rec)
+    assert all(np.array_equal(rec[0]["emigrants"][d], em[d]) for d in range(2))
+    for d in range(2):
+        assert np.array_equal(_row_hashes(demes[d]), cur_h[d]), "deme %d differs from the replay" % d
+        slots = [s for s, _ in placed[d]]
+        g, w, ok = demes[d].rows_numpy(slots)
+        final = {}
+        for s_, src in placed[d]:
+            final[s_] = src  # a slot placed twice keeps the later emigrant
+        for i, s_ in enumerate(slots):
+            assert np.array_equal(g[i], final[s_][0]) and w[i, 0] == final[s_][1] and ok[i]

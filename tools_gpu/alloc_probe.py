@@ -7,6 +7,8 @@ MODE: torch   — PyTorch caching allocator (what DevicePopulation does)
       raw     — one hipMalloc per genome buffer
       contig  — hipExtMallocWithFlags(hipDeviceMallocContiguous) per buffer
       arena   — ONE hipMalloc holding every genome buffer, 2 MiB aligned
+      pair    — per deme ONE hipMalloc for both genome buffers, the child
+                buffer argv[4] bytes past the parent buffer's 2 MiB-rounded end
 Prints each deme's mean kernel time (library HIP events) and the addresses."""
 import ctypes
 import sys
@@ -61,6 +63,18 @@ for i in range(ndemes):
                 ptr = hip_alloc(nb)
             elif mode == "contig":
                 ptr = hip_alloc(nb, 0x4)
+            elif mode == "pair":
+                # both genome buffers of the deme in ONE allocation, the child
+                # buffer DELTA bytes past the 2 MiB-rounded end of the parent
+                # buffer (argv[4], default 0)
+                if q is p:
+                    delta = int(float(sys.argv[4])) if len(sys.argv) > 4 else 0
+                    per = (nb + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+                    b0 = hip_alloc(2 * per + delta + (2 << 20))
+                    b0 = (b0 + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+                    ptr = b0
+                else:
+                    ptr = b0 + per + delta
             elif mode == "arena":
                 if arena is None:
                     per = (nb + (2 << 20) - 1) // (2 << 20) * (2 << 20)

@@ -42,6 +42,20 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
       step alloc_torch4 300 python tools_gpu/alloc_probe.py torch 4
       step alloc_arena4 300 python tools_gpu/alloc_probe.py arena 4 ;;
     counters) step counters 120 rocprofv3 -L ;;
+    c5ab2)
+      step c5_persist 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_multi 300 env DM_PEEL_MULTI=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_multi_fp 300 env DM_PEEL_MULTI=1 DM_CROWD_FP=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    c5ab)
+      step c5_t1 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_t0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_t0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_multi 300 env DM_PEEL_MULTI=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    alloc_pair)
+      for d in 0 4096 65536 262144 1048576 3145728 16777216 1073741824; do
+        step alloc_pair_$d 200 python tools_gpu/alloc_probe.py pair 1 12 $d
+      done
+      step alloc_torch1b 200 python tools_gpu/alloc_probe.py torch 1 12
+      step alloc_pair4 300 python tools_gpu/alloc_probe.py pair 4 12 0 ;;
     pmc_alloc)
       i=0
       for pmc in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_TCC_READ_REQ_LATENCY_sum" \
