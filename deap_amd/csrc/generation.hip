@@ -147,6 +147,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.sigma = a.sigma;
         q.w0 = a.w0;
         q.ev = a.ev;
+        q.ntload = std::getenv("DM_PIPE_NTLOAD") ? atoi(std::getenv("DM_PIPE_NTLOAD")) : 0;
         timing_begin(ctx);
         if (parents->gtype == DM_F64)
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);

@@ -129,16 +129,19 @@ struct ChunkLayout<double> {
     __device__ __forceinline__ static int gene(int c, int lane, int k) {
         return (c << 8) + ((k >> 1) << 7) + 2 * lane + (k & 1);
     }
+    // nt: non-temporal loads (the parent rows are read once per launch)
     __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
-                                                double (&x)[4]) {
+                                                double (&x)[4], bool nt = false) {
         const int g0 = gene(c, lane, 0), g2 = gene(c, lane, 2);
         if (g0 < dim) {
-            const double2 v = *reinterpret_cast<const double2*>(row + (size_t)g0 * 8);
+            const dm_d2* p = reinterpret_cast<const dm_d2*>(row + (size_t)g0 * 8);
+            const dm_d2 v = nt ? __builtin_nontemporal_load(p) : *p;
             x[0] = v.x;
             x[1] = v.y;
         }
         if (g2 < dim) {
-            const double2 v = *reinterpret_cast<const double2*>(row + (size_t)g2 * 8);
+            const dm_d2* p = reinterpret_cast<const dm_d2*>(row + (size_t)g2 * 8);
+            const dm_d2 v = nt ? __builtin_nontemporal_load(p) : *p;
             x[2] = v.x;
             x[3] = v.y;
         }
@@ -159,7 +162,7 @@ struct ChunkLayout<float> {
         return (c << 8) + 4 * lane + k;
     }
     __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
-                                                double (&x)[4]) {
+                                                double (&x)[4], bool nt = false) {
         const int g = gene(c, lane, 0);
         if (g < dim) Vec4<float>::load(row, g, x);
     }
@@ -256,6 +259,7 @@ struct PipeArgs {
     int64_t* nevals;
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
+    int32_t ntload;  // non-temporal parent-row loads (DM_PIPE_NTLOAD, A/B)
     Rng rng;
     uint64_t thr_ind;
     double alpha, mu, sigma, w0;
@@ -307,8 +311,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     double y0[D][4], y1[D][4];
 #pragma unroll
     for (int ch = 0; ch < D; ++ch) {
-        L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch]);
-        L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch]);
+        L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch], a.ntload);
+        L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch], a.ntload);
     }
     for (; p < npairs; p += nw) {
         const bool more = p + nw < npairs;
@@ -339,11 +343,11 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
             {
                 const int ca = ch + D;
                 if (ca < NCH) {
-                    L::load(r0, ca, lane, dim, y0[ch % D]);
-                    L::load(r1, ca, lane, dim, y1[ch % D]);
+                    L::load(r0, ca, lane, dim, y0[ch % D], a.ntload);
+                    L::load(r1, ca, lane, dim, y1[ch % D], a.ntload);
                 } else if (more) {
-                    L::load(n0, ca - NCH, lane, dim, y0[ch % D]);
-                    L::load(n1, ca - NCH, lane, dim, y1[ch % D]);
+                    L::load(n0, ca - NCH, lane, dim, y0[ch % D], a.ntload);
+                    L::load(n1, ca - NCH, lane, dim, y1[ch % D], a.ntload);
                 }
             }
             const uint32_t slot = (uint32_t)((ch << 6) + lane);  // gene_slot of this lane's genes
