@@ -193,6 +193,11 @@ __device__ __forceinline__ int32_t writelane(int32_t old, int32_t val) {
 #ifndef DM_TD_TCOUNT
 #define DM_TD_TCOUNT 1
 #endif
+// DM_TD_SROWS = 1: the v block's ranks (wave-uniform) come by scalar loads
+// into SGPRs instead of an LDS broadcast into VGPRs.
+#ifndef DM_TD_SROWS
+#define DM_TD_SROWS 1
+#endif
 
 // one row b (ranks y) against the group's lanes: shift the dominance bits
 // into tw, return b's dominator count over the group (0 when counted by
@@ -287,10 +292,12 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
                                                       const int32_t* __restrict__ toff,
                                                       int32_t* counter, uint64_t* __restrict__ D,
                                                       int16_t* __restrict__ part) {
+#if !DM_TD_SROWS
     __shared__ int4 sbuf[4][64];  // per wave: the ranks of the current v block
+    int4* Lw = sbuf[threadIdx.x >> 6];
+#endif
     const int lane = threadIdx.x & 63;
     const TransposerX tr(lane);
-    int4* L = sbuf[threadIdx.x >> 6];
     const int64_t Upad = NB * 64;
     const int32_t total = toff[ngroups];
     for (;;) {
@@ -319,7 +326,9 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
         const int32_t rmin = __builtin_amdgcn_readfirstlane(icomp(S[A0 * 64], M - 1));
         const int64_t B0 = c * TD_SEGS * 8;
         const int64_t B1 = std::min<int64_t>(std::min<int64_t>((int64_t)nseg[g], (c + 1) * TD_SEGS) * 8, NB);
+#if !DM_TD_SROWS
         int4 nxt = B0 < B1 ? S[B0 * 64 + lane] : make_int4(0, 0, 0, 0);
+#endif
         // words of 4 consecutive v blocks, stored together (whole 2 KB tiles)
         uint64_t wq[TD_WPW][4];
 #pragma unroll
@@ -328,9 +337,17 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
             for (int i = 0; i < 4; ++i) wq[k][i] = 0;
         for (int64_t B = B0; B < B1; ++B) {
             const int nb = (int)std::min<int64_t>(64, U - B * 64);
+#if DM_TD_SROWS
+            // the block's ranks are wave-uniform: scalar loads into SGPRs (no
+            // LDS staging, no VGPRs for the rows in flight)
+            const int4* L = S + B * 64;
+            const bool strict = icomp(L[nb - 1], M - 1) < rmin;
+#else
+            int4* L = Lw;
             L[lane] = nxt;  // the previous block's reads were issued before (in-order LDS)
             if (B + 1 < B1) nxt = S[(B + 1) * 64 + lane];
             const bool strict = __builtin_amdgcn_readfirstlane(icomp(L[nb - 1], M - 1)) < rmin;
+#endif
             uint32_t th[TD_WPW], tl[TD_WPW];
 #pragma unroll
             for (int k = 0; k < TD_WPW; ++k) th[k] = tl[k] = 0;

@@ -359,7 +359,13 @@ int dm_comm_destroy(dm_comm* comm);
  * rank hops are grouped ncclSend / ncclRecv of the packed emigrant blocks
  * (ncclGroupStart/End, RCCL point-to-point over xGMI) on the ctx stream;
  * placement is local to the receiver.  Must be called by every rank with the
- * same n_demes / migarray / owner / k.  flags: DM_MIG_FORCE_P2P. */
+ * same n_demes / migarray / owner / k — a rank holding no deme included
+ * (n_local = 0, demes / deme_ids / emig_idx may be NULL).  With more than one
+ * rank, every per-rank check (ids, owners, k against deme sizes, layouts,
+ * scratch) runs first and the ranks agree on the outcome (one ncclAllReduce
+ * of an ok flag) before any send or receive is posted: a rank whose check
+ * failed returns its own error, the others DM_ERR_INVALID, none hangs.
+ * flags: DM_MIG_FORCE_P2P. */
 int dm_mig_ring_rccl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
                      const int32_t* deme_ids, int32_t n_demes, const int32_t* migarray,
                      const int32_t* owner, int64_t k, int32_t* const* emig_idx,

@@ -43,6 +43,10 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
       step alloc_arena4 300 python tools_gpu/alloc_probe.py arena 4 ;;
     counters) step counters 120 rocprofv3 -L ;;
     abnt) step ab_nt 300 python tools_gpu/ab_inproc.py c3 DM_PIPE_NTLOAD 0 1 ;;
+    c5srows)
+      step c5_s1 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_s0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_s0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_s1b 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c5ab2)
       step c5_persist 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_multi 300 env DM_PEEL_MULTI=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
