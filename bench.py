@@ -330,6 +330,11 @@ def main(argv=None):
 
     for g in range(args.warmup):
         one_gen(g, False)
+    if n_demes > 1:
+        # one untimed migration: the RCCL communicator (ncclCommInitRank), the
+        # peers' point-to-point connections and the migration scratch are set
+        # up here, not inside the timed steps
+        migrate(False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

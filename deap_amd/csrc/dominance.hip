@@ -193,6 +193,11 @@ __device__ __forceinline__ int32_t writelane(int32_t old, int32_t val) {
 #ifndef DM_TD_TCOUNT
 #define DM_TD_TCOUNT 1
 #endif
+// DM_TD_WQ = 1: the D words of 4 consecutive v blocks are kept and stored
+// as two 16-B pieces per row; 0: one 8-B store per row and block.
+#ifndef DM_TD_WQ
+#define DM_TD_WQ 1
+#endif
 // DM_TD_SROWS = 1: the v block's ranks (wave-uniform) come by scalar loads
 // into SGPRs instead of an LDS broadcast into VGPRs.
 #ifndef DM_TD_SROWS
@@ -380,6 +385,15 @@ __global__ __launch_bounds__(256) void tri_dom_kernel(const int4* __restrict__ S
                 for (int k = 0; k < TD_WPW; ++k) cpark += __popc(lo[k]) + __popc(hi[k]);
             }
             part[g * Upad + B * 64 + lane] = (int16_t)cpark;
+#if !DM_TD_WQ
+            // one 8-B word per row and block, stored at once (no VGPRs for the
+            // 4-block line pieces; L2 merges the pieces of a line)
+#pragma unroll
+            for (int k = 0; k < TD_WPW; ++k)
+                if (A0 + k < NB)
+                    D[tword((A0 + k) * 64 + lane, B, NQ)] = ((uint64_t)th[k] << 32) | tl[k];
+            continue;
+#endif
             const int bq = (int)(B & 3);
 #pragma unroll
             for (int k = 0; k < TD_WPW; ++k) {

@@ -80,6 +80,26 @@ __global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, in
         if (start) isrep[perm[j]] = 1;
     }
 }
+// After a sort by objective 0 only: flag when two neighbours with equal
+// objective-0 keys are out of lexicographic order in the other objectives
+// (then the full lexicographic sort is needed; ties keep index order).
+__global__ void lex_tie_kernel(const double* wv, int m, const int32_t* perm, int64_t n,
+                               int32_t* flag) {
+    GRID_LOOP(j, n) {
+        if (j == 0) continue;
+        const double* a = wv + (int64_t)perm[j] * m;
+        const double* b = wv + (int64_t)perm[j - 1] * m;
+        if (ordered_key(a[0]) != ordered_key(b[0])) continue;
+        for (int o = 1; o < m; ++o) {
+            const uint64_t ka = ordered_key(a[o]), kb = ordered_key(b[o]);
+            if (ka > kb) break;
+            if (ka < kb) {
+                *flag = 1;
+                break;
+            }
+        }
+    }
+}
 __global__ void nan_any_kernel(const double* wv, int64_t cnt, int32_t* flag) {
     GRID_LOOP(i, cnt) if (wv[i] != wv[i]) *flag = 1;
 }
@@ -472,17 +492,35 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     int32_t* nanflag = small + 2;
     int32_t* ftotal = small + 4;
     int64_t* dtotal = (int64_t*)(small + 8);
-    // lexicographic ascending sort of wvalues (ties by index: stable)
-    int rc = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp);
-    if (rc) return rc;
-    zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
-    seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
-    if ((rc = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return rc;
-    if ((rc = exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp))) return rc;
+    // lexicographic ascending sort of wvalues (ties by index: stable).  First
+    // by objective 0 alone (8 radix passes instead of 8m): when no two rows
+    // with equal objective 0 are out of order in the others (lex_tie_kernel,
+    // read with U below), that IS the lexicographic order; otherwise the
+    // full sort and the grouping are redone.
+    int32_t* tieflag = small + 6;
+    static const bool full_lex = std::getenv("DM_LEX_FULL") != nullptr;
+    const bool quick = m > 1 && !full_lex;
+    int rc;
+    auto group = [&](int nlex) -> int {
+        int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex);
+        if (r) return r;
+        zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
+        seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
+        if ((r = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return r;
+        return exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp);
+    };
+    if ((rc = group(quick ? 1 : m))) return rc;
     DM_HIP(hipMemsetAsync(nanflag, 0, 4, s));
+    DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
     nan_any_kernel<<<g1(n * m), 256, 0, s>>>(wv, n * m, nanflag);
-    DM_HIP(hipMemcpyAsync(hostv, utotal, 12, hipMemcpyDeviceToHost, s));
+    if (quick) lex_tie_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, tieflag);
+    DM_HIP(hipMemcpyAsync(hostv, utotal, 28, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
+    if (quick && hostv[6]) {
+        if ((rc = group(m))) return rc;
+        DM_HIP(hipMemcpyAsync(hostv, utotal, 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+    }
     const int64_t U = hostv[0];
     const bool has_nan = hostv[2] != 0;
     // integer ranks + symmetric tiles + device-driven peel (dominance.hip);

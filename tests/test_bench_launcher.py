@@ -101,3 +101,26 @@ def test_failing_rank_fails_the_launch():
     p = _run(["--gpus", "2", "--backend", "gloo", "--dry-run", "--islands", "3"])
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_driver_torchrun_form():
+    """The driver's own form: ``torch.distributed.run --nproc-per-node N
+    bench.py --gpus N`` (WORLD_SIZE set by torchrun, equal to --gpus)."""
+    if not _lib_built():
+        pytest.skip("libdeapmi.so not built")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend",
+                        "gloo", "--dry-run"], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["owner"] == [0, 1]

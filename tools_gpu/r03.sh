@@ -46,7 +46,8 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
     c5srows)
       step c5_s1 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_s0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_s0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
-      step c5_s1b 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+      step c5_s1b 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_lexfull 300 env DM_LEX_FULL=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c5ab2)
       step c5_persist 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_multi 300 env DM_PEEL_MULTI=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
