@@ -167,12 +167,24 @@ __global__ __launch_bounds__(1024) void tri_plan_kernel(const int4* S, int m, in
 
 // t + t + (bit `lane` of mask): one v_addc_co_u32 with the wave mask as the
 // carry-in (lane-local "shift in the bit of this lane").
+#ifndef DM_TD_ILP
+#define DM_TD_ILP 1  // 0: the round-2 per-A-block order (A/B)
+#endif
+// Not volatile: a pure function of its operands, so the scheduler may
+// interleave the independent shift-ins of the 4 A-blocks (a volatile asm kept
+// them in program order, each waiting on its own compare -> s_and chain).
 __device__ __forceinline__ uint32_t add2_carry(uint32_t t, uint32_t a, uint64_t mask) {
     uint32_t out;
     uint64_t cout;
+#if DM_TD_ILP
+    asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4"
+        : "=v"(out), "=s"(cout)
+        : "v"(t), "v"(a), "s"(mask));
+#else
     asm volatile("v_addc_co_u32_e64 %0, %1, %2, %3, %4"
                  : "=v"(out), "=s"(cout)
                  : "v"(t), "v"(a), "s"(mask));
+#endif
     return out;
 }
 
@@ -216,13 +228,14 @@ __device__ __forceinline__ int32_t td_row(const int4 y4, const int32_t (&x)[TD_W
     if constexpr (M > 2) y[2] = y4.z;
     if constexpr (M > 3) y[3] = y4.w;
     int32_t cnt = 0;
+    // all compares of the row first (independent wave masks), then the ANDs,
+    // then the shift-ins: the VALU -> SALU -> VALU chains of the 4 A-blocks
+    // overlap instead of running one after the other
+    uint64_t msk[TD_WPW];
 #pragma unroll
     for (int k = 0; k < TD_WPW; ++k) {
-        uint64_t msk;
         if constexpr (STRICT) {
-            msk = __ballot(x[k][0] >= y[0]);
-#pragma unroll
-            for (int o = 1; o < M - 1; ++o) msk &= __ballot(x[k][o] >= y[o]);
+            msk[k] = __ballot(x[k][0] >= y[0]);
         } else {
             int32_t mn = x[k][0] - y[0], mx = mn;
 #pragma unroll
@@ -231,11 +244,20 @@ __device__ __forceinline__ int32_t td_row(const int4 y4, const int32_t (&x)[TD_W
                 mn = min(mn, d);
                 mx = max(mx, d);
             }
-            msk = __ballot(mn >= 0) & __ballot(mx > 0);
+            msk[k] = __ballot(mn >= 0) & __ballot(mx > 0);
         }
-        tw[k] = add2_carry(tw[k], tw[k], msk);
+    }
+    if constexpr (STRICT) {
+#pragma unroll
+        for (int o = 1; o < M - 1; ++o)
+#pragma unroll
+            for (int k = 0; k < TD_WPW; ++k) msk[k] &= __ballot(x[k][o] >= y[o]);
+    }
+#pragma unroll
+    for (int k = 0; k < TD_WPW; ++k) {
+        tw[k] = add2_carry(tw[k], tw[k], msk[k]);
 #if !defined(DM_TD_NOCOUNT) && !DM_TD_TCOUNT
-        cnt += __popcll(msk);
+        cnt += __popcll(msk[k]);
 #endif
     }
     return cnt;
@@ -750,7 +772,10 @@ __device__ void peel_segment(const uint64_t* __restrict__ D, int64_t NQ, const i
     __syncthreads();  // the LDS is reused by the caller's next task
 }
 
-__global__ __launch_bounds__(PEEL_WAVES * 64) void peel_owned_kernel(const uint64_t* __restrict__ D,
+#ifndef DM_PEEL_MINW
+#define DM_PEEL_MINW 1  // min waves per SIMD (4: two 512-thread workgroups per CU)
+#endif
+__global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kernel(const uint64_t* __restrict__ D,
                                                          int64_t NQ,
                                                          const int2* __restrict__ mrow,
                                                          const int32_t* __restrict__ gsize,

@@ -281,10 +281,10 @@ struct PipeArgs {
 #define DM_PIPE_DEPTH 2
 #endif
 
-template <typename T, int NCH, int CX, int MUT, int EC>
+template <typename T, int NCH, int CX, int MUT, int EC, int DEPTH = DM_PIPE_DEPTH>
 __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArgs a) {
     typedef ChunkLayout<T> L;
-    constexpr int D = NCH < DM_PIPE_DEPTH ? NCH : DM_PIPE_DEPTH;
+    constexpr int D = NCH < DEPTH ? NCH : DEPTH;
     static_assert(NCH % D == 0, "ring depth must divide the chunk count");
     __shared__ double szig[ZIG_N + 1];
     __shared__ double2 cstab[64];
@@ -496,6 +496,13 @@ dim3 pipe_grid(K kern, int num_cus, int64_t npairs) {
 }
 template <typename T, int NCH, int CX, int MUT, int EC>
 void launch_pipe_k(const PipeArgs& a, int num_cus, hipStream_t s) {
+    // DM_PIPE_DEPTH=4 (runtime, A/B): whole 1000-gene rows in flight
+    const char* dep = std::getenv("DM_PIPE_DEPTH");
+    if (NCH == 4 && dep && atoi(dep) == 4) {
+        auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC, 4>;
+        kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a);
+        return;
+    }
     auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC>;
     kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a);
 }

@@ -43,11 +43,20 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
       step alloc_arena4 300 python tools_gpu/alloc_probe.py arena 4 ;;
     counters) step counters 120 rocprofv3 -L ;;
     abnt) step ab_nt 300 python tools_gpu/ab_inproc.py c3 DM_PIPE_NTLOAD 0 1 ;;
+    abdepth) step ab_depth 300 python tools_gpu/ab_inproc.py c3 DM_PIPE_DEPTH 2 4 ;;
+    c5ilp)
+      step c5_ilp1 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_ilp0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_ilp0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    c5pb)
+      step c5_pb_base 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_pb1 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_pb1.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_pb_base2 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c5srows)
       step c5_s1 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_s0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_s0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_s1b 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
-      step c5_lexfull 300 env DM_LEX_FULL=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+      step c5_lexfull 300 env DM_LEX_FULL=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
+      step c5_wq0 300 env DEAPMI_LIB=$PWD/deap_amd/libdeapmi_wq0.so python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c5ab2)
       step c5_persist 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
       step c5_multi 300 env DM_PEEL_MULTI=1 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline
