@@ -1,0 +1,343 @@
+// bitdom.hip — the dominance words D and dominator counts of the fast
+// sortNondominated path (deap/tools/emo.py:53-117) from bitset tables.
+//
+// Over integer ranks (dominance.hip §1) Fitness.dominates (base.py:209-224)
+// factorises per objective:  u dominates v  <=>  r_i(u) >= r_i(v) for every
+// objective i and u != v (distinct unique fitnesses have distinct rank
+// vectors, so "not all equal" is u != v).  Over a chunk C of 512 consecutive
+// v of the q order, the set {v in C : r_i(v) <= t} is, for any threshold t,
+// a prefix of C sorted by r_i: one of only 513 sets.  bd_table_kernel stores
+// them all per chunk and objective i >= 1 (P_i[C][k], k = 0..512, 64 bytes
+// each, built by wave ballots), beside C's sorted ranks R_i[C].  Row u of D
+// over C is then
+//     prefix0(u) & P_1[C][k_1] & .. & P_{m-1}[C][k_{m-1}]  without bit u,
+//     k_i = #{v in C : r_i(v) <= r_i(u)}  (a binary search of R_i[C] in LDS),
+// and prefix0(u) = every v up to the last q of u's objective-0 tie group (q
+// order ascends in r_0).  16 dword ANDs per objective decide 512 pairs, where
+// the compare kernel (dominance.hip tri_dom_kernel) spends a VALU compare per
+// objective and 64 pairs; what is left is storing D (one 64-byte half line
+// per row and chunk).  The dominator counts use the same tables transposed:
+//     #{u in C : u dominates v} = popcount(suffix0(v) & ~(P_1[lb_1] | ..)) - [v in C],
+//     lb_i = #{u in C : r_i(u) < r_i(v)},
+// int16 partials per (chunk, v), summed per v over the chunks that reach it.
+//
+// Output = tri_dom_kernel's + tri_count's: the same D words for every row and
+// every 512-v half its A-group reaches (nseg), the same count / countq, so the
+// peel is unchanged.  DM_DOM_TRI=1 selects the compare kernel (A/B, tests).
+#include "bitdom.hpp"
+
+namespace dm {
+
+size_t bitdom_bytes(int64_t U, int m) { return bitdom_layout(U, m).total; }
+
+// first[r] / last[r]: the first / last q whose objective-0 rank is r (r_0 is
+// a dense rank and ascends with q).
+__global__ void bd_ties_kernel(const int4* __restrict__ S, int m, int64_t U, int32_t* first,
+                               int32_t* last) {
+    DGRID_LOOP(q, U) {
+        const int32_t r = icomp(S[q], m - 1);
+        if (!BD_OK(r, U, "ties r")) continue;
+        if (q == 0 || icomp(S[q - 1], m - 1) != r) first[r] = (int32_t)q;
+        if (q == U - 1 || icomp(S[q + 1], m - 1) != r) last[r] = (int32_t)q;
+    }
+}
+
+// span[q] = (first, last) q of q's objective-0 tie group: prefix0(u) is every
+// v <= span[u].y, suffix0(v) every u >= span[v].x.
+__global__ void bd_span_kernel(const int4* __restrict__ S, int m, int64_t U,
+                               const int32_t* __restrict__ first, const int32_t* __restrict__ last,
+                               int2* __restrict__ span) {
+    DGRID_LOOP(q, U) {
+        const int32_t r = icomp(S[q], m - 1);
+        if (!BD_OK(r, U, "span r")) continue;
+        span[q] = make_int2(first[r], last[r]);
+    }
+}
+
+// Tables of chunk c (blockIdx.x) for objective f + 1 (blockIdx.y; S component
+// f):  R[(cF + f) 512 + j] = the j-th smallest rank of C (positions past U:
+// INT32_MAX, last);  P[((cF + f) 513 + k) 16 + d] = dword d of the set of
+// positions whose local rank (rank, position) is below k — for k = 0..512 by
+// one ballot per 64 positions and k.
+__global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __restrict__ S,
+                                                              int64_t U, int F,
+                                                              uint32_t* __restrict__ P,
+                                                              int32_t* __restrict__ R) {
+    __shared__ int32_t r[BD_CW];
+    const int64_t c = blockIdx.x;
+    const int f = blockIdx.y;
+    const int t = threadIdx.x;
+    const int64_t v = c * BD_CW + t;
+    const int32_t rv = v < U ? icomp(S[v], f) : INT32_MAX;
+    r[t] = rv;
+    __syncthreads();
+    int32_t lr = 0;
+#pragma unroll 16
+    for (int i = 0; i < BD_CW; ++i) {
+        const int32_t ri = r[i];
+        lr += (ri < rv || (ri == rv && i < t)) ? 1 : 0;
+    }
+    const int64_t cf = c * F + f;
+    if (BD_OK(lr, BD_CW, "table lr")) R[cf * BD_CW + lr] = rv;
+    uint32_t* Pc = P + cf * BD_K * 16;
+    const int wave = t >> 6, lane = t & 63;
+    for (int k0 = 0; k0 < BD_K; k0 += 64) {
+        uint64_t mine = 0;
+#pragma unroll 16
+        for (int i = 0; i < 64; ++i) {
+            const uint64_t b = __ballot(lr < k0 + i);
+            mine = lane == i ? b : mine;
+        }
+        const int k = k0 + lane;
+        if (k < BD_K) *reinterpret_cast<uint64_t*>(Pc + (int64_t)k * 16 + 2 * wave) = mine;
+    }
+}
+
+// Per chunk c: rowfirst[c] = first row of the A-groups whose reach includes c
+// (nseg[g] > c; nseg is nondecreasing), reach[c] = 1 + the last q whose r_0
+// is at most chunk c's largest (the v a row of c can dominate); toffD /
+// toffC: first task of c in the row / count pass (BD_RT rows or v per task).
+__global__ __launch_bounds__(1024) void bd_plan_kernel(const int4* __restrict__ S, int m,
+                                                       const int32_t* __restrict__ last,
+                                                       const int32_t* __restrict__ nseg, int64_t U,
+                                                       int64_t NG, int64_t ngroups,
+                                                       int32_t* rowfirst, int32_t* reach,
+                                                       int32_t* toffD, int32_t* toffC) {
+    __shared__ int32_t shD[1024], shC[1024];
+    __shared__ int32_t carryD, carryC;
+    const int tid = threadIdx.x;
+    if (tid == 0) carryD = carryC = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < NG; base += 1024) {
+        const int64_t c = base + tid;
+        int32_t nD = 0, nC = 0;
+        if (c < NG) {
+            int64_t lo = 0, hi = ngroups;  // first g with nseg[g] > c
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (nseg[mid] > c) hi = mid;
+                else lo = mid + 1;
+            }
+            const int64_t r0 = lo * TD_WPW * 64;
+            rowfirst[c] = (int32_t)r0;
+            nD = r0 < U ? (int32_t)((U - r0 + BD_RT - 1) / BD_RT) : 0;
+            const int64_t qe = std::min<int64_t>(c * BD_CW + BD_CW - 1, U - 1);
+            const int32_t rq = icomp(S[qe], m - 1);
+            const int32_t re = BD_OK(rq, U, "plan last") ? last[rq] + 1 : 0;
+            reach[c] = re;
+            nC = (re + BD_RT - 1) / BD_RT;
+        }
+        shD[tid] = nD;
+        shC[tid] = nC;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            const int32_t aD = tid >= off ? shD[tid - off] : 0;
+            const int32_t aC = tid >= off ? shC[tid - off] : 0;
+            __syncthreads();
+            shD[tid] += aD;
+            shC[tid] += aC;
+            __syncthreads();
+        }
+        const int32_t cD = carryD, cC = carryC;
+        if (c < NG) {
+            toffD[c] = cD + shD[tid] - nD;
+            toffC[c] = cC + shC[tid] - nC;
+        }
+        __syncthreads();
+        if (tid == 1023) {
+            carryD = cD + shD[1023];
+            carryC = cC + shC[1023];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        toffD[NG] = carryD;
+        toffC[NG] = carryC;
+    }
+}
+
+// Row pass: task = (chunk c, BD_RT rows from rowfirst[c]); lane = row u, a
+// wave takes 64 rows at a time.  The 64-byte row of a table set is read as
+// four 16-byte pieces in a lane-rotated order (piece (i + lane) & 3 at step
+// i): random sets start on only 4 of the 16 bank quads, the rotation spreads
+// a lane group's reads over all 16.  The next row's ranks and span are loaded
+// before this row's D stores are issued: loads and stores share the in-order
+// vmcnt counter, so a load issued after the stores would wait for them.
+template <int M>
+__global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
+    const int4* __restrict__ S, const int2* __restrict__ span, int64_t U, int64_t NQ, int64_t NG,
+    const int32_t* __restrict__ rowfirst, const int32_t* __restrict__ toffD,
+    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, uint64_t* __restrict__ D) {
+    constexpr int F = M - 1;
+    __shared__ uint4 sP[F][BD_K * 4];
+    __shared__ int32_t sR[F][BD_RP];
+    const int32_t t = blockIdx.x;
+    if (t >= toffD[NG]) return;
+    const int64_t c = bd_task_chunk<F>(toffD, NG, t);
+    const int64_t row0 = rowfirst[c] + (int64_t)(t - toffD[c]) * BD_RT;
+    const int64_t row1 = std::min<int64_t>(U, row0 + BD_RT);
+    int64_t u = row0 + threadIdx.x;
+    int4 su = u < row1 ? S[u] : make_int4(0, 0, 0, 0);
+    int2 sp = u < row1 ? span[u] : make_int2(0, 0);
+    bd_load_tables<F>(P, R, c, sP, sR);
+    const int rot = threadIdx.x & 3;
+    const int64_t v0 = c * BD_CW;
+    for (; u < row1; u += BD_THREADS) {
+        const int4 cu = su;
+        const int64_t lim = (int64_t)sp.y - v0;  // prefix0(u): positions <= lim
+        const int64_t un = u + BD_THREADS;
+        if (un < row1) {
+            su = S[un];
+            sp = span[un];
+        }
+        uint4 w[4];
+        bd_row_words<M>(cu, lim, u - v0, sP, sR, rot, w);
+        if (!BD_OK(tword(u, 8 * c, NQ) + 7, (U + 63) / 64 * 64 * NQ * TW, "rows D")) continue;
+        uint4* dst = reinterpret_cast<uint4*>(D + tword(u, 8 * c, NQ));
+#if DM_BD_ABLATE & 1  // profiling only: no D stores
+        if (w[0].x == 0x12345u && w[1].y == 0x777u) dst[0] = w[2];
+        continue;
+#elif DM_BD_ABLATE & 2  // profiling only (wrong D): whole 128-B lines, both halves
+        uint4* line = reinterpret_cast<uint4*>(D + tword(u, 16 * (c >> 1), NQ));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            line[(i + rot) & 3] = w[i];
+            line[4 + ((i + rot) & 3)] = w[i];
+        }
+        continue;
+#endif
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[(i + rot) & 3] = w[i];
+    }
+}
+
+// Count pass: task = (chunk c of dominators u, BD_RT v below reach[c]); lane
+// = v: the u of C that dominate v, as an int16 partial part[c][v].  The next
+// v's ranks and span are loaded ahead (as in the row pass).
+template <int M>
+__global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
+    const int4* __restrict__ S, const int2* __restrict__ span, int64_t U, int64_t Upad, int64_t NG,
+    const int32_t* __restrict__ reach, const int32_t* __restrict__ toffC,
+    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, int16_t* __restrict__ part) {
+    constexpr int F = M - 1;
+    __shared__ uint4 sP[F][BD_K * 4];
+    __shared__ int32_t sR[F][BD_RP];
+    const int32_t t = blockIdx.x;
+    if (t >= toffC[NG]) return;
+    const int64_t c = bd_task_chunk<F>(toffC, NG, t);
+    const int64_t vb = (int64_t)(t - toffC[c]) * BD_RT;
+    const int64_t ve = std::min<int64_t>(reach[c], vb + BD_RT);
+    int64_t v = vb + threadIdx.x;
+    int4 sv = v < ve ? S[v] : make_int4(0, 0, 0, 0);
+    int32_t sf = v < ve ? span[v].x : 0;
+    bd_load_tables<F>(P, R, c, sP, sR);
+    const int rot = threadIdx.x & 3;
+    const int64_t v0 = c * BD_CW;
+    const int64_t nvalid = U - v0;  // positions < nvalid are real rows
+    for (; v < ve; v += BD_THREADS) {
+        const int4 cv = sv;
+        const int64_t lo = (int64_t)sf - v0;  // suffix0(v): positions >= lo
+        const int64_t vn = v + BD_THREADS;
+        if (vn < ve) {
+            sv = S[vn];
+            sf = span[vn].x;
+        }
+        int k[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) k[f] = bd_count_below<false>(sR[f], icomp(cv, f));
+        uint32_t cnt = 0;
+        const bool edge = lo > 0 || nvalid < BD_CW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = (i + rot) & 3;
+            uint4 o = sP[0][k[0] * 4 + j];
+#pragma unroll
+            for (int f = 1; f < F; ++f) {
+                const uint4 y = sP[f][k[f] * 4 + j];
+                o.x |= y.x;
+                o.y |= y.y;
+                o.z |= y.z;
+                o.w |= y.w;
+            }
+            uint32_t x0 = ~o.x, x1 = ~o.y, x2 = ~o.z, x3 = ~o.w;
+            if (edge) {
+                const int d0 = 4 * j;
+                x0 &= from_mask(lo, d0) & upto_mask(nvalid - 1, d0);
+                x1 &= from_mask(lo, d0 + 1) & upto_mask(nvalid - 1, d0 + 1);
+                x2 &= from_mask(lo, d0 + 2) & upto_mask(nvalid - 1, d0 + 2);
+                x3 &= from_mask(lo, d0 + 3) & upto_mask(nvalid - 1, d0 + 3);
+            }
+            cnt += __popc(x0) + __popc(x1) + __popc(x2) + __popc(x3);
+        }
+        if (v >= v0 && v < v0 + BD_CW) cnt -= 1;  // v itself
+        if (BD_OK(c * Upad + v, NG * Upad, "count part")) part[c * Upad + v] = (int16_t)cnt;
+    }
+}
+
+// count[sigma[q]] = countq[q] = sum of part[c][q] over the chunks c that
+// reach q: every c from the chunk of q's objective-0 tie group start on.
+__global__ void bd_sum_kernel(const int16_t* __restrict__ part, const int2* __restrict__ span,
+                              int64_t U, int64_t Upad, int64_t NG,
+                              const int32_t* __restrict__ sigma, int32_t* __restrict__ count,
+                              int32_t* __restrict__ countq) {
+    DGRID_LOOP(q, U) {
+        if (!BD_OK(sigma[q], U, "sum sigma")) continue;
+        const int64_t c0 = span[q].x / BD_CW;
+        int32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        int64_t c = c0;
+        for (; c + 4 <= NG; c += 4) {
+            a0 += part[c * Upad + q];
+            a1 += part[(c + 1) * Upad + q];
+            a2 += part[(c + 2) * Upad + q];
+            a3 += part[(c + 3) * Upad + q];
+        }
+        for (; c < NG; ++c) a0 += part[c * Upad + q];
+        const int32_t cnt = (a0 + a1) + (a2 + a3);
+        count[sigma[q]] = cnt;
+        countq[q] = cnt;
+    }
+}
+
+template <int M>
+static void bitdom_launch(hipStream_t s, const int4* S, int64_t U, int64_t NQ, const BitdomLayout& L,
+                          char* ws, uint64_t* D) {
+    const int2* span = (const int2*)(ws + L.span);
+    const uint32_t* P = (const uint32_t*)(ws + L.P);
+    const int32_t* R = (const int32_t*)(ws + L.R);
+    const int64_t maxtasks = L.NG * ((U + BD_RT - 1) / BD_RT);
+    if (D)  // D words only for the D-reading peel (the table-fed peel needs none)
+        bd_rows_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
+        S, span, U, NQ, L.NG, (const int32_t*)(ws + L.rowfirst), (const int32_t*)(ws + L.toffD), P,
+        R, D);
+    bd_count_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
+        S, span, U, L.Upad, L.NG, (const int32_t*)(ws + L.reach), (const int32_t*)(ws + L.toffC), P,
+        R, (int16_t*)(ws + L.part));
+}
+
+int bitdom_build(hipStream_t s, const int4* S, int m, int64_t U, int64_t NQ, int64_t ngroups,
+                 const int32_t* nseg, const int32_t* sigma, uint64_t* D, int32_t* count,
+                 int32_t* countq, char* ws) {
+    DM_CHECK_ARG(m >= 2 && m <= 4, "bitdom: 2..4 objectives");
+    const BitdomLayout L = bitdom_layout(U, m);
+    int32_t* first = (int32_t*)(ws + L.first);
+    int32_t* last = (int32_t*)(ws + L.last);
+    int2* span = (int2*)(ws + L.span);
+    bd_ties_kernel<<<dg1(U), 256, 0, s>>>(S, m, U, first, last);
+    bd_span_kernel<<<dg1(U), 256, 0, s>>>(S, m, U, first, last, span);
+    bd_table_kernel<<<dim3((unsigned)L.NG, (unsigned)(m - 1)), BD_THREADS, 0, s>>>(
+        S, U, m - 1, (uint32_t*)(ws + L.P), (int32_t*)(ws + L.R));
+    bd_plan_kernel<<<1, 1024, 0, s>>>(S, m, last, nseg, U, L.NG, ngroups,
+                                      (int32_t*)(ws + L.rowfirst), (int32_t*)(ws + L.reach),
+                                      (int32_t*)(ws + L.toffD), (int32_t*)(ws + L.toffC));
+    switch (m) {
+        case 2: bitdom_launch<2>(s, S, U, NQ, L, ws, D); break;
+        case 3: bitdom_launch<3>(s, S, U, NQ, L, ws, D); break;
+        default: bitdom_launch<4>(s, S, U, NQ, L, ws, D); break;
+    }
+    bd_sum_kernel<<<dg1(U), 256, 0, s>>>((const int16_t*)(ws + L.part), span, U, L.Upad, L.NG,
+                                         sigma, count, countq);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+}  // namespace dm

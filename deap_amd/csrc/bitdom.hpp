@@ -1,0 +1,188 @@
+// bitdom.hpp — bitset-table dominance (bitdom.hip): constants, the tables'
+// layout and the device helpers shared by the table passes and the
+// table-fed front peel (dominance.hip peel_tab_kernel).
+#pragma once
+#include "dominance.hpp"
+
+namespace dm {
+
+constexpr int BD_CW = 512;        // v of a chunk
+constexpr int BD_K = BD_CW + 1;   // prefix sets per chunk and objective
+constexpr int BD_RT = 16384;      // rows (row pass) / v (count pass) per task
+constexpr int BD_THREADS = 512;
+
+#ifndef DM_BD_ABLATE
+#define DM_BD_ABLATE 0
+#endif
+
+// DM_BD_CHECK builds (diagnostics only): every global index is range-checked
+// and an out-of-range one is printed and skipped.
+#ifdef DM_BD_CHECK
+__device__ __forceinline__ bool bd_ok(int64_t i, int64_t n, const char* tag) {
+    if (i >= 0 && i < n) return true;
+    printf("bitdom OOB %s: %lld of %lld (block %d,%d thread %d)\n", tag, (long long)i,
+           (long long)n, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);
+    return false;
+}
+#define BD_OK(i, n, tag) bd_ok((int64_t)(i), (int64_t)(n), tag)
+#else
+#define BD_OK(i, n, tag) true
+#endif
+
+struct BitdomLayout {
+    int64_t NB, NG, Upad;
+    size_t part, P, R, first, last, span, rowfirst, reach, toffD, toffC, total;
+};
+static inline BitdomLayout bitdom_layout(int64_t U, int m) {
+    BitdomLayout L;
+    const int64_t F = m - 1;
+    L.NB = (U + 63) / 64;
+    L.NG = (L.NB + 7) / 8;
+    L.Upad = L.NB * 64;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(std::max<size_t>(bytes, 1), 256);
+        return o;
+    };
+    L.part = take((size_t)L.NG * L.Upad * 2);
+    L.P = take((size_t)L.NG * F * BD_K * 64);
+    L.R = take((size_t)L.NG * F * BD_CW * 4);
+    L.first = take((size_t)U * 4);
+    L.last = take((size_t)U * 4);
+    L.span = take((size_t)U * 8);
+    L.rowfirst = take((size_t)L.NG * 4);
+    L.reach = take((size_t)L.NG * 4);
+    L.toffD = take((size_t)(L.NG + 1) * 4);
+    L.toffC = take((size_t)(L.NG + 1) * 4);
+    L.total = off;
+    return L;
+}
+// #{j : sr[j] <= x} (LE) or #{j : sr[j] < x} over 512 ascending values held
+// in LDS with one pad word after every 32 (value j at j + j / 32): without
+// the pads every probe of a binary-search step h >= 16 lies in one bank (the
+// probes are lo + h - 1 with lo a multiple of 2h), a 16-way conflict by step 5.
+constexpr int BD_RP = BD_CW + BD_CW / 32;  // padded sorted-rank array
+__device__ __forceinline__ int bd_rpad(int j) { return j + (j >> 5); }
+template <bool LE>
+__device__ __forceinline__ int bd_count_below(const int32_t* sr, int32_t x) {
+    int lo = 0;
+#pragma unroll
+    for (int h = 256; h > 0; h >>= 1) {
+        const int32_t y = sr[bd_rpad(lo + h - 1)];
+        lo += (LE ? y <= x : y < x) ? h : 0;
+    }
+    const int32_t y = sr[bd_rpad(lo)];
+    return lo + ((LE ? y <= x : y < x) ? 1 : 0);
+}
+
+// dword d of a chunk holds positions 32d..32d+31
+__device__ __forceinline__ uint32_t upto_mask(int64_t lim, int d) {  // positions <= lim
+    const int64_t x = lim - 32 * d;
+    return x >= 31 ? ~0u : x < 0 ? 0u : (2u << x) - 1u;
+}
+__device__ __forceinline__ uint32_t from_mask(int64_t lo, int d) {  // positions >= lo
+    const int64_t x = lo - 32 * d;
+    return x <= 0 ? ~0u : x > 31 ? 0u : ~0u << x;
+}
+
+// The task's chunk (last c with toff[c] <= t) and the tables of that chunk
+// into LDS.
+template <int F>
+__device__ __forceinline__ int64_t bd_task_chunk(const int32_t* toff, int64_t NG, int32_t t) {
+    int64_t lo = 0, hi = NG - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (toff[mid] <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+template <int F>
+__device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t* R, int64_t c,
+                                               uint4 (&sP)[F][BD_K * 4], int32_t (&sR)[F][BD_RP]) {
+    // every global load of the thread first, then the LDS stores (a load ->
+    // wait -> store loop exposes the global latency once per piece)
+    constexpr int NP = F * BD_K * 4, NR = F * BD_CW / 4;
+    constexpr int LP = (NP + BD_THREADS - 1) / BD_THREADS, LR = (NR + BD_THREADS - 1) / BD_THREADS;
+    const uint4* gP = reinterpret_cast<const uint4*>(P + c * F * BD_K * 16);
+    const int4* gR = reinterpret_cast<const int4*>(R + c * F * BD_CW);
+    uint4 tp[LP];
+    int4 tr[LR];
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+        const int i = threadIdx.x + j * BD_THREADS;
+        if (i < NP) tp[j] = gP[i];
+    }
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+        const int i = threadIdx.x + j * BD_THREADS;
+        if (i < NR) tr[j] = gR[i];
+    }
+    uint4* lP = &sP[0][0];
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+        const int i = threadIdx.x + j * BD_THREADS;
+        if (i < NP) lP[i] = tp[j];
+    }
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+        const int i = threadIdx.x + j * BD_THREADS;  // values 4i..4i+3 of the F arrays
+        if (i < NR) {
+            const int f = (4 * i) / BD_CW, e = (4 * i) % BD_CW;
+            int32_t* d = &sR[f][0];
+            d[bd_rpad(e)] = tr[j].x;
+            d[bd_rpad(e + 1)] = tr[j].y;
+            d[bd_rpad(e + 2)] = tr[j].z;
+            d[bd_rpad(e + 3)] = tr[j].w;
+        }
+    }
+    __syncthreads();
+}
+
+template <int M>
+__device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t ps,
+                                             const uint4 (&sP)[M - 1][BD_K * 4],
+                                             const int32_t (&sR)[M - 1][BD_RP], int rot,
+                                             uint4 (&w)[4]) {
+    constexpr int F = M - 1;
+    if (lim < 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = make_uint4(0, 0, 0, 0);
+        return;
+    }
+    int k[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], icomp(su, f));
+#ifdef DM_BD_CHECK
+    for (int f = 0; f < F; ++f)
+        if (!BD_OK(k[f], BD_K, "rows k")) k[f] = 0;
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = (i + rot) & 3;
+        w[i] = sP[0][k[0] * 4 + j];
+#pragma unroll
+        for (int f = 1; f < F; ++f) {
+            const uint4 y = sP[f][k[f] * 4 + j];
+            w[i].x &= y.x;
+            w[i].y &= y.y;
+            w[i].z &= y.z;
+            w[i].w &= y.w;
+        }
+    }
+    if (lim < BD_CW - 1 || (ps >= 0 && ps < BD_CW)) {  // prefix0 ends in C, or u is in C
+        const int ds = (ps >= 0 && ps < BD_CW) ? (int)(ps >> 5) : -1;
+        const uint32_t sb = ~(1u << (ps & 31));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d0 = 4 * ((i + rot) & 3);
+            w[i].x &= upto_mask(lim, d0) & (ds == d0 ? sb : ~0u);
+            w[i].y &= upto_mask(lim, d0 + 1) & (ds == d0 + 1 ? sb : ~0u);
+            w[i].z &= upto_mask(lim, d0 + 2) & (ds == d0 + 2 ? sb : ~0u);
+            w[i].w &= upto_mask(lim, d0 + 3) & (ds == d0 + 3 ? sb : ~0u);
+        }
+    }
+}
+
+}  // namespace dm

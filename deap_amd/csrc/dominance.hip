@@ -26,18 +26,10 @@
 //    §8a-a21) — writes the front, its ranks and its individual count, and
 //    decides termination on the device.  The host only checks a status word
 //    every few fronts.
-#include "sort.hpp"
+#include "bitdom.hpp"
 #include "transpose.hpp"
 
 namespace dm {
-
-#define DGRID_LOOP(i, n)                                                         \
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); \
-         i += (int64_t)gridDim.x * blockDim.x)
-
-static dim3 dg1(int64_t n) {
-    return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65535)));
-}
 
 // ---------------------------------------------------------------------------
 // 1. ranks in objective-0 order
@@ -98,24 +90,11 @@ __global__ void rank_scatter_kernel(const int32_t* vals, const int32_t* excl, co
 // (A-group, b).  Words above the reach of a group are never written (the
 // peel skips them), so the matrix costs about half the bytes and compares of
 // the symmetric pass and the strict inner step is m-1 compares + 1 add.
-#ifndef DM_TD_WPW
-#define DM_TD_WPW 4
-#endif
-constexpr int TD_WPW = DM_TD_WPW;  // 64-row blocks per A-group
 constexpr int TD_SEGS = 2;  // 8-block row segments (512 v) per task
 
-__host__ __device__ __forceinline__ int32_t icomp(const int4& r, int c) {
-    return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w;
-}
-
-// word w of row u in the tiled layout: tiles of 64 rows x TW = 16 words (one
-// 128-byte line per row, 8 KB), NQ = 16-word groups per row.  A wave's store
-// of 4 words of its 64 rows is 64 pieces of 32 bytes that fill the tile's
-// lines over four such stores; a peel read of a row segment is one whole line.
-constexpr int TW = 16;
-__host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t NQ) {
-    return ((((u >> 6) * NQ + w / TW) << 6) + (u & 63)) * TW + (w % TW);
-}
+// D layout: tword (dominance.hpp).  A wave's store of 4 words of its 64 rows
+// is 64 pieces of 32 bytes that fill the tile's lines over four such stores;
+// a peel read of a row segment is one whole line.
 
 // nseg[g]: 8-block segments of v the rows of A-group g reach (every v whose
 // rank_0 <= the group's largest); toff[g]: first task of g (TD_SEGS segments
@@ -604,15 +583,27 @@ __device__ __forceinline__ void cst2(int2* p, int2 v) {
 
 constexpr int PEEL_PV = PEEL_WORDS * 64;                 // v of a row segment
 constexpr int PEEL_IT = PEEL_PV / (PEEL_WAVES * 64);      // v per thread
-struct PeelLds {
-    int32_t sdec[PEEL_WAVES][PEEL_PV];
-    int32_t slast[PEEL_WAVES][PEEL_PV];
+template <int PV>
+struct PeelLdsT {
+    int32_t sdec[PEEL_WAVES][PV];
+    int32_t slast[PEEL_WAVES][PV];
 };
-struct PeelSmall {
-    int32_t wcnt[PEEL_IT][PEEL_WAVES];
-    int64_t wgs[PEEL_IT][PEEL_WAVES];
+template <int PV>
+struct PeelSmallT {
+    static constexpr int IT = PV / (PEEL_WAVES * 64);
+    int32_t wcnt[IT][PEEL_WAVES];
+    int64_t wgs[IT][PEEL_WAVES];
     int32_t sbase;
 };
+typedef PeelLdsT<PEEL_PV> PeelLds;
+typedef PeelSmallT<PEEL_PV> PeelSmall;
+
+template <bool COH, int PW>
+__device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW], int64_t vbase,
+                             const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
+                             FrontState* st, int32_t* countq, unsigned long long* lastq,
+                             uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S);
 
 // Slice y of the nsl slices of row segment s for the front of sF unique
 // fitnesses starting at sust in ulist / mrow (front number snf).
@@ -689,6 +680,22 @@ __device__ void peel_segment(const uint64_t* __restrict__ D, int64_t NQ, const i
             }
         }
     }
+    peel_release<COH, PW>(dec, last, s * PV, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
+                          snf, nsl, L, S);
+}
+
+// The workgroup's (dominators, last releasing position) per v of its segment
+// [vbase, vbase + 64 PW) (dec / last: word w of this thread = v 64 w + lane,
+// per wave) are reduced in LDS and applied to countq; a v whose count reaches
+// zero is released into the next front's candidates.
+template <bool COH, int PW>
+__device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW], int64_t vbase,
+                             const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
+                             FrontState* st, int32_t* countq, unsigned long long* lastq,
+                             uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S) {
+    constexpr int PEEL_IT = PeelSmallT<PW * 64>::IT;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int w = 0; w < PW; ++w) {
         L.sdec[wave][w * 64 + lane] = dec[w];
@@ -710,7 +717,7 @@ __device__ void peel_segment(const uint64_t* __restrict__ D, int64_t NQ, const i
             d += L.sdec[wv][t];
             l = max(l, L.slast[wv][t]);
         }
-        const int64_t v = s * PV + t;  // q order
+        const int64_t v = vbase + t;  // q order
         fresh[it] = false;
         if (v < U && d > 0) {
             if (nsl == 1) {
@@ -763,7 +770,7 @@ __device__ void peel_segment(const uint64_t* __restrict__ D, int64_t NQ, const i
 #pragma unroll
     for (int it = 0; it < PEEL_IT; ++it) {
         if (!fresh[it]) continue;
-        const int64_t v = s * PV + threadIdx.x + it * PEEL_WAVES * 64;
+        const int64_t v = vbase + threadIdx.x + it * PEEL_WAVES * 64;
         const int32_t slot = S.sbase + S.wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
         cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
         cst<COH>(cq + slot, (int32_t)v);
@@ -800,6 +807,96 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
     if ((int64_t)blockIdx.y >= nsl) return;
     peel_segment<false>(D, NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU, st->U, sF,
                         sust, snf, s, blockIdx.y, nsl, L, S);
+}
+
+// Table-fed peel (the default with the bitset pass, 2-3 objectives): one
+// workgroup per 512-v chunk c of the q order and member slice, as
+// peel_owned_kernel, but each member's row bits over c are computed from the
+// chunk's bitset tables held in LDS (bd_row_words: one binary search and one
+// 64-byte set read per objective) instead of read from a stored D, so the
+// dominance matrix is never written.  Member rows, their ranks and tie spans
+// are loaded two 64-member steps ahead (a row's ranks wait on its row index).
+template <int F>
+__global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
+    const int4* __restrict__ S, const int2* __restrict__ span, const uint32_t* __restrict__ P,
+    const int32_t* __restrict__ R, const int2* __restrict__ mrow, const int32_t* __restrict__ gsize,
+    const int32_t* __restrict__ sigma, FrontState* st, int32_t* countq, unsigned long long* lastq,
+    uint64_t* ckey, int32_t* cq, int32_t* rankU) {
+    static_assert(PEEL_WAVES * 64 == BD_THREADS, "the table loads stride by BD_THREADS");
+    constexpr int PW = BD_CW / 64;  // words of a chunk
+    __shared__ uint4 sP[F][BD_K * 4];
+    __shared__ int32_t sR[F][BD_RP];
+    __shared__ PeelLdsT<BD_CW> L;
+    __shared__ PeelSmallT<BD_CW> Sm;
+    __shared__ int32_t sF, sust, sstop, snf;
+    if (threadIdx.x == 0) {
+        sF = st->F;
+        sust = st->ustart;
+        snf = st->nfronts;
+        sstop = st->done | st->overflow;
+    }
+    __syncthreads();
+    if (sstop) return;
+    const int64_t c = blockIdx.x;
+    const int64_t nsl = peel_slices(sF, c, gridDim.x, gridDim.y);
+    if ((int64_t)blockIdx.y >= nsl) return;
+    const int64_t U = st->U;
+    const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
+    const int64_t j0s = blockIdx.y * slen;
+    const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
+    const int2* members = mrow + sust;  // (row in q order, 512-v halves it reaches)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int64_t STEP = PEEL_WAVES * 64;
+    auto mload = [&](int64_t j) { return j < Fm ? members[j] : make_int2(0, 0); };
+    int64_t j0 = j0s + (int64_t)wave * 64;
+    int2 mrA = mload(j0 + lane), mrB = mload(j0 + STEP + lane);
+    int4 suA = S[mrA.x];
+    int2 spA = span[mrA.x];
+    bd_load_tables<F>(P, R, c, sP, sR);
+    const TransposerX tr(lane);
+    int32_t dec[PW], last[PW];
+#pragma unroll
+    for (int w = 0; w < PW; ++w) {
+        dec[w] = 0;
+        last[w] = -1;
+    }
+    const int64_t v0 = c * BD_CW;
+    for (; j0 < Fm; j0 += STEP) {
+        const int2 mrC = mload(j0 + 2 * STEP + lane);
+        const int4 suB = S[mrB.x];
+        const int2 spB = span[mrB.x];
+        const bool has = j0 + lane < Fm && c < mrA.y;
+        if (__ballot(has) != 0) {
+            uint4 w[4];
+            if (has) {
+                bd_row_words<F + 1>(suA, (int64_t)spA.y - v0, (int64_t)mrA.x - v0, sP, sR, 0, w);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = make_uint4(0, 0, 0, 0);
+            }
+            uint32_t lo[8], hi[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                lo[2 * i] = w[i].x;
+                hi[2 * i] = w[i].y;
+                lo[2 * i + 1] = w[i].z;
+                hi[2 * i + 1] = w[i].w;
+            }
+            tr.run<8>(lo, hi);  // lane v: bit i <-> member j0+i dominates v
+#pragma unroll
+            for (int w2 = 0; w2 < 8; ++w2) {
+                dec[w2] += __popc(lo[w2]) + __popc(hi[w2]);
+                const int32_t top = hi[w2] ? 63 - __clz(hi[w2]) : (lo[w2] ? 31 - __clz(lo[w2]) : -1);
+                if (top >= 0) last[w2] = (int32_t)(j0 + top);
+            }
+        }
+        mrA = mrB;
+        suA = suB;
+        spA = spB;
+        mrB = mrC;
+    }
+    peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
+                            snf, nsl, L, Sm);
 }
 
 constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
@@ -1241,7 +1338,8 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
         off += align_up(std::max<size_t>(bytes, 1), 256);
         return o;
     };
-    L.part = take((size_t)L.ngroups * L.Upad * 2);
+    // the compare kernel's int16 partials, or the bitset pass's scratch
+    L.part = take(std::max((size_t)L.ngroups * L.Upad * 2, bitdom_bytes(U, 4)));
     L.S = take((size_t)L.Upad * 16);
     L.sigma = take((size_t)U * 4);
     L.pos = take((size_t)U * 4);
@@ -1259,6 +1357,22 @@ size_t fast_dom_bytes(int64_t n, int64_t U) { return fast_layout(n, U).total; }
 int64_t fast_dom_words(int64_t U) {
     const int64_t NB = (U + 63) / 64, NQ = (NB + TW - 1) / TW;
     return NB * 64 * NQ * TW;
+}
+
+// Bitset tables (bitdom.hip) are the default dominance pass for 2 and 3
+// objectives; four take the compare kernel: the m = 4 bitset kernels (three
+// 33-KB tables, 104,640 B of LDS per workgroup) faulted on the GPU in the
+// product build but not in a range-checked DM_BD_CHECK build, and a plain
+// 104,640-B LDS kernel runs clean on the same boxes (tools_gpu/lds_probe.hip) —
+// unresolved; DM_BD_MAXM=4 re-enables them for diagnosis.
+// With the bitset pass the peel reads the tables, not a D matrix
+// (peel_tab_kernel), unless DM_PEEL_D / DM_PEEL_PERSIST ask for the D peel.
+bool fast_bitset(int m) {
+    const char* bdmax = std::getenv("DM_BD_MAXM");
+    return m >= 2 && m <= (bdmax ? atoi(bdmax) : 3) && !std::getenv("DM_DOM_TRI");
+}
+bool fast_table_peel(int m) {
+    return fast_bitset(m) && !std::getenv("DM_PEEL_D") && !std::getenv("DM_PEEL_PERSIST");
 }
 
 // Ranks (objective 0 from the population's lexicographic order perm, whose
@@ -1304,6 +1418,15 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
         rank_scatter_kernel<<<dg1(U), 256, 0, s>>>(vals, vtmp, flag, pos, U, o - 1, (int32_t*)S);
     }
     tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
+    if (fast_bitset(m)) {  // bitset tables (bitdom.hip)
+        timing_begin(ctx, DM_TIME_DOMINANCE);
+        if ((rc = bitdom_build(s, S, m, U, L.NQ, L.ngroups, nseg, sigma,
+                               fast_table_peel(m) ? nullptr : D, count,
+                               (int32_t*)(ws + L.countq), (char*)part)))
+            return rc;
+        timing_end(ctx, DM_TIME_DOMINANCE);
+        return DM_OK;
+    }
     const unsigned blocks = (unsigned)std::max(1, num_cus) * 8;
     timing_begin(ctx, DM_TIME_DOMINANCE);
     switch (m) {
@@ -1352,7 +1475,7 @@ int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, con
 // fitnesses and individuals) stay on the device.  Fills ufront (front starts
 // in ulist, host; fstarts on the device) and *sorted (individuals).  ws: the
 // fast_dom_build workspace.
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
@@ -1400,8 +1523,12 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     // per generation on one box, profiles/r03d): the sc1 member / key traffic
     // and the barrier polling cost more than the launches they replace.
     static const bool persist = std::getenv("DM_PEEL_PERSIST") != nullptr;
+    // table-fed peel: the bitset pass's tables in the part region
+    const bool tab = fast_table_peel(m);
+    const BitdomLayout TL = bitdom_layout(U, m);
+    const char* tws = ws + L.part;
     int grid = 0;
-    if (persist) {
+    if (persist && !tab) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peel_persistent_kernel,
                                                          PP_THREADS, 0) == hipSuccess)
@@ -1437,8 +1564,22 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int3
     int batch = std::max(2, std::min(ctx->peel_hint + 1, 32));
     for (; grid == 0;) {
         for (int b = 0; b < batch; ++b) {
-            peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
-                D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
+            if (tab) {
+                const dim3 g((unsigned)TL.NG, PEEL_SLICES);
+                const int4* S = (const int4*)(ws + L.S);
+                const int2* span = (const int2*)(tws + TL.span);
+                const uint32_t* P = (const uint32_t*)(tws + TL.P);
+                const int32_t* R = (const int32_t*)(tws + TL.R);
+                if (m == 2)
+                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                                                                     st, countq, lastq, ckey, cq, rankU);
+                else
+                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                                                                     st, countq, lastq, ckey, cq, rankU);
+            } else {
+                peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
+                    D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
+            }
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
         }
         DM_LAUNCH_CHECK();

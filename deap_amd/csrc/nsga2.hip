@@ -35,7 +35,8 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
 int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, const int32_t* ui,
                    const int32_t* order, int64_t T, int32_t* rk);
-int fast_fronts(dm_ctx* ctx, const uint64_t* D, int64_t n, int64_t U, const int32_t* F0,
+bool fast_table_peel(int m);
+int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
@@ -554,7 +555,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         return DM_ERR_INVALID;
     }
     uint64_t* D = (uint64_t*)scratch_slot(
-        ctx, 1, fast ? (size_t)fast_dom_words(U) * 8 : (size_t)U * W * 8);
+        ctx, 1, fast ? (fast_table_peel(m) ? 256 : (size_t)fast_dom_words(U) * 8) : (size_t)U * W * 8);
     if (!D) return DM_ERR_NOMEM;
     char* fwork = nullptr;  // fast path workspace (dominance.hip)
     if (fast) {
@@ -606,7 +607,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         sum_gsize_dev_kernel<<<g1(U), 256, 0, s>>>(ulist, ftotal, gsize, dtotal);
         int64_t total = 0;
         // ufs doubles as the device front-start array
-        if ((rc = fast_fronts(ctx, D, n, U, ftotal, dtotal, N, gsize, ulist, rankU, count, ufs,
+        if ((rc = fast_fronts(ctx, D, m, n, U, ftotal, dtotal, N, gsize, ulist, rankU, count, ufs,
                               fwork, ufront, &total, &last_inds)))
             return rc;
         sorted_inds = total;

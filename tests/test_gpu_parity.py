@@ -395,17 +395,62 @@ def test_dominance_paths_agree_large(gpu, monkeypatch, m):
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
                            valid=np.ones(n))
     got = []
-    for env in (None, "DM_DOM_BALLOT", "DM_DOM_LDS"):
-        monkeypatch.delenv("DM_DOM_BALLOT", raising=False)
-        monkeypatch.delenv("DM_DOM_LDS", raising=False)
+    for env in (None, "DM_DOM_TRI", "DM_DOM_BALLOT", "DM_DOM_LDS", "DM_PEEL_D"):
+        for e in ("DM_DOM_TRI", "DM_DOM_BALLOT", "DM_DOM_LDS", "DM_PEEL_D"):
+            monkeypatch.delenv(e, raising=False)
         if env:
             monkeypatch.setenv(env, "1")
         fronts = tools.sortNondominated(pop, n)
         got.append(([f.cpu().numpy().tolist() for f in fronts],
                     tools.selNSGA2(pop, n // 2).cpu().numpy().tolist(),
                     [len(f) for f in tools.sortNondominated(pop, n // 3)]))
-    assert got[0] == got[1] == got[2]
+    assert got[0] == got[1] == got[2] == got[3] == got[4]
     assert sum(len(f) for f in got[0][0]) == n
+
+
+def _tie_fitness(rng, n, m, kind):
+    if kind == "cont":
+        return rng.uniform(0, 1, size=(n, m))
+    if kind == "ties":  # few values per objective: rank ties in every objective
+        return rng.integers(0, 9, size=(n, m)).astype(np.float64)
+    # objective 0 takes 3 values (tie groups span many 512-v chunks), the
+    # others continuous, a tenth of the rows duplicated
+    wv = np.concatenate([rng.integers(0, 3, size=(n, 1)).astype(np.float64),
+                         rng.uniform(0, 1, size=(n, m - 1))], 1)
+    wv[rng.integers(0, n, n // 10)] = wv[rng.integers(0, n, n // 10)]
+    return wv
+
+
+@pytest.mark.parametrize("m", [2, 3, 4])
+@pytest.mark.parametrize("n", [1, 37, 511, 513, 1100, 2900, 9001])
+def test_bitset_dominance_equals_compare_kernel(gpu, monkeypatch, m, n):
+    """The bitset-table dominance pass with the table-fed peel (bitdom.hip,
+    the default), the same pass writing D for the D-reading peel (DM_PEEL_D)
+    and the integer compare kernel (DM_DOM_TRI), and, up to n = 3,000, the oracle
+    (deap/tools/emo.py:53-117): identical fronts, member for member and in
+    order, on continuous fitnesses, ties in every objective, and objective-0
+    tie groups wider than a 512-v chunk (the prefix / suffix masks), at sizes
+    around one chunk and with a partial last chunk."""
+    from deap_amd import tools
+    rng = np.random.default_rng(1000 * m + n)
+    w = (1.0, -1.0, 1.0, -1.0)[:m]
+    for kind in ("cont", "ties", "obj0"):
+        wv = _tie_fitness(rng, n, m, kind)
+        pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
+                               valid=np.ones(n))
+        got = []
+        for env in (None, "DM_DOM_TRI", "DM_PEEL_D"):
+            for e in ("DM_DOM_TRI", "DM_PEEL_D"):
+                monkeypatch.delenv(e, raising=False)
+            if env:
+                monkeypatch.setenv(env, "1")
+            got.append([f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)])
+        for e in ("DM_DOM_TRI", "DM_PEEL_D"):
+            monkeypatch.delenv(e, raising=False)
+        assert got[0] == got[1] == got[2], kind
+        assert sum(len(f) for f in got[0]) == n
+        if n <= 3000:
+            assert got[0] == ops.sort_nondominated(wv, n), kind
 
 
 def test_front_larger_than_the_lds_sort(gpu, monkeypatch):
