@@ -191,7 +191,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
             sp = span[un];
         }
         uint4 w[4];
-        bd_row_words<M>(cu, lim, u - v0, sP, sR, rot, w);
+        bd_row_words<M>(cu, lim, u - v0, BdLdsSets<F>{sP}, sR, rot, w);
         if (!BD_OK(tword(u, 8 * c, NQ) + 7, (U + 63) / 64 * 64 * NQ * TW, "rows D")) continue;
         uint4* dst = reinterpret_cast<uint4*>(D + tword(u, 8 * c, NQ));
 #if DM_BD_ABLATE & 1  // profiling only: no D stores

@@ -140,9 +140,26 @@ __device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t*
     __syncthreads();
 }
 
-template <int M>
-__device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t ps,
-                                             const uint4 (&sP)[M - 1][BD_K * 4],
+// Sources of the 64-byte prefix sets P_f[C][k] (four 16-byte pieces j):
+// the chunk's tables in LDS, or its slice of the global table (the peel reads
+// only the sets its members need).
+template <int F>
+struct BdLdsSets {
+    const uint4 (&sP)[F][BD_K * 4];
+    __device__ __forceinline__ uint4 operator()(int f, int k, int j) const { return sP[f][k * 4 + j]; }
+};
+struct BdGlobalSets {
+    const uint4* gP;  // the chunk's F x BD_K x 4 pieces
+    __device__ __forceinline__ uint4 operator()(int f, int k, int j) const {
+        return gP[(f * BD_K + k) * 4 + j];
+    }
+};
+
+// Row u's 512 bits over chunk C (positions v0 + p): prefix0(u) (p <= lim) and
+// the prefix sets of its other ranks, without its own bit (position ps when
+// in C); piece i of w holds dwords 4j..4j+3 with j = (i + rot) & 3.
+template <int M, typename Sets>
+__device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t ps, const Sets& sets,
                                              const int32_t (&sR)[M - 1][BD_RP], int rot,
                                              uint4 (&w)[4]) {
     constexpr int F = M - 1;
@@ -161,10 +178,10 @@ __device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int j = (i + rot) & 3;
-        w[i] = sP[0][k[0] * 4 + j];
+        w[i] = sets(0, k[0], j);
 #pragma unroll
         for (int f = 1; f < F; ++f) {
-            const uint4 y = sP[f][k[f] * 4 + j];
+            const uint4 y = sets(f, k[f], j);
             w[i].x &= y.x;
             w[i].y &= y.y;
             w[i].z &= y.z;
@@ -183,6 +200,15 @@ __device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t
             w[i].w &= upto_mask(lim, d0 + 3) & (ds == d0 + 3 ? sb : ~0u);
         }
     }
+}
+
+// The chunk's sorted-rank arrays into LDS (padded, bd_rpad).
+template <int F>
+__device__ __forceinline__ void bd_load_ranks(const int32_t* R, int64_t c, int32_t (&sR)[F][BD_RP]) {
+    const int32_t* g = R + c * F * BD_CW;
+    for (int i = threadIdx.x; i < F * BD_CW; i += blockDim.x)
+        sR[i / BD_CW][bd_rpad(i % BD_CW)] = g[i];
+    __syncthreads();
 }
 
 }  // namespace dm

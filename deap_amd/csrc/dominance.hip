@@ -812,9 +812,11 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
 // Table-fed peel (the default with the bitset pass, 2-3 objectives): one
 // workgroup per 512-v chunk c of the q order and member slice, as
 // peel_owned_kernel, but each member's row bits over c are computed from the
-// chunk's bitset tables held in LDS (bd_row_words: one binary search and one
-// 64-byte set read per objective) instead of read from a stored D, so the
-// dominance matrix is never written.  Member rows, their ranks and tie spans
+// chunk's bitset tables (bd_row_words: a binary search of the chunk's sorted
+// ranks in LDS and one 64-byte prefix-set read from the global table per
+// objective; a workgroup reads only the sets its members need, mostly from
+// L2) instead of read from a stored D, so the dominance matrix is never
+// written.  Member rows, their ranks and tie spans
 // are loaded two 64-member steps ahead (a row's ranks wait on its row index).
 template <int F>
 __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
@@ -824,7 +826,6 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
     uint64_t* ckey, int32_t* cq, int32_t* rankU) {
     static_assert(PEEL_WAVES * 64 == BD_THREADS, "the table loads stride by BD_THREADS");
     constexpr int PW = BD_CW / 64;  // words of a chunk
-    __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
     __shared__ PeelLdsT<BD_CW> L;
     __shared__ PeelSmallT<BD_CW> Sm;
@@ -852,7 +853,8 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
     int2 mrA = mload(j0 + lane), mrB = mload(j0 + STEP + lane);
     int4 suA = S[mrA.x];
     int2 spA = span[mrA.x];
-    bd_load_tables<F>(P, R, c, sP, sR);
+    bd_load_ranks<F>(R, c, sR);
+    const BdGlobalSets sets{reinterpret_cast<const uint4*>(P + c * F * BD_K * 16)};
     const TransposerX tr(lane);
     int32_t dec[PW], last[PW];
 #pragma unroll
@@ -869,7 +871,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
         if (__ballot(has) != 0) {
             uint4 w[4];
             if (has) {
-                bd_row_words<F + 1>(suA, (int64_t)spA.y - v0, (int64_t)mrA.x - v0, sP, sR, 0, w);
+                bd_row_words<F + 1>(suA, (int64_t)spA.y - v0, (int64_t)mrA.x - v0, sets, sR, 0, w);
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) w[i] = make_uint4(0, 0, 0, 0);
