@@ -498,18 +498,21 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     A step is one eaMuPlusLambda generation (deap/algorithms.py:316-329): varOr
     of lambda = N offspring (cxBlend / mutGaussian) with the invalid ones
     evaluated, then selNSGA2(parents + offspring = 2N -> N) and the gather of
-    the chosen rows.  The dominant stage is the all-pairs dominance pass of
-    sortNondominated, VALU-bound: roofline = pairwise fitness comparisons per
-    second (M compares per ordered pair, U(U-1) ordered pairs of unique fits)
-    against the 32-bit integer VALU rate: the dominance kernel compares dense
-    integer ranks (MI355X_MICROARCH.md: 4 SIMD x 32 lanes per CU per cycle ->
-    256 x 128 x 2.4 GHz = 78.6 T lane-ops/s), and SURVEY.md §8d counts one
-    M-objective compare per UNORDERED pair of unique fitnesses, M*U(U-1)/2.
-    ``roofline`` is tri_dom_kernel's own average duration (HIP events the
-    library records around its launches, dm_ctx_set_timing_target), and
-    ``selection`` the same count over the whole selNSGA2.
+    the chosen rows.  The all-pairs stage of sortNondominated is the bitset
+    count pass (bitdom.hip bd_count_kernel: per (v, 512-u chunk) one binary
+    search per objective 1..M-1 over the chunk's sorted ranks and one 64-byte
+    prefix-set read per objective, all in LDS), LDS-bound: ``roofline`` is its
+    LDS bytes per launch — sum over chunks c of reach_c (the v a chunk can
+    dominate) x (M-1) x (11 probes x 4 B + 64 B) — over its average duration
+    (HIP events the library records around the launch,
+    dm_ctx_set_timing_target(DM_TIME_DOMINANCE)), against 256 CU x 256 B/clk x
+    2.4 GHz of LDS reads (MI355X_MICROARCH.md, ds_read_b128).  The §8d count of
+    M*U(U-1)/2 pair compares is reported beside it as a rate (a 32-bit AND of
+    two prefix sets decides 32 pairs, so it exceeds the 78.6 T/s a
+    compare-per-pair kernel could reach); ``selection`` is the whole selNSGA2.
     Replicas only at N > 1 (no exchange)."""
     import ctypes
+    import numpy as np
     import torch
     from deap_amd import _lib, algorithms, base, benchmarks, tools
     from deap_amd.ops import RandomStream
@@ -567,11 +570,19 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     sel_ms = sorted(sel_ms[1:])[(reps - 1) // 2]
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
-    uniq = int(torch.unique(wv, dim=0).shape[0])
+    ufit = torch.unique(wv, dim=0).cpu().numpy()
+    uniq = int(ufit.shape[0])
     cmp_per_sel = float(m) * uniq * (uniq - 1) / 2.0
+    # the count pass's (v, chunk) pairs: v below the reach of each 512-row
+    # chunk of the objective-0 order
+    o0 = np.sort(ufit[:, 0])
+    nch = (uniq + 511) // 512
+    reach = np.searchsorted(o0, o0[np.minimum(np.arange(nch) * 512 + 511, uniq - 1)], side="right")
+    lds_bytes = float(reach.sum()) * (m - 1) * (11 * 4 + 64)
+    lds_peak = 256 * 256 * 2.4e9 / 1e9  # GB/s of LDS reads (256 B/clk/CU)
     valu_peak = 256 * 4 * 32 * 2.4e9 / 1e9  # Gop/s of 32-bit integer VALU lane ops
-    achieved = cmp_per_sel / (dom_ms * 1e-3) / 1e9
-    sel_achieved = cmp_per_sel / (sel_ms * 1e-3) / 1e9
+    achieved = lds_bytes / (dom_ms * 1e-3) / 1e9
+    cmp_rate = cmp_per_sel / (dom_ms * 1e-3) / 1e9
     out = {"metric": "individual-generations/sec @pop=2^17 DTLZ2 NSGA-II (C5)",
            "value": round(n * args.steps * world / elapsed, 1),
            "unit": "individual-generations/sec",
@@ -583,19 +594,19 @@ def bench_nsga2(args, world=1, rank=0, local=0):
                       "operators": "varOr cxBlend(0.5) mutGaussian(0,0.1,1/D) cxpb=0.6 mutpb=0.3",
                       "parallelism": "replicas%d" % world},
            "gen_ms_events": round(gen_ms, 4),
-           "roofline": {"bound": "valu", "achieved": round(achieved, 1), "peak": valu_peak,
-                        "unit": "Gcompare/s", "frac": round(achieved / valu_peak, 4),
-                        "traffic": None, "kernel": "tri_dom_kernel<3>",
-                        "kernel_ms": round(dom_ms, 4),
+           "roofline": {"bound": "lds", "achieved": round(achieved, 1), "peak": lds_peak,
+                        "unit": "GB/s", "frac": round(achieved / lds_peak, 4),
+                        "traffic": None, "kernel": "bd_count_kernel<3>",
+                        "kernel_ms": round(dom_ms, 4), "lds_bytes_per_launch": lds_bytes,
+                        "count": "sum_c reach_c x (M-1) x (11 probes x 4 B + 64-B prefix set)",
+                        "peak_basis": "LDS reads: 256 CU x 256 B/clk x 2.4 GHz",
                         "compares_per_launch": cmp_per_sel,
-                        "count": "M*U(U-1)/2 (one M-objective compare per unordered pair of "
-                                 "unique fitnesses, SURVEY.md 8d)",
-                        "peak_basis": "32-bit int VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz",
+                        "compare_rate_G": round(cmp_rate, 1),
+                        "compare_rate_vs_valu_compare_peak": round(cmp_rate / valu_peak, 4),
                         "unique_fits": uniq, "fronts": len(fronts)},
-           "selection": {"ms": round(sel_ms, 4), "achieved": round(sel_achieved, 1),
-                         "frac": round(sel_achieved / valu_peak, 4),
-                         "what": "whole selNSGA2(2N -> N): ranks, dominance, peel, crowding, "
-                                 "last-front selection"},
+           "selection": {"ms": round(sel_ms, 4),
+                         "what": "whole selNSGA2(2N -> N): ranks, bitset tables, counts, peel, "
+                                 "crowding, last-front selection"},
            "cpu_baseline": None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_nsga2(wv.cpu().numpy(), (-1.0,) * m, n)

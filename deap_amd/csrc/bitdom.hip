@@ -191,7 +191,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
             sp = span[un];
         }
         uint4 w[4];
-        bd_row_words<M>(cu, lim, u - v0, BdLdsSets<F>{sP}, sR, rot, w);
+        bd_row_words<M>(cu, (int32_t)std::min<int64_t>(lim, BD_CW), (int32_t)std::max<int64_t>(-1, std::min<int64_t>(u - v0, BD_CW)), BdLdsSets<F>{sP}, sR, rot, w);
         if (!BD_OK(tword(u, 8 * c, NQ) + 7, (U + 63) / 64 * 64 * NQ * TW, "rows D")) continue;
         uint4* dst = reinterpret_cast<uint4*>(D + tword(u, 8 * c, NQ));
 #if DM_BD_ABLATE & 1  // profiling only: no D stores
@@ -233,10 +233,10 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     bd_load_tables<F>(P, R, c, sP, sR);
     const int rot = threadIdx.x & 3;
     const int64_t v0 = c * BD_CW;
-    const int64_t nvalid = U - v0;  // positions < nvalid are real rows
+    const int32_t nvalid = (int32_t)std::min<int64_t>(U - v0, BD_CW);  // positions < nvalid are real rows
     for (; v < ve; v += BD_THREADS) {
         const int4 cv = sv;
-        const int64_t lo = (int64_t)sf - v0;  // suffix0(v): positions >= lo
+        const int32_t lo = (int32_t)std::max<int64_t>(-1, (int64_t)sf - v0);  // suffix0(v): positions >= lo
         const int64_t vn = v + BD_THREADS;
         if (vn < ve) {
             sv = S[vn];
@@ -299,8 +299,9 @@ __global__ void bd_sum_kernel(const int16_t* __restrict__ part, const int2* __re
 }
 
 template <int M>
-static void bitdom_launch(hipStream_t s, const int4* S, int64_t U, int64_t NQ, const BitdomLayout& L,
+static void bitdom_launch(dm_ctx* ctx, const int4* S, int64_t U, int64_t NQ, const BitdomLayout& L,
                           char* ws, uint64_t* D) {
+    hipStream_t s = ctx->stream;
     const int2* span = (const int2*)(ws + L.span);
     const uint32_t* P = (const uint32_t*)(ws + L.P);
     const int32_t* R = (const int32_t*)(ws + L.R);
@@ -309,14 +310,17 @@ static void bitdom_launch(hipStream_t s, const int4* S, int64_t U, int64_t NQ, c
         bd_rows_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
         S, span, U, NQ, L.NG, (const int32_t*)(ws + L.rowfirst), (const int32_t*)(ws + L.toffD), P,
         R, D);
+    timing_begin(ctx, DM_TIME_DOMINANCE);
     bd_count_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
         S, span, U, L.Upad, L.NG, (const int32_t*)(ws + L.reach), (const int32_t*)(ws + L.toffC), P,
         R, (int16_t*)(ws + L.part));
+    timing_end(ctx, DM_TIME_DOMINANCE);
 }
 
-int bitdom_build(hipStream_t s, const int4* S, int m, int64_t U, int64_t NQ, int64_t ngroups,
+int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64_t ngroups,
                  const int32_t* nseg, const int32_t* sigma, uint64_t* D, int32_t* count,
                  int32_t* countq, char* ws) {
+    hipStream_t s = ctx->stream;
     DM_CHECK_ARG(m >= 2 && m <= 4, "bitdom: 2..4 objectives");
     const BitdomLayout L = bitdom_layout(U, m);
     int32_t* first = (int32_t*)(ws + L.first);
@@ -330,9 +334,9 @@ int bitdom_build(hipStream_t s, const int4* S, int m, int64_t U, int64_t NQ, int
                                       (int32_t*)(ws + L.rowfirst), (int32_t*)(ws + L.reach),
                                       (int32_t*)(ws + L.toffD), (int32_t*)(ws + L.toffC));
     switch (m) {
-        case 2: bitdom_launch<2>(s, S, U, NQ, L, ws, D); break;
-        case 3: bitdom_launch<3>(s, S, U, NQ, L, ws, D); break;
-        default: bitdom_launch<4>(s, S, U, NQ, L, ws, D); break;
+        case 2: bitdom_launch<2>(ctx, S, U, NQ, L, ws, D); break;
+        case 3: bitdom_launch<3>(ctx, S, U, NQ, L, ws, D); break;
+        default: bitdom_launch<4>(ctx, S, U, NQ, L, ws, D); break;
     }
     bd_sum_kernel<<<dg1(U), 256, 0, s>>>((const int16_t*)(ws + L.part), span, U, L.Upad, L.NG,
                                          sigma, count, countq);

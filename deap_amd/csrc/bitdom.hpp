@@ -77,13 +77,20 @@ __device__ __forceinline__ int bd_count_below(const int32_t* sr, int32_t x) {
 }
 
 // dword d of a chunk holds positions 32d..32d+31
-__device__ __forceinline__ uint32_t upto_mask(int64_t lim, int d) {  // positions <= lim
-    const int64_t x = lim - 32 * d;
+__device__ __forceinline__ uint32_t upto_mask(int32_t lim, int d) {  // positions <= lim
+    const int32_t x = lim - 32 * d;
     return x >= 31 ? ~0u : x < 0 ? 0u : (2u << x) - 1u;
 }
-__device__ __forceinline__ uint32_t from_mask(int64_t lo, int d) {  // positions >= lo
-    const int64_t x = lo - 32 * d;
+__device__ __forceinline__ uint32_t from_mask(int32_t lo, int d) {  // positions >= lo
+    const int32_t x = lo - 32 * d;
     return x <= 0 ? ~0u : x > 31 ? 0u : ~0u << x;
+}
+// positions <= lim without position ps, for dword d: dl = lim >> 5, part =
+// the mask of dword dl, ds = ps >> 5 (-1: none), sb = ~bit(ps)
+__device__ __forceinline__ uint32_t row_mask(int32_t dl, uint32_t part, int32_t ds, uint32_t sb,
+                                             int d) {
+    const uint32_t m = d < dl ? ~0u : (d == dl ? part : 0u);
+    return d == ds ? (m & sb) : m;
 }
 
 // The task's chunk (last c with toff[c] <= t) and the tables of that chunk
@@ -159,7 +166,7 @@ struct BdGlobalSets {
 // the prefix sets of its other ranks, without its own bit (position ps when
 // in C); piece i of w holds dwords 4j..4j+3 with j = (i + rot) & 3.
 template <int M, typename Sets>
-__device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t ps, const Sets& sets,
+__device__ __forceinline__ void bd_row_words(const int4 su, int32_t lim, int32_t ps, const Sets& sets,
                                              const int32_t (&sR)[M - 1][BD_RP], int rot,
                                              uint4 (&w)[4]) {
     constexpr int F = M - 1;
@@ -188,16 +195,63 @@ __device__ __forceinline__ void bd_row_words(const int4 su, int64_t lim, int64_t
             w[i].w &= y.w;
         }
     }
-    if (lim < BD_CW - 1 || (ps >= 0 && ps < BD_CW)) {  // prefix0 ends in C, or u is in C
-        const int ds = (ps >= 0 && ps < BD_CW) ? (int)(ps >> 5) : -1;
+    const bool self = (uint32_t)ps < (uint32_t)BD_CW;
+    if (lim < BD_CW - 1 || self) {  // prefix0 ends in C, or u is in C
+        const int32_t dl = lim >= BD_CW - 1 ? 16 : lim >> 5;
+        const uint32_t part = (2u << (lim & 31)) - 1u;
+        const int32_t ds = self ? ps >> 5 : -1;
         const uint32_t sb = ~(1u << (ps & 31));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int d0 = 4 * ((i + rot) & 3);
-            w[i].x &= upto_mask(lim, d0) & (ds == d0 ? sb : ~0u);
-            w[i].y &= upto_mask(lim, d0 + 1) & (ds == d0 + 1 ? sb : ~0u);
-            w[i].z &= upto_mask(lim, d0 + 2) & (ds == d0 + 2 ? sb : ~0u);
-            w[i].w &= upto_mask(lim, d0 + 3) & (ds == d0 + 3 ? sb : ~0u);
+            w[i].x &= row_mask(dl, part, ds, sb, d0);
+            w[i].y &= row_mask(dl, part, ds, sb, d0 + 1);
+            w[i].z &= row_mask(dl, part, ds, sb, d0 + 2);
+            w[i].w &= row_mask(dl, part, ds, sb, d0 + 3);
+        }
+    }
+}
+
+// The pieces of bd_row_words for a software pipeline (the table peel): the
+// searches, the set pieces (raw: loads in flight until used), and the merge.
+template <int F>
+__device__ __forceinline__ void bd_row_k(const int4 su, const int32_t (&sR)[F][BD_RP], int (&k)[F]) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], icomp(su, f));
+}
+template <int F, typename Sets>
+__device__ __forceinline__ void bd_row_fetch(const Sets& sets, const int (&k)[F], uint4 (&raw)[F][4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int f = 0; f < F; ++f) raw[f][i] = sets(f, k[f], i);
+}
+template <int F>
+__device__ __forceinline__ void bd_row_merge(const uint4 (&raw)[F][4], int32_t lim, int32_t ps,
+                                             uint4 (&w)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w[i] = raw[0][i];
+#pragma unroll
+        for (int f = 1; f < F; ++f) {
+            w[i].x &= raw[f][i].x;
+            w[i].y &= raw[f][i].y;
+            w[i].z &= raw[f][i].z;
+            w[i].w &= raw[f][i].w;
+        }
+    }
+    const bool self = (uint32_t)ps < (uint32_t)BD_CW;
+    if (lim < BD_CW - 1 || self) {
+        const int32_t dl = lim >= BD_CW - 1 ? 16 : (lim < 0 ? -1 : lim >> 5);
+        const uint32_t part = lim < 0 ? 0u : (2u << (lim & 31)) - 1u;
+        const int32_t ds = self ? ps >> 5 : -1;
+        const uint32_t sb = ~(1u << (ps & 31));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            w[i].x &= row_mask(dl, part, ds, sb, 4 * i);
+            w[i].y &= row_mask(dl, part, ds, sb, 4 * i + 1);
+            w[i].z &= row_mask(dl, part, ds, sb, 4 * i + 2);
+            w[i].w &= row_mask(dl, part, ds, sb, 4 * i + 3);
         }
     }
 }

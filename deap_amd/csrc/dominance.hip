@@ -598,12 +598,21 @@ struct PeelSmallT {
 typedef PeelLdsT<PEEL_PV> PeelLds;
 typedef PeelSmallT<PEEL_PV> PeelSmall;
 
+// Per-v values a peel kernel may load in its prologue, long before the
+// release needs them (the release's chain countq -> sigma -> gsize is then
+// three dependent loads shorter): the count, the U index and the individual
+// count of each v of the thread.
+template <int IT>
+struct PeelPre {
+    int32_t cnt[IT], vu[IT], gs[IT];
+};
 template <bool COH, int PW>
 __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW], int64_t vbase,
                              const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
-                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S);
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
+                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre = nullptr);
 
 // Slice y of the nsl slices of row segment s for the front of sF unique
 // fitnesses starting at sust in ulist / mrow (front number snf).
@@ -693,7 +702,8 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
                              const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
-                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S) {
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
+                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre) {
     constexpr int PEEL_IT = PeelSmallT<PW * 64>::IT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -721,7 +731,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         fresh[it] = false;
         if (v < U && d > 0) {
             if (nsl == 1) {
-                const int32_t left = cld<COH>(countq + v) - d;
+                const int32_t left = (pre ? pre->cnt[it] : cld<COH>(countq + v)) - d;
                 cst<COH>(countq + v, left);
                 fresh[it] = left == 0;
             } else {
@@ -742,9 +752,9 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
             }
         }
         lk[it] = l;
-        vu[it] = fresh[it] ? sigma[v] : 0;
+        vu[it] = fresh[it] ? (pre ? pre->vu[it] : sigma[v]) : 0;
         fm[it] = __ballot(fresh[it]);
-        int64_t gs = fresh[it] ? gsize[vu[it]] : 0;
+        int64_t gs = fresh[it] ? (pre ? pre->gs[it] : gsize[vu[it]]) : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
         if (lane == 0) {
@@ -818,30 +828,53 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
 // L2) instead of read from a stored D, so the dominance matrix is never
 // written.  Member rows, their ranks and tie spans
 // are loaded two 64-member steps ahead (a row's ranks wait on its row index).
+#ifndef DM_PEEL_TAB_MINW
+#define DM_PEEL_TAB_MINW 1  // min waves per SIMD the table peel is compiled for (A/B)
+#endif
 template <int F>
-__global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
+__global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_kernel(
     const int4* __restrict__ S, const int2* __restrict__ span, const uint32_t* __restrict__ P,
     const int32_t* __restrict__ R, const int2* __restrict__ mrow, const int32_t* __restrict__ gsize,
     const int32_t* __restrict__ sigma, FrontState* st, int32_t* countq, unsigned long long* lastq,
     uint64_t* ckey, int32_t* cq, int32_t* rankU) {
-    static_assert(PEEL_WAVES * 64 == BD_THREADS, "the table loads stride by BD_THREADS");
+    static_assert(PEEL_WAVES * 64 == BD_CW, "one thread per v of the chunk (sorted ranks, release)");
     constexpr int PW = BD_CW / 64;  // words of a chunk
     __shared__ int32_t sR[F][BD_RP];
     __shared__ PeelLdsT<BD_CW> L;
     __shared__ PeelSmallT<BD_CW> Sm;
     __shared__ int32_t sF, sust, sstop, snf;
+    __shared__ int64_t sU;
+    // grid x = NG rounded up to a multiple of 8: the slices y of chunk c (linear
+    // workgroup ids c + y gridDim.x) land on one XCD, whose L2 then serves
+    // the chunk's table slice to all of them
+    const int64_t c = blockIdx.x;
+    const int64_t NG = (st->U + BD_CW - 1) / BD_CW;
+    if (c >= NG) return;
+    // loads that do not depend on the front go out first: the chunk's sorted
+    // ranks, and this thread's v (count, U index, individual count)
+    const int32_t* gR = R + c * F * BD_CW;
+    int32_t rr[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) rr[f] = gR[f * BD_CW + threadIdx.x];
     if (threadIdx.x == 0) {
         sF = st->F;
         sust = st->ustart;
         snf = st->nfronts;
         sstop = st->done | st->overflow;
+        sU = st->U;
     }
     __syncthreads();
     if (sstop) return;
-    const int64_t c = blockIdx.x;
-    const int64_t nsl = peel_slices(sF, c, gridDim.x, gridDim.y);
+    const int64_t nsl = peel_slices(sF, c, NG, gridDim.y);
     if ((int64_t)blockIdx.y >= nsl) return;
-    const int64_t U = st->U;
+    const int64_t U = sU;
+    PeelPre<1> pre;
+    {
+        const int64_t v = c * BD_CW + threadIdx.x;
+        pre.cnt[0] = v < U ? countq[v] : 0;
+        pre.vu[0] = v < U ? sigma[v] : 0;
+        pre.gs[0] = v < U ? gsize[pre.vu[0]] : 0;
+    }
     const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
     const int64_t j0s = blockIdx.y * slen;
     const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
@@ -853,7 +886,9 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
     int2 mrA = mload(j0 + lane), mrB = mload(j0 + STEP + lane);
     int4 suA = S[mrA.x];
     int2 spA = span[mrA.x];
-    bd_load_ranks<F>(R, c, sR);
+#pragma unroll
+    for (int f = 0; f < F; ++f) sR[f][bd_rpad(threadIdx.x)] = rr[f];
+    __syncthreads();
     const BdGlobalSets sets{reinterpret_cast<const uint4*>(P + c * F * BD_K * 16)};
     const TransposerX tr(lane);
     int32_t dec[PW], last[PW];
@@ -863,19 +898,35 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
         last[w] = -1;
     }
     const int64_t v0 = c * BD_CW;
+    // two-stage software pipeline over the wave's 64-member groups: the next
+    // group's searches run and its set loads are in flight while this
+    // group's bits are transposed.  A lane without a member (or whose row does
+    // not reach the chunk) searches nothing and reads P[0] = the empty set.
+    auto stage = [&](const int2 mr, const int4 su, const int2 sp, int64_t jj, int32_t& lim,
+                     int32_t& ps, uint4 (&raw)[F][4]) {
+        int k[F];
+        const bool h = jj + lane < Fm && c < mr.y;
+        lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)sp.y - v0, BD_CW));
+        ps = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mr.x - v0, BD_CW));
+        if (h && lim >= 0) {
+            bd_row_k<F>(su, sR, k);
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; ++f) k[f] = 0;
+        }
+        bd_row_fetch<F>(sets, k, raw);
+        return h;
+    };
+    int32_t limA, psA;
+    uint4 rawA[F][4];
+    bool hasA = j0 < Fm ? stage(mrA, suA, spA, j0, limA, psA, rawA) : false;
     for (; j0 < Fm; j0 += STEP) {
         const int2 mrC = mload(j0 + 2 * STEP + lane);
         const int4 suB = S[mrB.x];
         const int2 spB = span[mrB.x];
-        const bool has = j0 + lane < Fm && c < mrA.y;
-        if (__ballot(has) != 0) {
+        if (__ballot(hasA) != 0) {
             uint4 w[4];
-            if (has) {
-                bd_row_words<F + 1>(suA, (int64_t)spA.y - v0, (int64_t)mrA.x - v0, sets, sR, 0, w);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) w[i] = make_uint4(0, 0, 0, 0);
-            }
+            bd_row_merge<F>(rawA, limA, psA, w);
             uint32_t lo[8], hi[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -892,13 +943,11 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, 1) void peel_tab_kernel(
                 if (top >= 0) last[w2] = (int32_t)(j0 + top);
             }
         }
-        mrA = mrB;
-        suA = suB;
-        spA = spB;
+        if (j0 + STEP < Fm) hasA = stage(mrB, suB, spB, j0 + STEP, limA, psA, rawA);
         mrB = mrC;
     }
     peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
-                            snf, nsl, L, Sm);
+                            snf, nsl, L, Sm, &pre);
 }
 
 constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
@@ -1420,15 +1469,10 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
         rank_scatter_kernel<<<dg1(U), 256, 0, s>>>(vals, vtmp, flag, pos, U, o - 1, (int32_t*)S);
     }
     tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
-    if (fast_bitset(m)) {  // bitset tables (bitdom.hip)
-        timing_begin(ctx, DM_TIME_DOMINANCE);
-        if ((rc = bitdom_build(s, S, m, U, L.NQ, L.ngroups, nseg, sigma,
-                               fast_table_peel(m) ? nullptr : D, count,
-                               (int32_t*)(ws + L.countq), (char*)part)))
-            return rc;
-        timing_end(ctx, DM_TIME_DOMINANCE);
-        return DM_OK;
-    }
+    if (fast_bitset(m))  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)
+        return bitdom_build(ctx, S, m, U, L.NQ, L.ngroups, nseg, sigma,
+                            fast_table_peel(m) ? nullptr : D, count, (int32_t*)(ws + L.countq),
+                            (char*)part);
     const unsigned blocks = (unsigned)std::max(1, num_cus) * 8;
     timing_begin(ctx, DM_TIME_DOMINANCE);
     switch (m) {
@@ -1567,7 +1611,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     for (; grid == 0;) {
         for (int b = 0; b < batch; ++b) {
             if (tab) {
-                const dim3 g((unsigned)TL.NG, PEEL_SLICES);
+                const dim3 g((unsigned)((TL.NG + 7) & ~7ll), PEEL_SLICES);
                 const int4* S = (const int4*)(ws + L.S);
                 const int2* span = (const int2*)(tws + TL.span);
                 const uint32_t* P = (const uint32_t*)(tws + TL.P);

@@ -39,7 +39,7 @@ __host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t 
 // scratch of bitdom_bytes(U, m) bytes, which keeps the tables for the
 // table-fed peel.
 size_t bitdom_bytes(int64_t U, int m);
-int bitdom_build(hipStream_t s, const int4* S, int m, int64_t U, int64_t NQ, int64_t ngroups,
+int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64_t ngroups,
                  const int32_t* nseg, const int32_t* sigma, uint64_t* D, int32_t* count,
                  int32_t* countq, char* ws);
 

@@ -121,11 +121,22 @@ struct TransposerX {
             lo[w] = __builtin_amdgcn_perm(rl, lo[w], sel16);
             hi[w] = __builtin_amdgcn_perm(rh, hi[w], sel16);
         }
+        {
+            // the two-step DPP partners: every word's first step before any
+            // second step (a DPP reading the VGPR the previous VALU wrote needs
+            // wait states, s_nop when nothing else can fill them)
+            uint32_t tl[N], th[N];
 #pragma unroll
-        for (int w = 0; w < N; ++w) {
-            const uint32_t rl = dpp<0x141>(dpp<0x140>(lo[w])), rh = dpp<0x141>(dpp<0x140>(hi[w]));
-            lo[w] = __builtin_amdgcn_perm(rl, lo[w], sel8);
-            hi[w] = __builtin_amdgcn_perm(rh, hi[w], sel8);
+            for (int w = 0; w < N; ++w) {
+                tl[w] = dpp<0x140>(lo[w]);
+                th[w] = dpp<0x140>(hi[w]);
+            }
+#pragma unroll
+            for (int w = 0; w < N; ++w) {
+                const uint32_t rl = dpp<0x141>(tl[w]), rh = dpp<0x141>(th[w]);
+                lo[w] = __builtin_amdgcn_perm(rl, lo[w], sel8);
+                hi[w] = __builtin_amdgcn_perm(rh, hi[w], sel8);
+            }
         }
         bits<N, 0x1B, true>(lo, hi, m4, r4);
         bits<N, 0x4E, false>(lo, hi, m2, r2);
@@ -134,12 +145,21 @@ struct TransposerX {
     template <int N, int QP, bool HM>
     __device__ __forceinline__ static void bits(uint32_t (&lo)[N], uint32_t (&hi)[N], uint32_t m,
                                                 uint32_t rot) {
+        uint32_t rl[N], rh[N];
 #pragma unroll
         for (int w = 0; w < N; ++w) {
-            const uint32_t rl = HM ? dpp<QP>(dpp<0x141>(lo[w])) : dpp<QP>(lo[w]);
-            const uint32_t rh = HM ? dpp<QP>(dpp<0x141>(hi[w])) : dpp<QP>(hi[w]);
-            const uint32_t tl = __builtin_amdgcn_alignbit(rl, rl, rot);
-            const uint32_t th = __builtin_amdgcn_alignbit(rh, rh, rot);
+            rl[w] = HM ? dpp<0x141>(lo[w]) : lo[w];
+            rh[w] = HM ? dpp<0x141>(hi[w]) : hi[w];
+        }
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            rl[w] = dpp<QP>(rl[w]);
+            rh[w] = dpp<QP>(rh[w]);
+        }
+#pragma unroll
+        for (int w = 0; w < N; ++w) {
+            const uint32_t tl = __builtin_amdgcn_alignbit(rl[w], rl[w], rot);
+            const uint32_t th = __builtin_amdgcn_alignbit(rh[w], rh[w], rot);
             lo[w] = (m & lo[w]) | (~m & tl);
             hi[w] = (m & hi[w]) | (~m & th);
         }
