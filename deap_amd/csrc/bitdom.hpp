@@ -226,7 +226,10 @@ __device__ __forceinline__ void bd_row_fetch(const Sets& sets, const int (&k)[F]
 #pragma unroll
         for (int f = 0; f < F; ++f) raw[f][i] = sets(f, k[f], i);
 }
-template <int F>
+// SELF = false (the peel): u's own bit is left set — u is a member of the
+// front being peeled, its count is already zero and one more decrement
+// releases nothing; only the objective-0 prefix is masked.
+template <int F, bool SELF = true>
 __device__ __forceinline__ void bd_row_merge(const uint4 (&raw)[F][4], int32_t lim, int32_t ps,
                                              uint4 (&w)[4]) {
 #pragma unroll
@@ -240,18 +243,28 @@ __device__ __forceinline__ void bd_row_merge(const uint4 (&raw)[F][4], int32_t l
             w[i].w &= raw[f][i].w;
         }
     }
-    const bool self = (uint32_t)ps < (uint32_t)BD_CW;
+    const bool self = SELF && (uint32_t)ps < (uint32_t)BD_CW;
     if (lim < BD_CW - 1 || self) {
         const int32_t dl = lim >= BD_CW - 1 ? 16 : (lim < 0 ? -1 : lim >> 5);
         const uint32_t part = lim < 0 ? 0u : (2u << (lim & 31)) - 1u;
-        const int32_t ds = self ? ps >> 5 : -1;
-        const uint32_t sb = ~(1u << (ps & 31));
+        if (SELF) {
+            const int32_t ds = self ? ps >> 5 : -1;
+            const uint32_t sb = ~(1u << (ps & 31));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            w[i].x &= row_mask(dl, part, ds, sb, 4 * i);
-            w[i].y &= row_mask(dl, part, ds, sb, 4 * i + 1);
-            w[i].z &= row_mask(dl, part, ds, sb, 4 * i + 2);
-            w[i].w &= row_mask(dl, part, ds, sb, 4 * i + 3);
+            for (int i = 0; i < 4; ++i) {
+                w[i].x &= row_mask(dl, part, ds, sb, 4 * i);
+                w[i].y &= row_mask(dl, part, ds, sb, 4 * i + 1);
+                w[i].z &= row_mask(dl, part, ds, sb, 4 * i + 2);
+                w[i].w &= row_mask(dl, part, ds, sb, 4 * i + 3);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[i].x &= 4 * i < dl ? ~0u : (4 * i == dl ? part : 0u);
+                w[i].y &= 4 * i + 1 < dl ? ~0u : (4 * i + 1 == dl ? part : 0u);
+                w[i].z &= 4 * i + 2 < dl ? ~0u : (4 * i + 2 == dl ? part : 0u);
+                w[i].w &= 4 * i + 3 < dl ? ~0u : (4 * i + 3 == dl ? part : 0u);
+            }
         }
     }
 }

@@ -926,7 +926,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         const int2 spB = span[mrB.x];
         if (__ballot(hasA) != 0) {
             uint4 w[4];
-            bd_row_merge<F>(rawA, limA, psA, w);
+            bd_row_merge<F, false>(rawA, limA, psA, w);
             uint32_t lo[8], hi[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1648,7 +1648,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
         // ~10 us; each extra status check a round trip)
         const double mean = (double)hst->sorted / (double)(hst->nfronts + 1);
         const double left = (double)(hst->N - hst->sorted);
-        const int need = mean > 0 ? (int)std::ceil(left / mean) : 32;
+        int need = mean > 0 ? (int)std::ceil(left / mean) : 32;
+        // the previous call's front count, when it had more fronts than done
+        // so far, is the better estimate (later fronts are larger than the
+        // mean so far); launches past `done` return at once but cost ~10 us
+        if (ctx->peel_hint > hst->nfronts) need = std::min(need, ctx->peel_hint - hst->nfronts + 1);
         batch = std::max(2, std::min(need + 2, 32));
     }
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones

@@ -82,6 +82,9 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
     c2ab)
       step c2_keys 200 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline
       step c2_nokeys 200 env DM_BITS_NOKEYS=1 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
+    pmc_c2sq)
+      step pmc_c2sq1 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_BUSY_CYCLES -d $OUT/pmc_c2sq1 -o run --output-format csv -- python3 bench.py --config c2 --steps 4 --warmup 1 --no-cpu-baseline
+      step pmc_c2sq2 200 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INSTS_SMEM -d $OUT/pmc_c2sq2 -o run --output-format csv -- python3 bench.py --config c2 --steps 4 --warmup 1 --no-cpu-baseline ;;
     pmc_c5sq) step pmc_c5sq 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS -d $OUT/pmc_c5sq -o run --output-format csv -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
