@@ -199,7 +199,9 @@ def test_ea_simple_bookkeeping_cost_at_full_size(gpu):
             assert best <= min(mins) + 1e-9
     plain = min(res["plain"], res["plain2"])
     print("eaSimple ms/gen at 2^20: plain %.3f, with stats+hof %.3f" % (plain, res["stats+hof"]))
-    assert res["stats+hof"] < 1.5 * plain + 2.0
+    # measured +0.28 ms (8 %); the bound fails a bookkeeping
+    # regression of a third of the generation, not box-to-box noise
+    assert res["stats+hof"] < 1.2 * plain + 0.5
 
 
 @pytest.mark.parametrize("n,k", [(200, 1), (4097, 15), (100000, 32), (1 << 20, 15),
