@@ -108,41 +108,33 @@ __device__ __forceinline__ int64_t bd_task_chunk(const int32_t* toff, int64_t NG
 template <int F>
 __device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t* R, int64_t c,
                                                uint4 (&sP)[F][BD_K * 4], int32_t (&sR)[F][BD_RP]) {
-    // every global load of the thread first, then the LDS stores (a load ->
-    // wait -> store loop exposes the global latency once per piece)
+    // batches of 4 global loads in flight, then their LDS stores: the staging
+    // stays in registers (a whole-table register array of up to 13 pieces was
+    // placed in scratch memory by the compiler)
     constexpr int NP = F * BD_K * 4, NR = F * BD_CW / 4;
-    constexpr int LP = (NP + BD_THREADS - 1) / BD_THREADS, LR = (NR + BD_THREADS - 1) / BD_THREADS;
     const uint4* gP = reinterpret_cast<const uint4*>(P + c * F * BD_K * 16);
     const int4* gR = reinterpret_cast<const int4*>(R + c * F * BD_CW);
-    uint4 tp[LP];
-    int4 tr[LR];
-#pragma unroll
-    for (int j = 0; j < LP; ++j) {
-        const int i = threadIdx.x + j * BD_THREADS;
-        if (i < NP) tp[j] = gP[i];
-    }
-#pragma unroll
-    for (int j = 0; j < LR; ++j) {
-        const int i = threadIdx.x + j * BD_THREADS;
-        if (i < NR) tr[j] = gR[i];
-    }
     uint4* lP = &sP[0][0];
-#pragma unroll
-    for (int j = 0; j < LP; ++j) {
-        const int i = threadIdx.x + j * BD_THREADS;
-        if (i < NP) lP[i] = tp[j];
+    for (int i0 = threadIdx.x; i0 < NP; i0 += 4 * BD_THREADS) {
+        uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0, t2 = t0, t3 = t0;
+        const int i1 = i0 + BD_THREADS, i2 = i1 + BD_THREADS, i3 = i2 + BD_THREADS;
+        t0 = gP[i0];
+        if (i1 < NP) t1 = gP[i1];
+        if (i2 < NP) t2 = gP[i2];
+        if (i3 < NP) t3 = gP[i3];
+        lP[i0] = t0;
+        if (i1 < NP) lP[i1] = t1;
+        if (i2 < NP) lP[i2] = t2;
+        if (i3 < NP) lP[i3] = t3;
     }
-#pragma unroll
-    for (int j = 0; j < LR; ++j) {
-        const int i = threadIdx.x + j * BD_THREADS;  // values 4i..4i+3 of the F arrays
-        if (i < NR) {
-            const int f = (4 * i) / BD_CW, e = (4 * i) % BD_CW;
-            int32_t* d = &sR[f][0];
-            d[bd_rpad(e)] = tr[j].x;
-            d[bd_rpad(e + 1)] = tr[j].y;
-            d[bd_rpad(e + 2)] = tr[j].z;
-            d[bd_rpad(e + 3)] = tr[j].w;
-        }
+    for (int i = threadIdx.x; i < NR; i += BD_THREADS) {  // values 4i..4i+3 of the F arrays
+        const int4 t = gR[i];
+        const int f = (4 * i) / BD_CW, e = (4 * i) % BD_CW;
+        int32_t* d = &sR[f][0];
+        d[bd_rpad(e)] = t.x;
+        d[bd_rpad(e + 1)] = t.y;
+        d[bd_rpad(e + 2)] = t.z;
+        d[bd_rpad(e + 3)] = t.w;
     }
     __syncthreads();
 }

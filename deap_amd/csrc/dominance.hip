@@ -1619,8 +1619,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 if (m == 2)
                     peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
-                else
+                else if (m == 3)
                     peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                                                                     st, countq, lastq, ckey, cq, rankU);
+                else
+                    peel_tab_kernel<3><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
             } else {
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
