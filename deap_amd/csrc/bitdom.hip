@@ -62,8 +62,10 @@ __global__ void bd_span_kernel(const int4* __restrict__ S, int m, int64_t U,
 __global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __restrict__ S,
                                                               int64_t U, int F,
                                                               uint32_t* __restrict__ P,
-                                                              int32_t* __restrict__ R) {
+                                                              int32_t* __restrict__ R,
+                                                              uint16_t* __restrict__ BK) {
     __shared__ int32_t r[BD_CW];
+    __shared__ int32_t sorted[BD_CW];
     const int64_t c = blockIdx.x;
     const int f = blockIdx.y;
     const int t = threadIdx.x;
@@ -78,7 +80,23 @@ __global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __rest
         lr += (ri < rv || (ri == rv && i < t)) ? 1 : 0;
     }
     const int64_t cf = c * F + f;
-    if (BD_OK(lr, BD_CW, "table lr")) R[cf * BD_CW + lr] = rv;
+    if (BD_OK(lr, BD_CW, "table lr")) {
+        R[cf * BD_CW + lr] = rv;
+        sorted[lr] = rv;
+    }
+    __syncthreads();
+    // bucket starts: BK[b] = #{sorted ranks < b << sh}
+    const int sh = bd_bucket_shift(U);
+    for (int b = t; b < BD_BKN; b += BD_THREADS) {
+        const int64_t th = (int64_t)b << sh;
+        int lo = 0, hi = BD_CW;  // first j with sorted[j] >= th
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((int64_t)sorted[mid] < th) lo = mid + 1;
+            else hi = mid;
+        }
+        BK[cf * BD_BKN + b] = (uint16_t)lo;
+    }
     uint32_t* Pc = P + cf * BD_K * 16;
     const int wave = t >> 6, lane = t & 63;
     for (int k0 = 0; k0 < BD_K; k0 += 64) {
@@ -167,10 +185,13 @@ template <int M>
 __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
     const int4* __restrict__ S, const int2* __restrict__ span, int64_t U, int64_t NQ, int64_t NG,
     const int32_t* __restrict__ rowfirst, const int32_t* __restrict__ toffD,
-    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, uint64_t* __restrict__ D) {
+    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
+    uint64_t* __restrict__ D) {
     constexpr int F = M - 1;
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
+    __shared__ uint16_t sB[F][BD_BKN];
+    const int sh = bd_bucket_shift(U);
     const int32_t t = blockIdx.x;
     if (t >= toffD[NG]) return;
     const int64_t c = bd_task_chunk<F>(toffD, NG, t);
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
     int64_t u = row0 + threadIdx.x;
     int4 su = u < row1 ? S[u] : make_int4(0, 0, 0, 0);
     int2 sp = u < row1 ? span[u] : make_int2(0, 0);
-    bd_load_tables<F>(P, R, c, sP, sR);
+    bd_load_tables<F>(P, R, BK, c, sP, sR, sB);
     const int rot = threadIdx.x & 3;
     const int64_t v0 = c * BD_CW;
     for (; u < row1; u += BD_THREADS) {
@@ -191,7 +212,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
             sp = span[un];
         }
         uint4 w[4];
-        bd_row_words<M>(cu, (int32_t)std::min<int64_t>(lim, BD_CW), (int32_t)std::max<int64_t>(-1, std::min<int64_t>(u - v0, BD_CW)), BdLdsSets<F>{sP}, sR, rot, w);
+        bd_row_words<M>(cu, (int32_t)std::min<int64_t>(lim, BD_CW), (int32_t)std::max<int64_t>(-1, std::min<int64_t>(u - v0, BD_CW)), BdLdsSets<F>{sP}, sR, sB, sh, rot, w);
         if (!BD_OK(tword(u, 8 * c, NQ) + 7, (U + 63) / 64 * 64 * NQ * TW, "rows D")) continue;
         uint4* dst = reinterpret_cast<uint4*>(D + tword(u, 8 * c, NQ));
 #if DM_BD_ABLATE & 1  // profiling only: no D stores
@@ -218,10 +239,13 @@ template <int M>
 __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     const int4* __restrict__ S, const int2* __restrict__ span, int64_t U, int64_t Upad, int64_t NG,
     const int32_t* __restrict__ reach, const int32_t* __restrict__ toffC,
-    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, int16_t* __restrict__ part) {
+    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
+    int16_t* __restrict__ part) {
     constexpr int F = M - 1;
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
+    __shared__ uint16_t sB[F][BD_BKN];
+    const int sh = bd_bucket_shift(U);
     const int32_t t = blockIdx.x;
     if (t >= toffC[NG]) return;
     const int64_t c = bd_task_chunk<F>(toffC, NG, t);
@@ -230,7 +254,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     int64_t v = vb + threadIdx.x;
     int4 sv = v < ve ? S[v] : make_int4(0, 0, 0, 0);
     int32_t sf = v < ve ? span[v].x : 0;
-    bd_load_tables<F>(P, R, c, sP, sR);
+    bd_load_tables<F>(P, R, BK, c, sP, sR, sB);
     const int rot = threadIdx.x & 3;
     const int64_t v0 = c * BD_CW;
     const int32_t nvalid = (int32_t)std::min<int64_t>(U - v0, BD_CW);  // positions < nvalid are real rows
@@ -244,7 +268,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
         }
         int k[F];
 #pragma unroll
-        for (int f = 0; f < F; ++f) k[f] = bd_count_below<false>(sR[f], icomp(cv, f));
+        for (int f = 0; f < F; ++f) k[f] = bd_count_below<false>(sR[f], sB[f], sh, icomp(cv, f));
         uint32_t cnt = 0;
         const bool edge = lo > 0 || nvalid < BD_CW;
 #pragma unroll
@@ -305,15 +329,16 @@ static void bitdom_launch(dm_ctx* ctx, const int4* S, int64_t U, int64_t NQ, con
     const int2* span = (const int2*)(ws + L.span);
     const uint32_t* P = (const uint32_t*)(ws + L.P);
     const int32_t* R = (const int32_t*)(ws + L.R);
+    const uint16_t* BK = (const uint16_t*)(ws + L.BK);
     const int64_t maxtasks = L.NG * ((U + BD_RT - 1) / BD_RT);
     if (D)  // D words only for the D-reading peel (the table-fed peel needs none)
         bd_rows_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
         S, span, U, NQ, L.NG, (const int32_t*)(ws + L.rowfirst), (const int32_t*)(ws + L.toffD), P,
-        R, D);
+        R, BK, D);
     timing_begin(ctx, DM_TIME_DOMINANCE);
     bd_count_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
         S, span, U, L.Upad, L.NG, (const int32_t*)(ws + L.reach), (const int32_t*)(ws + L.toffC), P,
-        R, (int16_t*)(ws + L.part));
+        R, BK, (int16_t*)(ws + L.part));
     timing_end(ctx, DM_TIME_DOMINANCE);
 }
 
@@ -329,7 +354,7 @@ int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64
     bd_ties_kernel<<<dg1(U), 256, 0, s>>>(S, m, U, first, last);
     bd_span_kernel<<<dg1(U), 256, 0, s>>>(S, m, U, first, last, span);
     bd_table_kernel<<<dim3((unsigned)L.NG, (unsigned)(m - 1)), BD_THREADS, 0, s>>>(
-        S, U, m - 1, (uint32_t*)(ws + L.P), (int32_t*)(ws + L.R));
+        S, U, m - 1, (uint32_t*)(ws + L.P), (int32_t*)(ws + L.R), (uint16_t*)(ws + L.BK));
     bd_plan_kernel<<<1, 1024, 0, s>>>(S, m, last, nseg, U, L.NG, ngroups,
                                       (int32_t*)(ws + L.rowfirst), (int32_t*)(ws + L.reach),
                                       (int32_t*)(ws + L.toffD), (int32_t*)(ws + L.toffC));

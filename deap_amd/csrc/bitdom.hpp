@@ -10,6 +10,14 @@ constexpr int BD_CW = 512;        // v of a chunk
 constexpr int BD_K = BD_CW + 1;   // prefix sets per chunk and objective
 constexpr int BD_RT = 16384;      // rows (row pass) / v (count pass) per task
 constexpr int BD_THREADS = 512;
+// bucket starts per chunk and objective: bucket b holds the ranks in
+// [b << sh, (b + 1) << sh), sh the smallest shift with U >> sh <= 1024
+constexpr int BD_BKN = 1026;
+__host__ __device__ __forceinline__ int bd_bucket_shift(int64_t U) {
+    int sh = 0;
+    while ((U >> sh) > 1024) ++sh;
+    return sh;
+}
 
 #ifndef DM_BD_ABLATE
 #define DM_BD_ABLATE 0
@@ -31,7 +39,7 @@ __device__ __forceinline__ bool bd_ok(int64_t i, int64_t n, const char* tag) {
 
 struct BitdomLayout {
     int64_t NB, NG, Upad;
-    size_t part, P, R, first, last, span, rowfirst, reach, toffD, toffC, total;
+    size_t part, P, R, BK, first, last, span, rowfirst, reach, toffD, toffC, total;
 };
 static inline BitdomLayout bitdom_layout(int64_t U, int m) {
     BitdomLayout L;
@@ -48,6 +56,7 @@ static inline BitdomLayout bitdom_layout(int64_t U, int m) {
     L.part = take((size_t)L.NG * L.Upad * 2);
     L.P = take((size_t)L.NG * F * BD_K * 64);
     L.R = take((size_t)L.NG * F * BD_CW * 4);
+    L.BK = take((size_t)L.NG * F * BD_BKN * 2);
     L.first = take((size_t)U * 4);
     L.last = take((size_t)U * 4);
     L.span = take((size_t)U * 8);
@@ -59,21 +68,25 @@ static inline BitdomLayout bitdom_layout(int64_t U, int m) {
     return L;
 }
 // #{j : sr[j] <= x} (LE) or #{j : sr[j] < x} over 512 ascending values held
-// in LDS with one pad word after every 32 (value j at j + j / 32): without
-// the pads every probe of a binary-search step h >= 16 lies in one bank (the
-// probes are lo + h - 1 with lo a multiple of 2h), a 16-way conflict by step 5.
+// in LDS with one pad word after every 32 (value j at j + j / 32, bd_rpad),
+// starting from the bucket table sb: sb[b] = #{j : sr[j] < b << sh}, so only
+// the values of x's own bucket are scanned (0.6 of them on average at 512
+// values per ~830 buckets) — two or three dependent LDS reads where a binary
+// search over the 512 needs ten.
 constexpr int BD_RP = BD_CW + BD_CW / 32;  // padded sorted-rank array
 __device__ __forceinline__ int bd_rpad(int j) { return j + (j >> 5); }
 template <bool LE>
-__device__ __forceinline__ int bd_count_below(const int32_t* sr, int32_t x) {
-    int lo = 0;
-#pragma unroll
-    for (int h = 256; h > 0; h >>= 1) {
-        const int32_t y = sr[bd_rpad(lo + h - 1)];
-        lo += (LE ? y <= x : y < x) ? h : 0;
+__device__ __forceinline__ int bd_count_below(const int32_t* sr, const uint16_t* sb, int sh,
+                                              int32_t x) {
+    const int b = x >> sh;
+    int j = sb[b];
+    const int e = sb[b + 1];
+    while (j < e) {
+        const int32_t y = sr[bd_rpad(j)];
+        if (!(LE ? y <= x : y < x)) break;
+        ++j;
     }
-    const int32_t y = sr[bd_rpad(lo)];
-    return lo + ((LE ? y <= x : y < x) ? 1 : 0);
+    return j;
 }
 
 // dword d of a chunk holds positions 32d..32d+31
@@ -105,9 +118,19 @@ __device__ __forceinline__ int64_t bd_task_chunk(const int32_t* toff, int64_t NG
     }
     return lo;
 }
+// The chunk's bucket tables (F x BD_BKN uint16) into LDS.
 template <int F>
-__device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t* R, int64_t c,
-                                               uint4 (&sP)[F][BD_K * 4], int32_t (&sR)[F][BD_RP]) {
+__device__ __forceinline__ void bd_load_buckets(const uint16_t* BK, int64_t c,
+                                                uint16_t (&sB)[F][BD_BKN]) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(BK + c * F * BD_BKN);
+    uint32_t* l = reinterpret_cast<uint32_t*>(&sB[0][0]);
+    for (int i = threadIdx.x; i < F * BD_BKN / 2; i += blockDim.x) l[i] = g[i];
+}
+template <int F>
+__device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t* R, const uint16_t* BK,
+                                               int64_t c, uint4 (&sP)[F][BD_K * 4],
+                                               int32_t (&sR)[F][BD_RP], uint16_t (&sB)[F][BD_BKN]) {
+    bd_load_buckets<F>(BK, c, sB);
     // batches of 4 global loads in flight, then their LDS stores: the staging
     // stays in registers (a whole-table register array of up to 13 pieces was
     // placed in scratch memory by the compiler)
@@ -159,7 +182,8 @@ struct BdGlobalSets {
 // in C); piece i of w holds dwords 4j..4j+3 with j = (i + rot) & 3.
 template <int M, typename Sets>
 __device__ __forceinline__ void bd_row_words(const int4 su, int32_t lim, int32_t ps, const Sets& sets,
-                                             const int32_t (&sR)[M - 1][BD_RP], int rot,
+                                             const int32_t (&sR)[M - 1][BD_RP],
+                                             const uint16_t (&sB)[M - 1][BD_BKN], int sh, int rot,
                                              uint4 (&w)[4]) {
     constexpr int F = M - 1;
     if (lim < 0) {
@@ -169,7 +193,7 @@ __device__ __forceinline__ void bd_row_words(const int4 su, int32_t lim, int32_t
     }
     int k[F];
 #pragma unroll
-    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], icomp(su, f));
+    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], sB[f], sh, icomp(su, f));
 #ifdef DM_BD_CHECK
     for (int f = 0; f < F; ++f)
         if (!BD_OK(k[f], BD_K, "rows k")) k[f] = 0;
@@ -207,9 +231,10 @@ __device__ __forceinline__ void bd_row_words(const int4 su, int32_t lim, int32_t
 // The pieces of bd_row_words for a software pipeline (the table peel): the
 // searches, the set pieces (raw: loads in flight until used), and the merge.
 template <int F>
-__device__ __forceinline__ void bd_row_k(const int4 su, const int32_t (&sR)[F][BD_RP], int (&k)[F]) {
+__device__ __forceinline__ void bd_row_k(const int4 su, const int32_t (&sR)[F][BD_RP],
+                                         const uint16_t (&sB)[F][BD_BKN], int sh, int (&k)[F]) {
 #pragma unroll
-    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], icomp(su, f));
+    for (int f = 0; f < F; ++f) k[f] = bd_count_below<true>(sR[f], sB[f], sh, icomp(su, f));
 }
 template <int F, typename Sets>
 __device__ __forceinline__ void bd_row_fetch(const Sets& sets, const int (&k)[F], uint4 (&raw)[F][4]) {

@@ -829,17 +829,19 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
 // written.  Member rows, their ranks and tie spans
 // are loaded two 64-member steps ahead (a row's ranks wait on its row index).
 #ifndef DM_PEEL_TAB_MINW
-#define DM_PEEL_TAB_MINW 1  // min waves per SIMD the table peel is compiled for (A/B)
+#define DM_PEEL_TAB_MINW 4  // min waves per SIMD (4: two 512-thread workgroups per CU)
 #endif
 template <int F>
 __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_kernel(
     const int4* __restrict__ S, const int2* __restrict__ span, const uint32_t* __restrict__ P,
-    const int32_t* __restrict__ R, const int2* __restrict__ mrow, const int32_t* __restrict__ gsize,
+    const int32_t* __restrict__ R, const uint16_t* __restrict__ BK, const int2* __restrict__ mrow,
+    const int32_t* __restrict__ gsize,
     const int32_t* __restrict__ sigma, FrontState* st, int32_t* countq, unsigned long long* lastq,
     uint64_t* ckey, int32_t* cq, int32_t* rankU) {
     static_assert(PEEL_WAVES * 64 == BD_CW, "one thread per v of the chunk (sorted ranks, release)");
     constexpr int PW = BD_CW / 64;  // words of a chunk
     __shared__ int32_t sR[F][BD_RP];
+    __shared__ uint16_t sB[F][BD_BKN];
     __shared__ PeelLdsT<BD_CW> L;
     __shared__ PeelSmallT<BD_CW> Sm;
     __shared__ int32_t sF, sust, sstop, snf;
@@ -888,6 +890,8 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     int2 spA = span[mrA.x];
 #pragma unroll
     for (int f = 0; f < F; ++f) sR[f][bd_rpad(threadIdx.x)] = rr[f];
+    bd_load_buckets<F>(BK, c, sB);
+    const int sh = bd_bucket_shift(U);
     __syncthreads();
     const BdGlobalSets sets{reinterpret_cast<const uint4*>(P + c * F * BD_K * 16)};
     const TransposerX tr(lane);
@@ -898,35 +902,27 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         last[w] = -1;
     }
     const int64_t v0 = c * BD_CW;
-    // two-stage software pipeline over the wave's 64-member groups: the next
-    // group's searches run and its set loads are in flight while this
-    // group's bits are transposed.  A lane without a member (or whose row does
-    // not reach the chunk) searches nothing and reads P[0] = the empty set.
-    auto stage = [&](const int2 mr, const int4 su, const int2 sp, int64_t jj, int32_t& lim,
-                     int32_t& ps, uint4 (&raw)[F][4]) {
-        int k[F];
-        const bool h = jj + lane < Fm && c < mr.y;
-        lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)sp.y - v0, BD_CW));
-        ps = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mr.x - v0, BD_CW));
-        if (h && lim >= 0) {
-            bd_row_k<F>(su, sR, k);
-        } else {
-#pragma unroll
-            for (int f = 0; f < F; ++f) k[f] = 0;
-        }
-        bd_row_fetch<F>(sets, k, raw);
-        return h;
-    };
-    int32_t limA, psA;
-    uint4 rawA[F][4];
-    bool hasA = j0 < Fm ? stage(mrA, suA, spA, j0, limA, psA, rawA) : false;
+    // one 64-member group per step (a two-stage software pipeline over the
+    // groups measured no faster and needed 116-138 VGPRs); the next group's
+    // rows, ranks and spans are loaded a step ahead.  A lane without a member
+    // (or whose row does not reach the chunk) reads P[0] = the empty set.
     for (; j0 < Fm; j0 += STEP) {
         const int2 mrC = mload(j0 + 2 * STEP + lane);
         const int4 suB = S[mrB.x];
         const int2 spB = span[mrB.x];
-        if (__ballot(hasA) != 0) {
-            uint4 w[4];
-            bd_row_merge<F, false>(rawA, limA, psA, w);
+        const bool has = j0 + lane < Fm && c < mrA.y;
+        if (__ballot(has) != 0) {
+            const int32_t lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)spA.y - v0, BD_CW));
+            int k[F];
+            if (has && lim >= 0) {
+                bd_row_k<F>(suA, sR, sB, sh, k);
+            } else {
+#pragma unroll
+                for (int f = 0; f < F; ++f) k[f] = 0;
+            }
+            uint4 raw[F][4], w[4];
+            bd_row_fetch<F>(sets, k, raw);
+            bd_row_merge<F, false>(raw, lim, -1, w);
             uint32_t lo[8], hi[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -943,7 +939,9 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
                 if (top >= 0) last[w2] = (int32_t)(j0 + top);
             }
         }
-        if (j0 + STEP < Fm) hasA = stage(mrB, suB, spB, j0 + STEP, limA, psA, rawA);
+        mrA = mrB;
+        suA = suB;
+        spA = spB;
         mrB = mrC;
     }
     peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
@@ -1607,7 +1605,14 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     }
     // multi-launch peel (DM_PEEL_MULTI, or no cooperative grid): first status
     // check after as many fronts as the previous call needed
-    int batch = std::max(2, std::min(ctx->peel_hint + 1, 32));
+    // (the previous call's front count + 1, so that a selection like the last
+    // one needs a single status read; up to PEEL_BATCH_MAX launch pairs)
+    constexpr int PEEL_BATCH_MAX = 96;
+    // the hint counts only for a problem of about the same size
+    const bool hinted = 4 * U >= 3 * ctx->peel_hint_U && 3 * U <= 4 * ctx->peel_hint_U &&
+                        N == ctx->peel_hint_N;
+    const int hint = hinted ? ctx->peel_hint : 4;
+    int batch = std::max(2, std::min(hint + 1, PEEL_BATCH_MAX));
     for (; grid == 0;) {
         for (int b = 0; b < batch; ++b) {
             if (tab) {
@@ -1616,14 +1621,15 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 const int2* span = (const int2*)(tws + TL.span);
                 const uint32_t* P = (const uint32_t*)(tws + TL.P);
                 const int32_t* R = (const int32_t*)(tws + TL.R);
+                const uint16_t* BK = (const uint16_t*)(tws + TL.BK);
                 if (m == 2)
-                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
                 else if (m == 3)
-                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
                 else
-                    peel_tab_kernel<3><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, mrow, gsize, sigma,
+                    peel_tab_kernel<3><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
             } else {
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
@@ -1655,11 +1661,13 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
         // the previous call's front count, when it had more fronts than done
         // so far, is the better estimate (later fronts are larger than the
         // mean so far); launches past `done` return at once but cost ~10 us
-        if (ctx->peel_hint > hst->nfronts) need = std::min(need, ctx->peel_hint - hst->nfronts + 1);
-        batch = std::max(2, std::min(need + 2, 32));
+        if (hint > hst->nfronts) need = std::min(need, hint - hst->nfronts + 1);
+        batch = std::max(2, std::min(need + 2, PEEL_BATCH_MAX));
     }
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones
     ctx->peel_hint = hst->nfronts;
+    ctx->peel_hint_U = U;
+    ctx->peel_hint_N = N;
     ufront.resize(nf + 1);
     if (nf + 1 <= npre) {
         std::copy(hfs, hfs + nf + 1, ufront.begin());
