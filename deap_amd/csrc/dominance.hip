@@ -882,17 +882,15 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
     const int2* members = mrow + sust;  // (row in q order, 512-v halves it reaches)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int64_t STEP = PEEL_WAVES * 64;
-    auto mload = [&](int64_t j) { return j < Fm ? members[j] : make_int2(0, 0); };
-    int64_t j0 = j0s + (int64_t)wave * 64;
-    int2 mrA = mload(j0 + lane), mrB = mload(j0 + STEP + lane);
-    int4 suA = S[mrA.x];
-    int2 spA = span[mrA.x];
+    constexpr int STEP = PEEL_WAVES * 64;
+    constexpr int WIN = 2048;       // 4 members per thread (8 spilled, and so did
+                                    // loading the first window in the prologue)
+    constexpr int WR = WIN / STEP;  // members per thread per window
+    static_assert(WIN * sizeof(int2) <= sizeof(PeelLdsT<BD_CW>), "window list in the release's LDS");
 #pragma unroll
     for (int f = 0; f < F; ++f) sR[f][bd_rpad(threadIdx.x)] = rr[f];
     bd_load_buckets<F>(BK, c, sB);
     const int sh = bd_bucket_shift(U);
-    __syncthreads();
     const BdGlobalSets sets{reinterpret_cast<const uint4*>(P + c * F * BD_K * 16)};
     const TransposerX tr(lane);
     int32_t dec[PW], last[PW];
@@ -902,16 +900,53 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         last[w] = -1;
     }
     const int64_t v0 = c * BD_CW;
-    // one 64-member group per step (a two-stage software pipeline over the
-    // groups measured no faster and needed 116-138 VGPRs); the next group's
-    // rows, ranks and spans are loaded a step ahead.  A lane without a member
-    // (or whose row does not reach the chunk) reads P[0] = the empty set.
-    for (; j0 < Fm; j0 += STEP) {
-        const int2 mrC = mload(j0 + 2 * STEP + lane);
-        const int4 suB = S[mrB.x];
-        const int2 spB = span[mrB.x];
-        const bool has = j0 + lane < Fm && c < mrA.y;
-        if (__ballot(has) != 0) {
+    // The slice is taken in windows of WIN members.  A window's members whose
+    // row reaches chunk c are compacted, in front order, into LDS as (row,
+    // front position) -- the release's LDS, not yet in use -- and processed
+    // 64 at a time, so no group carries members that do not reach the chunk
+    // (a front's members reach chunks up to their objective-0 position: in
+    // front order about half of a group's lanes were idle on the high
+    // chunks).  Positions rise within a group, so the top set bit of a
+    // transposed word is its last dominator, read back by a lane shuffle.
+    int2* sM = reinterpret_cast<int2*>(&L);
+    for (int64_t wb = j0s; wb < Fm; wb += WIN) {
+        uint64_t bal[WR];
+        int2 mr[WR];
+        int nw = 0;
+#pragma unroll
+        for (int r = 0; r < WR; ++r) {
+            const int64_t j = wb + (int64_t)(wave * WR + r) * 64 + lane;
+            mr[r] = j < Fm ? members[j] : make_int2(0, 0);
+            bal[r] = __ballot(j < Fm && c < mr[r].y);
+            nw += __popcll(bal[r]);
+        }
+        if (lane == 0) Sm.wcnt[0][wave] = nw;
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < PEEL_WAVES; ++w) {
+            const int x = Sm.wcnt[0][w];
+            base += w < wave ? x : 0;
+            total += x;
+        }
+        const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+        for (int r = 0; r < WR; ++r) {
+            if ((bal[r] >> lane) & 1)
+                sM[base + __popcll(bal[r] & below)] =
+                    make_int2(mr[r].x, (int32_t)(wb - j0s + (int64_t)(wave * WR + r) * 64 + lane));
+            base += __popcll(bal[r]);
+        }
+        __syncthreads();
+        auto mget = [&](int g) { return g < total ? sM[g] : make_int2(0, -1); };
+        int2 mA = mget(wave * 64 + lane);
+        int4 suA = S[mA.x];
+        int2 spA = span[mA.x];
+        for (int g0 = wave * 64; g0 < total; g0 += STEP) {
+            const int2 mB = mget(g0 + STEP + lane);
+            const int4 suB = S[mB.x];
+            const int2 spB = span[mB.x];
+            const bool has = mA.y >= 0;
             const int32_t lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)spA.y - v0, BD_CW));
             int k[F];
             if (has && lim >= 0) {
@@ -931,18 +966,20 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
                 lo[2 * i + 1] = w[i].z;
                 hi[2 * i + 1] = w[i].w;
             }
-            tr.run<8>(lo, hi);  // lane v: bit i <-> member j0+i dominates v
+            tr.run<8>(lo, hi);  // lane v: bit i <-> group member i dominates v
+            const int32_t posA = (int32_t)(j0s + mA.y);
 #pragma unroll
             for (int w2 = 0; w2 < 8; ++w2) {
                 dec[w2] += __popc(lo[w2]) + __popc(hi[w2]);
-                const int32_t top = hi[w2] ? 63 - __clz(hi[w2]) : (lo[w2] ? 31 - __clz(lo[w2]) : -1);
-                if (top >= 0) last[w2] = (int32_t)(j0 + top);
+                const int32_t top = hi[w2] ? 63 - __clz(hi[w2]) : (lo[w2] ? 31 - __clz(lo[w2]) : 0);
+                const int32_t pt = __shfl(posA, top);
+                if (lo[w2] | hi[w2]) last[w2] = pt;
             }
+            mA = mB;
+            suA = suB;
+            spA = spB;
         }
-        mrA = mrB;
-        suA = suB;
-        spA = spB;
-        mrB = mrC;
+        __syncthreads();  // the window's list is read out before the next (or the release) reuses it
     }
     peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
                             snf, nsl, L, Sm, &pre);
