@@ -537,9 +537,16 @@ constexpr int PEEL_SLICES = DM_PEEL_SLICES;
 #define DM_PEEL_SLICE_MIN 1024
 #endif
 constexpr int64_t PEEL_SLICE_MIN = DM_PEEL_SLICE_MIN;
-__device__ __forceinline__ int64_t peel_slices(int64_t F, int64_t s, int64_t NS, int64_t K) {
+// the table peel's slices hold at least 2,048 members: its workgroups repeat
+// the chunk's table loads and release per slice, and C5 measured 3.58 ms/gen
+// with 2,048-8,192 against 3.69 with 1,024 (profiles/r03y)
+#ifndef DM_PEEL_TAB_SLICE_MIN
+#define DM_PEEL_TAB_SLICE_MIN 2048
+#endif
+__device__ __forceinline__ int64_t peel_slices(int64_t F, int64_t s, int64_t NS, int64_t K,
+                                               int64_t smin = PEEL_SLICE_MIN) {
     const int64_t byload = (K * (NS - s) + NS - 1) / NS;
-    return std::max<int64_t>(1, std::min<int64_t>(byload, F / PEEL_SLICE_MIN));
+    return std::max<int64_t>(1, std::min<int64_t>(byload, F / smin));
 }
 // Data one phase of the persistent peel hands to another crosses workgroups
 // on different XCDs, whose L2s are not coherent with each other: those
@@ -831,6 +838,15 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
 #ifndef DM_PEEL_TAB_MINW
 #define DM_PEEL_TAB_MINW 4  // min waves per SIMD (4: two 512-thread workgroups per CU)
 #endif
+#ifdef DM_PEEL_PROF
+// phase clocks of each table-peel workgroup (diagnostic builds only):
+// {chunk, slice, F, t_start, t_tables, t_members, t_release, 0}
+__device__ unsigned long long g_pprof[1 << 20];
+__device__ unsigned int g_pprof_n;
+#define PPROF_T(x) const unsigned long long x = wall_clock64()
+#else
+#define PPROF_T(x)
+#endif
 template <int F>
 __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_kernel(
     const int4* __restrict__ S, const int2* __restrict__ span, const uint32_t* __restrict__ P,
@@ -849,6 +865,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     // grid x = NG rounded up to a multiple of 8: the slices y of chunk c (linear
     // workgroup ids c + y gridDim.x) land on one XCD, whose L2 then serves
     // the chunk's table slice to all of them
+    PPROF_T(pt0);
     const int64_t c = blockIdx.x;
     const int64_t NG = (st->U + BD_CW - 1) / BD_CW;
     if (c >= NG) return;
@@ -867,7 +884,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     }
     __syncthreads();
     if (sstop) return;
-    const int64_t nsl = peel_slices(sF, c, NG, gridDim.y);
+    const int64_t nsl = peel_slices(sF, c, NG, gridDim.y, DM_PEEL_TAB_SLICE_MIN);
     if ((int64_t)blockIdx.y >= nsl) return;
     const int64_t U = sU;
     PeelPre<1> pre;
@@ -909,6 +926,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     // chunks).  Positions rise within a group, so the top set bit of a
     // transposed word is its last dominator, read back by a lane shuffle.
     int2* sM = reinterpret_cast<int2*>(&L);
+    PPROF_T(pt1);
     for (int64_t wb = j0s; wb < Fm; wb += WIN) {
         uint64_t bal[WR];
         int2 mr[WR];
@@ -981,8 +999,19 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         }
         __syncthreads();  // the window's list is read out before the next (or the release) reuses it
     }
+    PPROF_T(pt2);
     peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
                             snf, nsl, L, Sm, &pre);
+#ifdef DM_PEEL_PROF
+    PPROF_T(pt3);
+    if (threadIdx.x == 0) {
+        const unsigned int e = atomicAdd(&g_pprof_n, 1u);
+        if (e < (1u << 17)) {
+            unsigned long long* o = g_pprof + (size_t)e * 8;
+            o[0] = c; o[1] = blockIdx.y; o[2] = sF; o[3] = pt0; o[4] = pt1; o[5] = pt2; o[6] = pt3; o[7] = 0;
+        }
+    }
+#endif
 }
 
 constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
@@ -1718,3 +1747,18 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
 }
 
 }  // namespace dm
+
+#ifdef DM_PEEL_PROF
+// diagnostic builds: copy out and reset the table-peel phase clocks
+extern "C" int dm_debug_peel_prof(unsigned long long* host, int64_t cap) {
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(dm::g_pprof_n), 4) != hipSuccess) return -1;
+    n = std::min<unsigned int>(n, 1u << 17);
+    const int64_t k = std::min<int64_t>(n, cap);
+    if (k > 0 && hipMemcpyFromSymbol(host, HIP_SYMBOL(dm::g_pprof), (size_t)k * 64) != hipSuccess) return -1;
+    const unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(dm::g_pprof_n), &z, 4) != hipSuccess) return -1;
+    return (int)k;
+}
+#endif
