@@ -81,24 +81,88 @@ __global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, in
         if (start) isrep[perm[j]] = 1;
     }
 }
-// After a sort by objective 0 only: flag when two neighbours with equal
-// objective-0 keys are out of lexicographic order in the other objectives
-// (then the full lexicographic sort is needed; ties keep index order).
-__global__ void lex_tie_kernel(const double* wv, int m, const int32_t* perm, int64_t n,
-                               int32_t* flag) {
+// After a stable sort by objective 0 alone (keys0: the sorted objective-0
+// keys): the runs of equal objective 0 that are out of lexicographic order in
+// the other objectives are sorted in place, which gives the order of the full
+// lexicographic sort.  lex_bad_kernel flags the start of every run holding an
+// adjacent pair out of order (a run starts in index order, and identical rows
+// -- clones -- are in order); lex_run_sort_kernel sorts each flagged run with
+// one wave (a bitonic sort over the lanes of (objectives 1.., index)).  A
+// flagged run longer than LEX_RUN_CAP = 64 sets *overflow: the caller then
+// sorts in full.
+constexpr int LEX_RUN_CAP = 64;
+__device__ __forceinline__ bool lex_less_rest(const double* wv, int m, int32_t x, int32_t y) {
+    const double* a = wv + (int64_t)x * m;
+    const double* b = wv + (int64_t)y * m;
+    for (int o = 1; o < m; ++o) {
+        const uint64_t ka = ordered_key(a[o]), kb = ordered_key(b[o]);
+        if (ka != kb) return ka < kb;
+    }
+    return x < y;
+}
+__global__ void lex_bad_kernel(const double* wv, int m, const uint64_t* keys0, const int32_t* perm,
+                               int64_t n, int32_t* runflag, int32_t* overflow) {
     GRID_LOOP(j, n) {
-        if (j == 0) continue;
-        const double* a = wv + (int64_t)perm[j] * m;
-        const double* b = wv + (int64_t)perm[j - 1] * m;
-        if (ordered_key(a[0]) != ordered_key(b[0])) continue;
-        for (int o = 1; o < m; ++o) {
-            const uint64_t ka = ordered_key(a[o]), kb = ordered_key(b[o]);
-            if (ka > kb) break;
-            if (ka < kb) {
-                *flag = 1;
-                break;
+        if (j == 0 || keys0[j] != keys0[j - 1]) continue;
+        if (lex_less_rest(wv, m, perm[j - 1], perm[j])) continue;
+        int64_t st = j - 1;
+        while (st > 0 && keys0[st - 1] == keys0[j] && j - st < LEX_RUN_CAP) --st;
+        if (st > 0 && keys0[st - 1] == keys0[j]) {
+            *overflow = 1;
+            continue;
+        }
+        runflag[st] = 1;
+    }
+}
+struct LexRest {
+    uint64_t k[3];
+    int32_t x;
+};
+__device__ __forceinline__ bool lex_rest_less(const LexRest& a, const LexRest& b) {
+    for (int o = 0; o < 3; ++o)
+        if (a.k[o] != b.k[o]) return a.k[o] < b.k[o];
+    return a.x < b.x;
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64l(uint64_t v, int mask) {
+    const int lo = __shfl_xor((int)(uint32_t)v, mask, 64);
+    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), mask, 64);
+    return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+__global__ __launch_bounds__(256) void lex_run_sort_kernel(const double* wv, int m,
+                                                           const uint64_t* keys0, int32_t* perm,
+                                                           int64_t n, const int32_t* runflag,
+                                                           int32_t* overflow) {
+    const int lane = threadIdx.x & 63;
+    const int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64;
+    if (base >= n) return;
+    uint64_t todo = __ballot(base + lane < n && runflag[base + lane] != 0);
+    while (todo) {  // wave-uniform
+        const int64_t st = base + __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const uint64_t k0 = keys0[st];
+        if (st + LEX_RUN_CAP < n && keys0[st + LEX_RUN_CAP] == k0) {
+            if (lane == 0) *overflow = 1;
+            continue;
+        }
+        const int64_t i = st + lane;
+        const bool in = i < n && keys0[i] == k0;
+        LexRest r;
+        r.x = in ? perm[i] : INT32_MAX;
+        for (int o = 0; o < 3; ++o)
+            r.k[o] = in && o + 1 < m ? ordered_key(wv[(int64_t)r.x * m + o + 1]) : (in ? 0ull : ~0ull);
+        for (int size = 2; size <= 64; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                LexRest p;
+                for (int o = 0; o < 3; ++o) p.k[o] = shfl_xor_u64l(r.k[o], stride);
+                p.x = __shfl_xor(r.x, stride, 64);
+                const bool lower = (lane & stride) == 0;
+                const bool up = (lane & size) == 0;
+                const bool pl = lex_rest_less(p, r);
+                // lower lane of an ascending pair keeps the minimum
+                if ((lower == up) ? pl : !pl && (p.x != r.x)) r = p;
             }
         }
+        if (in) perm[i] = r.x;
     }
 }
 __global__ void nan_any_kernel(const double* wv, int64_t cnt, int32_t* flag) {
@@ -493,18 +557,27 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     int32_t* nanflag = small + 2;
     int32_t* ftotal = small + 4;
     int64_t* dtotal = (int64_t*)(small + 8);
-    // lexicographic ascending sort of wvalues (ties by index: stable).  First
-    // by objective 0 alone (8 radix passes instead of 8m): when no two rows
-    // with equal objective 0 are out of order in the others (lex_tie_kernel,
-    // read with U below), that IS the lexicographic order; otherwise the
-    // full sort and the grouping are redone.
+    // lexicographic ascending sort of wvalues (ties by index: stable): by
+    // objective 0 alone (8 radix passes instead of 8m), then the runs of equal
+    // objective 0 that are out of order in the others are sorted in place
+    // (lex_bad_kernel, lex_run_sort_kernel); only when such a run is longer than LEX_RUN_CAP (flag
+    // read with U below) are the full sort and the grouping redone.  (C5's
+    // populations hold near-clones equal in objective 0 and a few ulps apart
+    // in the others: the full redo cost 24 radix passes per selection.)
     int32_t* tieflag = small + 6;
     static const bool full_lex = std::getenv("DM_LEX_FULL") != nullptr;
     const bool quick = m > 1 && !full_lex;
     int rc;
+    DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
     auto group = [&](int nlex) -> int {
         int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex);
         if (r) return r;
+        if (nlex < m) {
+            zero_i32_kernel<<<g1(n), 256, 0, s>>>(vtmp, n);
+            lex_bad_kernel<<<g1(n), 256, 0, s>>>(wv, m, keys, perm, n, vtmp, tieflag);
+            lex_run_sort_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, s>>>(wv, m, keys, perm,
+                                                                             n, vtmp, tieflag);
+        }
         zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
         seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
         if ((r = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return r;
@@ -512,9 +585,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     };
     if ((rc = group(quick ? 1 : m))) return rc;
     DM_HIP(hipMemsetAsync(nanflag, 0, 4, s));
-    DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
     nan_any_kernel<<<g1(n * m), 256, 0, s>>>(wv, n * m, nanflag);
-    if (quick) lex_tie_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, tieflag);
     DM_HIP(hipMemcpyAsync(hostv, utotal, 28, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
     if (quick && hostv[6]) {

@@ -360,6 +360,52 @@ def test_sort_nondominated_large_random(gpu):
         assert chosen == want_c
 
 
+def _near_clone_fitness(rng, m, nbase, long_mixed):
+    """Rows in runs of equal objective 0: exact clones, and near-clones a few
+    ulps apart in the other objectives (what cxBlend of two clones leaves in
+    C5's populations), in shuffled order; a run of 100 exact clones; with
+    long_mixed a run of 90 rows equal in objective 0 and all different in the
+    others (longer than the 64-row in-place run sort: the full sort)."""
+    base = rng.uniform(0, 1, size=(nbase, m))
+    rows = []
+    for b in base:
+        for _ in range(int(rng.integers(1, 9))):
+            r = b.copy()
+            if rng.random() < 0.6:
+                for o in range(1, m):
+                    for _ in range(int(rng.integers(0, 3))):
+                        r[o] = np.nextafter(r[o], 2.0 if rng.random() < 0.5 else -1.0)
+            rows.append(r)
+    rows += [base[0]] * 100
+    if long_mixed:
+        rows += [np.concatenate([[0.25], rng.uniform(0, 1, m - 1)]) for _ in range(90)]
+    wv = np.array(rows)
+    return wv[rng.permutation(len(wv))]
+
+
+@pytest.mark.parametrize("m", [2, 3, 4])
+@pytest.mark.parametrize("long_mixed", [False, True])
+def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed):
+    """The grouping sorts by objective 0 and then sorts, in place, only the
+    runs of equal objective 0 that are out of order in the other objectives
+    (nsga2.hip lex_bad_kernel / lex_run_sort_kernel), falling back to the full
+    lexicographic sort for such a run over 64 rows: fronts and selNSGA2 equal
+    the oracle (deap/tools/emo.py:15-50, 53-117) exactly on near-clone
+    populations."""
+    from deap_amd import tools
+    rng = np.random.default_rng(70 + 10 * m + long_mixed)
+    wv = _near_clone_fitness(rng, m, 500, long_mixed)
+    n = len(wv)
+    w = (-1.0,) * m
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
+                           valid=np.ones(n))
+    fronts = tools.sortNondominated(pop, n)
+    assert [f.cpu().numpy().tolist() for f in fronts] == ops.sort_nondominated(wv, n)
+    chosen = tools.selNSGA2(pop, n // 2).cpu().numpy().tolist()
+    want_c, _ = ops.sel_nsga2(wv, w, n // 2)
+    assert chosen == want_c
+
+
 @pytest.mark.parametrize("m", [2, 3, 4])
 def test_sort_nondominated_with_nan_fitness(gpu, m):
     """NaN objectives (e.g. ZDT1 of an out-of-range gene): Fitness.dominates
