@@ -57,19 +57,26 @@ __global__ void lex_sigma_kernel(const int32_t* perm, const int32_t* uidx, const
         }
     }
 }
-__global__ void rank_key_kernel(const double* ufit, int m, int o, int64_t U, uint64_t* keys,
+// Dense ranks of objectives 1..m-1 over the U unique fitnesses, batched:
+// element j of segment g = j / U holds objective g + 1 of unique row j % U.
+__global__ void rank_key_kernel(const double* ufit, int m, int64_t U, int64_t nb, uint64_t* keys,
                                 int32_t* vals) {
-    DGRID_LOOP(u, U) {
-        keys[u] = ordered_key(ufit[u * m + o]);
-        vals[u] = (int32_t)u;
+    DGRID_LOOP(j, nb) {
+        const int64_t g = j / U, u = j - g * U;
+        keys[j] = ordered_key(ufit[u * m + g + 1]);
+        vals[j] = (int32_t)u;
     }
 }
-__global__ void rank_flag_kernel(const uint64_t* keys, int64_t U, int32_t* flag) {
-    DGRID_LOOP(j, U) flag[j] = (j > 0 && keys[j] != keys[j - 1]) ? 1 : 0;
+__global__ void rank_flag_kernel(const uint64_t* keys, int64_t U, int64_t nb, int32_t* flag) {
+    DGRID_LOOP(j, nb) flag[j] = (j % U != 0 && keys[j] != keys[j - 1]) ? 1 : 0;
 }
+// rank within the segment: the prefix count of new values since its start
 __global__ void rank_scatter_kernel(const int32_t* vals, const int32_t* excl, const int32_t* flag,
-                                    const int32_t* pos, int64_t U, int c, int32_t* S) {
-    DGRID_LOOP(j, U) S[(int64_t)pos[vals[j]] * 4 + c] = excl[j] + flag[j];
+                                    const int32_t* pos, int64_t U, int64_t nb, int32_t* S) {
+    DGRID_LOOP(j, nb) {
+        const int64_t g = j / U;
+        S[(int64_t)pos[vals[j]] * 4 + g] = excl[j] + flag[j] - excl[g * U];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1432,9 +1439,14 @@ struct FastLayout {
     int64_t NB, NG, NQ, ngroups, Upad;  // NG: 512-v segments (tri_dom), NQ: TW-word lines (peel)
     size_t part, S, sigma, pos, nseg, toff, counter, mrow, countq, cq, work, total;
 };
-static size_t ranks_work_bytes(int64_t n) {
-    return 2 * align_up((size_t)n * 8, 256) + 3 * align_up((size_t)n * 4, 256) +
-           radix_sort_temp_bytes(n) + scan_temp_bytes(n);
+// elements of the rank pass's key / value buffers: the population (objective
+// 0's q order) or the M-1 <= 3 objectives' unique values sorted as one batch
+static int64_t ranks_elems(int64_t n, int64_t U) { return std::max<int64_t>(n, 3 * U); }
+static size_t ranks_work_bytes(int64_t n, int64_t U) {
+    const int64_t e = ranks_elems(n, U);
+    return 2 * align_up((size_t)e * 8, 256) + 3 * align_up((size_t)e * 4, 256) +
+           std::max(radix_sort_temp_bytes(n), radix_sort_batched_temp_bytes(3, U)) +
+           scan_temp_bytes(e);
 }
 static size_t fronts_work_bytes(int64_t U) {
     return align_up(sizeof(FrontState), 256) + 3 * align_up((size_t)U * 8, 256) +
@@ -1464,7 +1476,7 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
     L.mrow = take((size_t)U * 8);
     L.countq = take((size_t)U * 4);
     L.cq = take((size_t)U * 4);
-    L.work = take(std::max(ranks_work_bytes(n), fronts_work_bytes(U)));
+    L.work = take(std::max(ranks_work_bytes(n, U), fronts_work_bytes(U)));
     L.total = off;
     return L;
 }
@@ -1507,14 +1519,15 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
     int32_t* counter = (int32_t*)(ws + L.counter);
     int16_t* part = (int16_t*)(ws + L.part);
     char* w = ws + L.work;
+    const int64_t e = ranks_elems(n, U);
     uint64_t* keys = (uint64_t*)w;
-    uint64_t* ktmp = (uint64_t*)(w + align_up((size_t)n * 8, 256));
-    char* p = w + 2 * align_up((size_t)n * 8, 256);
+    uint64_t* ktmp = (uint64_t*)(w + align_up((size_t)e * 8, 256));
+    char* p = w + 2 * align_up((size_t)e * 8, 256);
     int32_t* vals = (int32_t*)p;
-    int32_t* vtmp = (int32_t*)(p + align_up((size_t)n * 4, 256));
-    int32_t* flag = (int32_t*)(p + 2 * align_up((size_t)n * 4, 256));
-    void* rtemp = p + 3 * align_up((size_t)n * 4, 256);
-    void* stemp = (char*)rtemp + radix_sort_temp_bytes(n);
+    int32_t* vtmp = (int32_t*)(p + align_up((size_t)e * 4, 256));
+    int32_t* flag = (int32_t*)(p + 2 * align_up((size_t)e * 4, 256));
+    void* rtemp = p + 3 * align_up((size_t)e * 4, 256);
+    void* stemp = (char*)rtemp + std::max(radix_sort_temp_bytes(n), radix_sort_batched_temp_bytes(3, U));
     DM_HIP(hipMemsetAsync(S, 0, (size_t)L.Upad * 16, s));
     // objective 0 and the q order from the lexicographic order
     lex_flags_kernel<<<dg1(n), 256, 0, s>>>(wv, m, perm, segin, n, vals, vtmp);
@@ -1523,14 +1536,17 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
     if ((rc = exclusive_scan_i32(s, vtmp, (int32_t*)keys, n, nullptr, stemp))) return rc;
     lex_sigma_kernel<<<dg1(n), 256, 0, s>>>(perm, uidx, vals, flag, vtmp, (int32_t*)keys, n, m,
                                             sigma, pos, (int32_t*)S);
-    // objectives 1..m-1: dense ranks by a sort of the unique values
-    for (int o = 1; o < m; ++o) {
-        rank_key_kernel<<<dg1(U), 256, 0, s>>>(ufit, m, o, U, keys, vals);
-        if ((rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, U, 0, 64, rtemp))) return rc;
-        rank_flag_kernel<<<dg1(U), 256, 0, s>>>(keys, U, flag);
+    // objectives 1..m-1: dense ranks by ONE batched sort of the unique values
+    // (segment o - 1 = objective o), one flag pass, one scan, one scatter
+    if (m > 1) {
+        const int64_t nb = (int64_t)(m - 1) * U;
+        rank_key_kernel<<<dg1(nb), 256, 0, s>>>(ufit, m, U, nb, keys, vals);
+        if ((rc = radix_sort_pairs_batched(s, keys, vals, ktmp, vtmp, m - 1, U, 0, 64, rtemp)))
+            return rc;
+        rank_flag_kernel<<<dg1(nb), 256, 0, s>>>(keys, U, nb, flag);
         // the scan may not alias its input: the exclusive prefix goes to vtmp
-        if ((rc = exclusive_scan_i32(s, flag, vtmp, U, nullptr, stemp))) return rc;
-        rank_scatter_kernel<<<dg1(U), 256, 0, s>>>(vals, vtmp, flag, pos, U, o - 1, (int32_t*)S);
+        if ((rc = exclusive_scan_i32(s, flag, vtmp, nb, nullptr, stemp))) return rc;
+        rank_scatter_kernel<<<dg1(nb), 256, 0, s>>>(vals, vtmp, flag, pos, U, nb, (int32_t*)S);
     }
     tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
     if (fast_bitset(m))  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)

@@ -22,16 +22,20 @@ constexpr int RS_HIST_BLOCKS = 512;
 constexpr size_t RS_GHIST_BYTES = (RS_MAX_PASSES * RS_BINS * 4 + 255) / 256 * 256;
 constexpr size_t RS_TICKET_BYTES = 256;
 
-size_t radix_sort_temp_bytes(int64_t n) {
-    const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
-    return RS_GHIST_BYTES + RS_TICKET_BYTES +
+size_t radix_sort_batched_temp_bytes(int64_t nseg, int64_t seglen) {
+    const int64_t tiles = nseg * ((seglen + RS_TILE - 1) / RS_TILE);
+    return (size_t)nseg * RS_GHIST_BYTES + RS_TICKET_BYTES +
            align_up((size_t)tiles * RS_MAX_PASSES * RS_BINS * 4, 256);
 }
+size_t radix_sort_temp_bytes(int64_t n) { return radix_sort_batched_temp_bytes(1, n); }
 
-// ghist[p][d] += count of digit d of pass p (shift begin + 8p)
+// ghist[p][d] += count of digit d of pass p (shift begin + 8p); segment
+// blockIdx.y of the batch: keys + y seglen, histograms + y RS_GHIST_BYTES
 __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* __restrict__ keys,
                                                              int64_t n, int begin, int passes,
                                                              int32_t* __restrict__ ghist) {
+    keys += (int64_t)blockIdx.y * n;
+    ghist += (int64_t)blockIdx.y * (RS_GHIST_BYTES / 4);
     __shared__ int32_t h[RS_MAX_PASSES][RS_BINS];
     for (int p = 0; p < passes; ++p) h[p][threadIdx.x] = 0;
     __syncthreads();
@@ -51,10 +55,13 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* __r
 // prefix) in bits 30-31, the count below
 constexpr uint32_t RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_COUNT = (1u << 30) - 1;
 
+// A batch of independent segments of `seglen` keys (tps tiles each) sorts in
+// the same launches: a tile's digit offsets, look-back and output stay
+// inside its segment.  One segment: seglen = n.
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
-    uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n, int shift,
-    const int32_t* __restrict__ ghist, uint32_t* status, uint32_t* ticket) {
+    uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t seglen, int64_t tps,
+    int shift, const int32_t* __restrict__ ghist, uint32_t* status, uint32_t* ticket) {
     __shared__ int32_t cnt[RS_ROUNDS][RS_THREADS / 64][RS_BINS];
     __shared__ int32_t gofs[RS_BINS];
     __shared__ uint32_t tile_id;
@@ -65,13 +72,16 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     if (tid == 0) tile_id = atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = tile_id;
-    const int64_t base = tile * RS_TILE;
+    const int64_t seg = tile / tps, lt = tile - seg * tps;  // segment, tile within it
+    const int64_t sbase = seg * seglen;
+    const int64_t base = sbase + lt * RS_TILE;
+    const int64_t n = sbase + seglen;  // end of the segment
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r)
 #pragma unroll
         for (int w = 0; w < RS_THREADS / 64; ++w) cnt[r][w][tid] = 0;
     // exclusive scan of the global digit histogram (thread d -> digit d)
-    gofs[tid] = ghist[tid];
+    gofs[tid] = ghist[seg * (RS_GHIST_BYTES / 4) + tid];
     __syncthreads();
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t k[RS_ROUNDS];
@@ -123,11 +133,11 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     // decoupled look-back over the earlier tiles for digit tid
     uint32_t* my = status + tile * RS_BINS + tid;
     int32_t excl = 0;
-    if (tile == 0) {
+    if (lt == 0) {
         __hip_atomic_store(my, RS_PREFIX | (uint32_t)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         __hip_atomic_store(my, RS_AGG | (uint32_t)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int64_t t = tile - 1; t >= 0;) {
+        for (int64_t t = tile - 1; t >= seg * tps;) {
             const uint32_t st = __hip_atomic_load(status + t * RS_BINS + tid, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
             if (st == 0) {
@@ -146,33 +156,40 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
         if (d[r] >= 0) {
-            const int32_t pos = gofs[d[r]] + cnt[r][wave][d[r]] + rk[r];
+            const int64_t pos = sbase + gofs[d[r]] + cnt[r][wave][d[r]] + rk[r];
             keys_out[pos] = k[r];
             vals_out[pos] = v[r];
         }
     }
 }
 
-int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
-                     int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp) {
-    if (n <= 1 || end_bit <= begin_bit) return DM_OK;
+int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                             int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
+                             int end_bit, void* temp) {
+    if (nseg <= 0 || seglen <= 1 || end_bit <= begin_bit) return DM_OK;
+    const int64_t n = nseg * seglen;
     DM_CHECK_ARG(n < (1ll << 30), "radix sort of more than 2^30 keys");
-    const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    DM_CHECK_ARG(nseg <= 65535, "radix sort of more than 65,535 segments");
+    const int64_t tps = (seglen + RS_TILE - 1) / RS_TILE;
+    const int64_t tiles = nseg * tps;
     const int passes = std::min(RS_MAX_PASSES, (end_bit - begin_bit + 7) / 8);
     int32_t* ghist = (int32_t*)temp;
-    uint32_t* ticket = (uint32_t*)((char*)temp + RS_GHIST_BYTES);
-    uint32_t* status = (uint32_t*)((char*)temp + RS_GHIST_BYTES + RS_TICKET_BYTES);
+    uint32_t* ticket = (uint32_t*)((char*)temp + nseg * RS_GHIST_BYTES);
+    uint32_t* status = (uint32_t*)((char*)temp + nseg * RS_GHIST_BYTES + RS_TICKET_BYTES);
     DM_HIP(hipMemsetAsync(temp, 0,
-                          RS_GHIST_BYTES + RS_TICKET_BYTES + (size_t)passes * tiles * RS_BINS * 4,
+                          nseg * RS_GHIST_BYTES + RS_TICKET_BYTES +
+                              (size_t)passes * tiles * RS_BINS * 4,
                           s));
-    const unsigned hb = (unsigned)std::min<int64_t>(RS_HIST_BLOCKS, (n + RS_THREADS * 8 - 1) / (RS_THREADS * 8));
-    rs_hist_kernel<<<hb, RS_THREADS, 0, s>>>(keys, n, begin_bit, passes, ghist);
+    const unsigned hb = (unsigned)std::min<int64_t>(
+        RS_HIST_BLOCKS, (seglen + RS_THREADS * 8 - 1) / (RS_THREADS * 8));
+    rs_hist_kernel<<<dim3(hb, (unsigned)nseg), RS_THREADS, 0, s>>>(keys, seglen, begin_bit, passes,
+                                                                   ghist);
     uint64_t* kin = keys;
     int32_t* vin = vals;
     uint64_t* kout = keys_tmp;
     int32_t* vout = vals_tmp;
     for (int p = 0; p < passes; ++p) {
-        rs_pass_kernel<<<(unsigned)tiles, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n,
+        rs_pass_kernel<<<(unsigned)tiles, RS_THREADS, 0, s>>>(kin, vin, kout, vout, seglen, tps,
                                                              begin_bit + 8 * p, ghist + p * RS_BINS,
                                                              status + (size_t)p * tiles * RS_BINS,
                                                              ticket + p);
@@ -185,6 +202,12 @@ int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* key
     }
     DM_LAUNCH_CHECK();
     return DM_OK;
+}
+
+int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                     int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp) {
+    return radix_sort_pairs_batched(s, keys, vals, keys_tmp, vals_tmp, 1, n, begin_bit, end_bit,
+                                    temp);
 }
 
 // ---------------------------------------------------------------------------

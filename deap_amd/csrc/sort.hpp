@@ -24,6 +24,13 @@ size_t radix_sort_temp_bytes(int64_t n);
 // `temp` must hold radix_sort_temp_bytes(n) bytes.
 int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                      int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp);
+// nseg independent segments of seglen keys each (segment g at [g seglen,
+// (g + 1) seglen)), sorted in the same launches; `temp` must hold
+// radix_sort_batched_temp_bytes(nseg, seglen) bytes.
+size_t radix_sort_batched_temp_bytes(int64_t nseg, int64_t seglen);
+int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                             int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
+                             int end_bit, void* temp);
 
 size_t scan_temp_bytes(int64_t n);
 // out[i] = sum_{j<i} in[j] (exclusive); *total (device, may be null) = sum.
