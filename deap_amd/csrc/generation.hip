@@ -176,10 +176,18 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 if (!kb) return DM_ERR_NOMEM;
                 a.pkeys = kb;
             }
+            static const bool split = std::getenv("DM_BITS_SPLIT") != nullptr;
+            void* bplans = nullptr;
+            if (split && !(bplans = scratch_slot(ctx, 1, gen_bits_split_bytes(a))))
+                return DM_ERR_NOMEM;
             timing_begin(ctx);
             if (keys) launch_fit_keys(a, (int16_t*)a.pkeys, ctx->stream);
-            launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
-                                  ctx->stream);
+            if (split)
+                launch_gen_bits_split(a, ec != EC_NONE, bplans,
+                                      count ? ctx->evals_spread : nullptr, ctx->stream);
+            else
+                launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
+                                      ctx->stream);
             timing_end(ctx);
             DM_LAUNCH_CHECK();
             return DM_OK;

@@ -538,6 +538,11 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 // Decisions of every pair (thread per pair), generation_pipe_f64.hip.
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
+// plan + stream form of the fused kernel (same children): plans of
+// gen_bits_split_bytes(a) bytes
+size_t gen_bits_split_bytes(const GenArgs& a);
+void launch_gen_bits_split(const GenArgs& a, bool eval, void* plans, long long* spread,
+                           hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
