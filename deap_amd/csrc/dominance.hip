@@ -1131,6 +1131,34 @@ struct OrderScalars {
 // candidates: overflow, the host's radix sort orders them (presorted: ckey
 // already ordered).
 constexpr int ORDER_BIN_MAX = 64;
+// Exclusive prefix sum over the workgroup's threads: lane shuffles within
+// each wave, one wave scans the wave totals (two barriers; a Hillis-Steele
+// scan over 1,024 LDS slots took 20).  sh: NT / 64 ints of LDS.
+template <int NT>
+__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* sh) {
+    static_assert(NT % 64 == 0 && NT / 64 <= 64, "whole waves, at most 64");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        int32_t w = lane < NT / 64 ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < NT / 64; o <<= 1) {
+            const int32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < NT / 64) sh[lane] = w;
+    }
+    __syncthreads();
+    return x - v + (wave ? sh[wave - 1] : 0);
+}
+
 template <int NT, int CAP, bool COH>
 __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t* cq,
                             int32_t* ulist, int2* mrow, const int32_t* pos, const int32_t* nseg,
@@ -1192,16 +1220,8 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
             sum += c;
             mx = max(mx, c);
         }
-        part[tid] = sum;
         if (mx > ORDER_BIN_MAX) atomicMax(&sc.smax, mx);
-        __syncthreads();
-        for (int o = 1; o < NT; o <<= 1) {
-            const int32_t yv = tid >= o ? part[tid - o] : 0;
-            __syncthreads();
-            part[tid] += yv;
-            __syncthreads();
-        }
-        int32_t run = part[tid] - sum;
+        int32_t run = block_excl_scan<NT>(sum, part);
         for (int b = b0; b < b1; ++b) {
             const int32_t c = lds.cs.base[b];
             lds.cs.base[b] = run;

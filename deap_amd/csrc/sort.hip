@@ -107,19 +107,12 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
         rk[r] = __popcll(same & below);
         if (ok && rk[r] == 0) cnt[r][wave][d[r]] = __popcll(same);
     }
-    int32_t gex = 0;  // global exclusive offset of digit tid
-    {
-        int32_t x = gofs[tid];
-        __syncthreads();
-        // Hillis-Steele inclusive scan over the 256 digits
-        for (int o = 1; o < RS_BINS; o <<= 1) {
-            const int32_t y = tid >= o ? gofs[tid - o] : 0;
-            __syncthreads();
-            gofs[tid] += y;
-            __syncthreads();
-        }
-        gex = gofs[tid] - x;
-    }
+    static_assert(RS_BINS == RS_THREADS, "thread d owns digit d");
+    __shared__ int32_t wsum[RS_THREADS / 64];
+    // global exclusive offset of digit tid (the scan's barriers also order
+    // the per-(round, wave) counts above before the offsets below)
+    const int32_t gx = gofs[tid];
+    const int32_t gex = block_incl_scan<RS_THREADS, false>(gx, wsum) - gx;
     // tile-local exclusive offsets per (round, wave) in key order; tile total
     int32_t run = 0;
 #pragma unroll
@@ -247,15 +240,10 @@ __global__ __launch_bounds__(SC_THREADS) void scan_tile_kernel(const int32_t* in
         v[j] = i < n ? in[i] : ident;
         acc = op2<MAX>(acc, v[j]);
     }
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (int o = 1; o < SC_THREADS; o <<= 1) {
-        const int32_t x = threadIdx.x >= o ? sh[threadIdx.x - o] : ident;
-        __syncthreads();
-        sh[threadIdx.x] = op2<MAX>(sh[threadIdx.x], x);
-        __syncthreads();
-    }
-    int32_t run = threadIdx.x > 0 ? sh[threadIdx.x - 1] : ident;
+    const int32_t incl = block_incl_scan<SC_THREADS, MAX>(acc, sh);
+    // exclusive: the previous thread's inclusive value
+    int32_t run = __shfl_up(incl, 1, 64);
+    if ((threadIdx.x & 63) == 0) run = threadIdx.x > 0 ? sh[(threadIdx.x >> 6) - 1] : ident;
 #pragma unroll
     for (int j = 0; j < SC_ITEMS; ++j) {
         const int64_t i = base + j;
@@ -263,7 +251,7 @@ __global__ __launch_bounds__(SC_THREADS) void scan_tile_kernel(const int32_t* in
         if (i < n) out[i] = INCL ? nxt : run;
         run = nxt;
     }
-    if (threadIdx.x == SC_THREADS - 1 && block_sums) block_sums[blockIdx.x] = sh[SC_THREADS - 1];
+    if (threadIdx.x == SC_THREADS - 1 && block_sums) block_sums[blockIdx.x] = incl;
 }
 
 template <bool MAX>

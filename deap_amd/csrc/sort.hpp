@@ -32,6 +32,35 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
                              int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
                              int end_bit, void* temp);
 
+// Inclusive scan (sum, or max when MAX) over the NT threads of a workgroup:
+// lane shuffles within each wave, one wave scans the wave totals -- two
+// barriers (an LDS Hillis-Steele scan over 256 slots takes 16).  sh: NT / 64
+// ints of LDS.  Every thread must call it.
+template <int NT, bool MAX>
+__device__ __forceinline__ int32_t block_incl_scan(int32_t v, int32_t* sh) {
+    static_assert(NT % 64 == 0 && NT / 64 <= 64, "whole waves, at most 64");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = MAX ? max(x, y) : x + y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        int32_t w = lane < NT / 64 ? sh[lane] : (MAX ? INT32_MIN : 0);
+#pragma unroll
+        for (int o = 1; o < NT / 64; o <<= 1) {
+            const int32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w = MAX ? max(w, y) : w + y;
+        }
+        if (lane < NT / 64) sh[lane] = w;
+    }
+    __syncthreads();
+    return wave ? (MAX ? max(x, sh[wave - 1]) : x + sh[wave - 1]) : x;
+}
+
 size_t scan_temp_bytes(int64_t n);
 // out[i] = sum_{j<i} in[j] (exclusive); *total (device, may be null) = sum.
 int exclusive_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
