@@ -872,8 +872,16 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
         for (int i = 0; i < m; ++i) {
             crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U, weights[i] < 0.0,
                                                         fid, pos, rbits, keys, T);
-            int rc = radix_sort_pairs(s, keys, pos, ktmp, vtmp, T, 0, kbits, rtemp);
+            // an odd pass count leaves the pairs in the tmp buffers: swap
+            // the roles instead of copying back (the keys are rebuilt per
+            // objective, only pos carries over)
+            bool in_tmp = false;
+            int rc = radix_sort_pairs_any(s, keys, pos, ktmp, vtmp, T, 0, kbits, rtemp, &in_tmp);
             if (rc) return rc;
+            if (in_tmp) {
+                std::swap(keys, ktmp);
+                std::swap(pos, vtmp);
+            }
             crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
                                                       fstart_dev, T, crowd);
         }

@@ -158,7 +158,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
 
 int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                              int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
-                             int end_bit, void* temp) {
+                             int end_bit, void* temp, bool* in_tmp) {
+    if (in_tmp) *in_tmp = false;
     if (nseg <= 0 || seglen <= 1 || end_bit <= begin_bit) return DM_OK;
     const int64_t n = nseg * seglen;
     DM_CHECK_ARG(n < (1ll << 30), "radix sort of more than 2^30 keys");
@@ -189,7 +190,9 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    if (passes & 1) {
+    if ((passes & 1) && in_tmp) {
+        *in_tmp = true;  // the caller takes the result from the tmp buffers
+    } else if (passes & 1) {
         DM_HIP(hipMemcpyAsync(keys, kin, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
         DM_HIP(hipMemcpyAsync(vals, vin, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
     }
@@ -200,7 +203,13 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
 int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                      int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp) {
     return radix_sort_pairs_batched(s, keys, vals, keys_tmp, vals_tmp, 1, n, begin_bit, end_bit,
-                                    temp);
+                                    temp, nullptr);
+}
+int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                         int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp,
+                         bool* in_tmp) {
+    return radix_sort_pairs_batched(s, keys, vals, keys_tmp, vals_tmp, 1, n, begin_bit, end_bit,
+                                    temp, in_tmp);
 }
 
 // ---------------------------------------------------------------------------

@@ -30,7 +30,12 @@ int radix_sort_pairs(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* key
 size_t radix_sort_batched_temp_bytes(int64_t nseg, int64_t seglen);
 int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                              int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
-                             int end_bit, void* temp);
+                             int end_bit, void* temp, bool* in_tmp = nullptr);
+// radix_sort_pairs without the copy back after an odd number of passes:
+// *in_tmp tells whether the sorted pairs are in keys_tmp / vals_tmp.
+int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
+                         int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp,
+                         bool* in_tmp);
 
 // Inclusive scan (sum, or max when MAX) over the NT threads of a workgroup:
 // lane shuffles within each wave, one wave scans the wave totals -- two
