@@ -121,7 +121,7 @@ __global__ __launch_bounds__(1024) void bd_plan_kernel(const int4* __restrict__ 
                                                        int64_t NG, int64_t ngroups,
                                                        int32_t* rowfirst, int32_t* reach,
                                                        int32_t* toffD, int32_t* toffC) {
-    __shared__ int32_t shD[1024], shC[1024];
+    __shared__ int32_t shD[1024 / 64], shC[1024 / 64];  // wave totals of the scans
     __shared__ int32_t carryD, carryC;
     const int tid = threadIdx.x;
     if (tid == 0) carryD = carryC = 0;
@@ -145,26 +145,17 @@ __global__ __launch_bounds__(1024) void bd_plan_kernel(const int4* __restrict__ 
             reach[c] = re;
             nC = (re + BD_RT - 1) / BD_RT;
         }
-        shD[tid] = nD;
-        shC[tid] = nC;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            const int32_t aD = tid >= off ? shD[tid - off] : 0;
-            const int32_t aC = tid >= off ? shC[tid - off] : 0;
-            __syncthreads();
-            shD[tid] += aD;
-            shC[tid] += aC;
-            __syncthreads();
-        }
+        const int32_t iD = block_incl_scan<1024, false>(nD, shD);
+        const int32_t iC = block_incl_scan<1024, false>(nC, shC);
         const int32_t cD = carryD, cC = carryC;
         if (c < NG) {
-            toffD[c] = cD + shD[tid] - nD;
-            toffC[c] = cC + shC[tid] - nC;
+            toffD[c] = cD + iD - nD;
+            toffC[c] = cC + iC - nC;
         }
         __syncthreads();
         if (tid == 1023) {
-            carryD = cD + shD[1023];
-            carryC = cC + shC[1023];
+            carryD = cD + iD;
+            carryC = cC + iC;
         }
         __syncthreads();
     }

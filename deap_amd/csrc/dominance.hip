@@ -106,6 +106,29 @@ constexpr int TD_SEGS = 2;  // 8-block row segments (512 v) per task
 // nseg[g]: 8-block segments of v the rows of A-group g reach (every v whose
 // rank_0 <= the group's largest); toff[g]: first task of g (TD_SEGS segments
 // per task), toff[ngroups] = tasks.  One workgroup; nseg is nondecreasing.
+// nseg[g] = the 512-v segments row group g (TD_WPW 64-row blocks) can
+// reach: up to the last q whose rank_0 does not exceed the group's largest
+// (rank_0 ascends with q).
+__device__ __forceinline__ int32_t group_reach(const int4* S, int m, int64_t U, int64_t NG,
+                                               int64_t g) {
+    const int64_t last = std::min<int64_t>((g + 1) * TD_WPW * 64, U) - 1;
+    const int32_t rmax = icomp(S[last], m - 1);
+    int64_t lo = last, hi = U - 1;  // last q with rank_0 <= rmax
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (icomp(S[mid], m - 1) <= rmax) lo = mid;
+        else hi = mid - 1;
+    }
+    return (int32_t)std::min<int64_t>(NG, (lo >> 9) + 1);
+}
+// the bitset path needs only nseg (no compare-kernel tile offsets): one
+// thread per group over the whole grid instead of tri_plan_kernel's single
+// workgroup (18.6 us at C5)
+__global__ void group_reach_kernel(const int4* S, int m, int64_t U, int64_t NG, int64_t ngroups,
+                                   int32_t* nseg) {
+    DGRID_LOOP(g, ngroups) nseg[g] = group_reach(S, m, U, NG, g);
+}
+
 __global__ __launch_bounds__(1024) void tri_plan_kernel(const int4* S, int m, int64_t U,
                                                         int64_t NG, int64_t ngroups,
                                                         int32_t* nseg, int32_t* toff,
@@ -122,15 +145,7 @@ __global__ __launch_bounds__(1024) void tri_plan_kernel(const int4* S, int m, in
         const int64_t g = base + tid;
         int32_t nt = 0;
         if (g < ngroups) {
-            const int64_t last = std::min<int64_t>((g + 1) * TD_WPW * 64, U) - 1;
-            const int32_t rmax = icomp(S[last], m - 1);
-            int64_t lo = last, hi = U - 1;  // last q with rank_0 <= rmax
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) >> 1;
-                if (icomp(S[mid], m - 1) <= rmax) lo = mid;
-                else hi = mid - 1;
-            }
-            const int32_t ns = (int32_t)std::min<int64_t>(NG, (lo >> 9) + 1);
+            const int32_t ns = group_reach(S, m, U, NG, g);
             nseg[g] = ns;
             nt = (ns + TD_SEGS - 1) / TD_SEGS;
         }
@@ -1568,11 +1583,13 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
         if ((rc = exclusive_scan_i32(s, flag, vtmp, nb, nullptr, stemp))) return rc;
         rank_scatter_kernel<<<dg1(nb), 256, 0, s>>>(vals, vtmp, flag, pos, U, nb, (int32_t*)S);
     }
-    tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
-    if (fast_bitset(m))  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)
+    if (fast_bitset(m)) {  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)
+        group_reach_kernel<<<dg1(L.ngroups), 256, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg);
         return bitdom_build(ctx, S, m, U, L.NQ, L.ngroups, nseg, sigma,
                             fast_table_peel(m) ? nullptr : D, count, (int32_t*)(ws + L.countq),
                             (char*)part);
+    }
+    tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
     const unsigned blocks = (unsigned)std::max(1, num_cus) * 8;
     timing_begin(ctx, DM_TIME_DOMINANCE);
     switch (m) {
