@@ -64,27 +64,25 @@ __global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __rest
                                                               uint32_t* __restrict__ P,
                                                               int32_t* __restrict__ R,
                                                               uint16_t* __restrict__ BK) {
-    __shared__ int32_t r[BD_CW];
+    __shared__ uint64_t sk[BD_CW];  // the bitonic sort's long strides
+    __shared__ int32_t lrs[BD_CW];
     __shared__ int32_t sorted[BD_CW];
     const int64_t c = blockIdx.x;
     const int f = blockIdx.y;
     const int t = threadIdx.x;
     const int64_t v = c * BD_CW + t;
-    const int32_t rv = v < U ? icomp(S[v], f) : INT32_MAX;
-    r[t] = rv;
-    __syncthreads();
-    int32_t lr = 0;
-#pragma unroll 16
-    for (int i = 0; i < BD_CW; ++i) {
-        const int32_t ri = r[i];
-        lr += (ri < rv || (ri == rv && i < t)) ? 1 : 0;
-    }
+    const int32_t rv = v < U ? icomp(S[v], f) : INT32_MAX;  // ranks >= 0
+    // local rank of v = its place in the chunk sorted by (rank, position): a
+    // bitonic sort of (rank << 32 | position) (the direct count compared
+    // every pair of the chunk, 512 LDS reads and compares per thread)
+    uint64_t key[1] = {((uint64_t)(uint32_t)rv << 32) | (uint32_t)t};
+    block_bitonic<BD_THREADS, 1>(key, sk);
+    lrs[(uint32_t)key[0]] = t;
+    sorted[t] = (int32_t)(key[0] >> 32);
     const int64_t cf = c * F + f;
-    if (BD_OK(lr, BD_CW, "table lr")) {
-        R[cf * BD_CW + lr] = rv;
-        sorted[lr] = rv;
-    }
+    R[cf * BD_CW + t] = sorted[t];
     __syncthreads();
+    const int32_t lr = lrs[t];
     // bucket starts: BK[b] = #{sorted ranks < b << sh}
     const int sh = bd_bucket_shift(U);
     for (int b = t; b < BD_BKN; b += BD_THREADS) {
@@ -97,7 +95,11 @@ __global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __rest
         }
         BK[cf * BD_BKN + b] = (uint16_t)lo;
     }
-    uint32_t* Pc = P + cf * BD_K * 16;
+    // the sets are built in LDS (wave w owns word w of every set) and then
+    // stored as whole 64-B sets by consecutive threads: 16-B stores, each
+    // wave instruction one contiguous KiB (the direct form wrote 8 B per lane
+    // into 64 different lines per instruction)
+    __shared__ uint64_t sP[BD_K][BD_CW / 64];
     const int wave = t >> 6, lane = t & 63;
     for (int k0 = 0; k0 < BD_K; k0 += 64) {
         uint64_t mine = 0;
@@ -107,8 +109,12 @@ __global__ __launch_bounds__(BD_THREADS) void bd_table_kernel(const int4* __rest
             mine = lane == i ? b : mine;
         }
         const int k = k0 + lane;
-        if (k < BD_K) *reinterpret_cast<uint64_t*>(Pc + (int64_t)k * 16 + 2 * wave) = mine;
+        if (k < BD_K) sP[k][wave] = mine;
     }
+    __syncthreads();
+    uint4* Pc = reinterpret_cast<uint4*>(P + cf * BD_K * 16);
+    const uint4* src = reinterpret_cast<const uint4*>(&sP[0][0]);
+    for (int i = t; i < BD_K * 4; i += BD_THREADS) Pc[i] = src[i];
 }
 
 // Per chunk c: rowfirst[c] = first row of the A-groups whose reach includes c

@@ -34,6 +34,72 @@ __host__ __device__ __forceinline__ int64_t tword(int64_t u, int64_t w, int64_t 
     return ((((u >> 6) * NQ + w / TW) << 6) + (u & 63)) * TW + (w % TW);
 }
 
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+    const uint32_t lo = __shfl_xor((uint32_t)x, m, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Bitonic sort of P = NT * E keys held E per thread (element i = tid*E + e),
+// ascending: compare-exchanges of stride < E stay in registers, strides below
+// 64 E go through lane shuffles, only the longer ones through LDS (one
+// barrier per stage), so a 2,048-key sort needs 18 barriers instead of 66.
+template <int NT, int E>
+__device__ void block_bitonic(uint64_t (&k)[E], uint64_t* lds) {
+    constexpr int P = NT * E;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int size = 2; size <= P; size <<= 1) {
+        int stride = size >> 1;
+        if (stride >= 64 * E) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) lds[tid * E + e] = k[e];
+            __syncthreads();
+            for (; stride >= 64 * E; stride >>= 1) {
+                for (int q = tid; q < P / 2; q += NT) {
+                    const int a = 2 * q - (q & (stride - 1));
+                    const int b = a + stride;
+                    const bool up = (a & size) == 0;
+                    const uint64_t ka = lds[a], kb = lds[b];
+                    if ((ka > kb) == up) {
+                        lds[a] = kb;
+                        lds[b] = ka;
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) k[e] = lds[tid * E + e];
+            __syncthreads();
+        }
+        for (; stride >= E; stride >>= 1) {
+            const int ls = stride / E;
+            const bool lower = (lane & ls) == 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t p = shfl_xor_u64(k[e], ls);
+                const bool up = ((tid * E + e) & size) == 0;
+                const bool take_min = lower == up;
+                k[e] = take_min ? (p < k[e] ? p : k[e]) : (p > k[e] ? p : k[e]);
+            }
+        }
+        // strides below E: registers of this thread (compile-time indices)
+#pragma unroll
+        for (int st2 = E / 2; st2 > 0; st2 >>= 1) {
+            if (st2 >= size) continue;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                if (e & st2) continue;
+                const int f = e | st2;
+                const bool up = ((tid * E + e) & size) == 0;
+                const uint64_t a = k[e], b = k[f];
+                const bool sw = (a > b) == up;
+                k[e] = sw ? b : a;
+                k[f] = sw ? a : b;
+            }
+        }
+    }
+}
+
 // bitdom.hip: dominator counts and (when D is not null) the D words by bitset
 // tables (the default dominance pass of the fast path).  ws: that pass's
 // scratch of bitdom_bytes(U, m) bytes, which keeps the tables for the
