@@ -24,6 +24,8 @@ DM_MUT_NONE, DM_MUT_FLIPBIT, DM_MUT_GAUSSIAN = 0, 1, 2
 DM_SEL_IDENTITY, DM_SEL_INDEX, DM_SEL_TOURNAMENT, DM_SEL_RANDOM = 0, 1, 2, 3
 DM_RNG_NATIVE, DM_RNG_INJECT, DM_RNG_DUMP = 0, 1, 2
 DM_TIME_GENERATION, DM_TIME_DOMINANCE = 0, 1
+# enum dm_dom_path: sortNondominated's default path and its cross-check paths
+DM_DOM_PATHS = {"default": 0, "compare": 1, "peel_d": 2, "ballot": 3, "lds": 4}
 (DM_EVAL_NONE, DM_EVAL_ONEMAX, DM_EVAL_RASTRIGIN, DM_EVAL_ROSENBROCK, DM_EVAL_ZDT1,
  DM_EVAL_ZDT2, DM_EVAL_ZDT3, DM_EVAL_ZDT4, DM_EVAL_ZDT6, DM_EVAL_DTLZ1, DM_EVAL_DTLZ2,
  DM_EVAL_DTLZ3, DM_EVAL_DTLZ4, DM_EVAL_SPHERE) = range(14)
@@ -85,6 +87,8 @@ SIGNATURES = {
     "dm_ctx_set_timing": (ctypes.c_int, [_p, _i32]),
     "dm_ctx_kernel_times": (ctypes.c_int, [_p, _p, _i32, _PP(_i32)]),
     "dm_ctx_set_timing_target": (ctypes.c_int, [_p, _i32]),
+    "dm_ctx_set_dom_path": (ctypes.c_int, [_p, _i32]),
+    "dm_ctx_dom_bitset": (ctypes.c_int, [_p, _i32]),
     "dm_philox_blocks": (ctypes.c_int, [_p, _PP(_u32), _PP(_u32), _i64, _p]),
     "dm_init_uniform": (ctypes.c_int, [_p, _PP(DevicePop), _f64, _f64, Rng]),
     "dm_evaluate": (ctypes.c_int, [_p, _PP(DevicePop), _PP(Eval), ctypes.c_int, _p]),
@@ -102,6 +106,10 @@ SIGNATURES = {
                                             _PP(_i64), _PP(_i32)]),
     "dm_crowding_dist": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _p, _p, _i32, _p]),
     "dm_sel_nsga2": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _i64, _p, _p]),
+    "dm_sort_log_nondominated": (ctypes.c_int, [_p, _PP(DevicePop), _i64, _i32, _p, _p,
+                                                _PP(_i64), _PP(_i32)]),
+    "dm_sel_nsga2_log": (ctypes.c_int, [_p, _PP(DevicePop), _PP(_f64), _i64, _p, _p]),
+    "dm_gather_f64": (ctypes.c_int, [_p, _p, _p, _i64, _p]),
     "dm_sel_tournament_dcd": (ctypes.c_int, [_p, _PP(DevicePop), _p, _i64, Rng, _i32, _p, _p, _p,
                                              _p]),
     "dm_vary_bounded": (ctypes.c_int, [_p, _PP(DevicePop), _p, _PP(DevicePop), _PP(BoundedVar),

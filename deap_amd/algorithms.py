@@ -371,7 +371,15 @@ class MuPlusLambdaStep:
         _lib.call("dm_gather", ctx, ctypes.byref(pool.c_pop()), ctypes.c_void_p(idx.data_ptr()),
                   ctypes.byref(self.nxt.c_pop(0, self.mu)))
         if getattr(pool, "crowding_dist", None) is not None:
-            self.nxt.crowding_dist = pool.crowding_dist[idx.long()]
+            # fitness.crowding_dist travels with the clones (base.py:252-261
+            # copies the fitness object): one library gather, buffers of the
+            # same capacity swap with the storage below
+            if self.nxt.crowding_dist is None or \
+                    len(self.nxt.crowding_dist) < len(pool.crowding_dist):
+                self.nxt.crowding_dist = pool.crowding_dist.new_empty(len(pool.crowding_dist))
+            _lib.call("dm_gather_f64", ctx, ctypes.c_void_p(pool.crowding_dist.data_ptr()),
+                      ctypes.c_void_p(idx.data_ptr()), len(idx),
+                      ctypes.c_void_p(self.nxt.crowding_dist.data_ptr()))
         comb.swap_storage(self.nxt)
         self.n = self.mu
         comb.resize(self.mu)

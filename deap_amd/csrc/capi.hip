@@ -416,6 +416,7 @@ __global__ __launch_bounds__(256) void stats_combine_kernel(const StatAcc* part,
     q[7] = (double)(a.cnt + a.nan);
 }
 
+bool fast_bitset(const dm_ctx* ctx, int m);  // dominance.hip
 }  // namespace dm
 
 using namespace dm;
@@ -425,12 +426,28 @@ extern "C" {
 const char* dm_last_error(void) { return dm::g_err; }
 const char* dm_version(void) { return "deapmi 0.1 gfx950"; }
 
+static int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
 int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
     DM_CHECK_ARG(out != nullptr, "null out");
     DM_HIP(hipSetDevice(device));
     dm_ctx* c = new dm_ctx();
     c->device = device;
     c->stream = (hipStream_t)hip_stream;
+    dm_knobs& kn = c->knobs;  // A/B switches, read once (common.hpp)
+    kn.disable_pipe = std::getenv("DM_DISABLE_PIPE") != nullptr;
+    kn.bits_plan = std::getenv("DM_BITS_PLAN") != nullptr;
+    kn.bits_nocount = std::getenv("DM_BITS_NOCOUNT") != nullptr;
+    kn.bits_nokeys = std::getenv("DM_BITS_NOKEYS") != nullptr;
+    kn.bits_pp4 = std::getenv("DM_BITS_PP4") != nullptr;
+    kn.lex_full = std::getenv("DM_LEX_FULL") != nullptr;
+    kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
+    kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
+    kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);
+    kn.bd_maxm = env_int("DM_BD_MAXM", 3);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
@@ -453,6 +470,18 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
     }
     *out = c;
     return DM_OK;
+}
+
+int dm_ctx_set_dom_path(dm_ctx* ctx, int32_t path) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    DM_CHECK_ARG(path >= DM_DOM_DEFAULT && path <= DM_DOM_LDS, "unknown dominance path %d", path);
+    ctx->dom_path = path;
+    return DM_OK;
+}
+
+int dm_ctx_dom_bitset(dm_ctx* ctx, int32_t nobj) {
+    return ctx && dm::fast_bitset(ctx, nobj) && ctx->dom_path != DM_DOM_LDS &&
+           ctx->dom_path != DM_DOM_BALLOT ? 1 : 0;
 }
 
 int dm_ctx_destroy(dm_ctx* ctx) {

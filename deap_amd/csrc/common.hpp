@@ -46,6 +46,22 @@ constexpr int kEvalSpread = 64, kEvalSpreadStride = 16;  // counters, int64 stri
 // evals_spread layout (int64 words): count[g] at g*16, ticket[g] at (64+g)*16,
 // the total at 128*16 and its ticket at 129*16 (g < kEvalSpread)
 constexpr int kEvalSpreadWords = (2 * kEvalSpread + 2) * kEvalSpreadStride;
+// Tuning switches for A/B measurements (tools_gpu/), read ONCE from the
+// environment at dm_ctx_create; all off by default.  None of them changes a
+// result: every one selects between bit-identical kernels.
+struct dm_knobs {
+    bool disable_pipe = false;      // DM_DISABLE_PIPE: general kernels instead of the hot ones
+    bool bits_plan = false;         // DM_BITS_PLAN: C2 through the plan + burst kernels
+    bool bits_nocount = false;      // DM_BITS_NOCOUNT: C2 without the nevals count (ablation)
+    bool bits_nokeys = false;       // DM_BITS_NOKEYS: C2 tournaments read wvalues, no int16 keys
+    bool bits_pp4 = false;          // DM_BITS_PP4: 4 pairs per wave in the fused C2 kernel
+    bool lex_full = false;          // DM_LEX_FULL: full lexicographic sort in the grouping
+    bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
+    int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
+    int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)
+    int bd_maxm = 3;                // DM_BD_MAXM: most objectives on the bitset dominance path
+};
+
 struct dm_ctx {
     static constexpr int kSlots = 5;
     int device = 0;
@@ -67,6 +83,10 @@ struct dm_ctx {
     std::vector<hipEvent_t> tev;
     int tev_used = 0;  // pairs recorded so far
     int timing_target = 0;  // DM_TIME_GENERATION / DM_TIME_DOMINANCE: which launches
+    dm_knobs knobs;
+    // sortNondominated dominance path (dm_ctx_set_dom_path): DM_DOM_DEFAULT or
+    // one of the cross-check paths the parity tests compare against it
+    int32_t dom_path = 0;
 };
 
 namespace dm {

@@ -1250,131 +1250,6 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
                                         lds, part, sc);
 }
 
-// ---------------------------------------------------------------------------
-// Persistent peel: ONE cooperative launch peels front after front (VERDICT
-// r2: 58 peel + 58 order launches per selection at ~33 + 8 us each, mostly
-// dispatch and dependent-load latency).  Every workgroup of the co-resident
-// grid takes (segment, slice) tasks of the current front; the workgroup that
-// finishes last orders the released candidates (order_front, NT = the peel's
-// 512 threads, PP_CAP candidates in the peel's LDS) while the others wait for
-// it (front_arrive / front_wait); all read the state and stop together when
-// done (or on an overflow of PP_CAP,
-// which the host's radix sort resolves before relaunching).  Cross-workgroup
-// data moves through sc1 accesses and device atomics (cld / cst), the
-// barrier is an arrival counter; a watchdog turns a barrier that does not
-// complete in ~0.25 s into an error flag instead of a hang.
-// ---------------------------------------------------------------------------
-constexpr int PP_THREADS = PEEL_WAVES * 64;
-constexpr int PP_CAP = 8192;
-struct PersistLds {
-    union {
-        PeelLds peel;
-        OrderLds<PP_CAP> order;
-    } u;
-    PeelSmall ps;
-    OrderScalars os;
-    int32_t part[PP_THREADS];
-    int32_t sF, sust, snf, sstop, ok;
-};
-static_assert(sizeof(PersistLds) <= 80 * 1024, "persistent peel LDS");
-
-// Front barrier of the persistent peel, "last arriver orders": every
-// workgroup arrives once per front (a returning device atomic on bar[0]); the
-// one that completes the count (bar[0] == front * grid) runs the ordering
-// phase itself and then publishes the front number in bar[16]; the others
-// wait for that word.  One barrier per front, no second rendezvous, and the
-// ordering starts the moment the last peel task ends.  Returns -1 when the
-// wait timed out or another workgroup flagged an error (*err set), 1 for the
-// orderer, 0 otherwise.
-__device__ int front_arrive(unsigned* bar, unsigned front, unsigned nwg, int32_t* err,
-                            int32_t& role) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are performed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        role = old + 1 == front * nwg ? 1 : 0;
-    }
-    __syncthreads();
-    return role;
-}
-__device__ bool front_wait(unsigned* bar, unsigned front, int32_t* err, int32_t& ok) {
-    if (threadIdx.x == 0) {
-        ok = 1;
-        uint32_t it = 0;
-        while (__hip_atomic_load(bar + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < front) {
-            __builtin_amdgcn_s_sleep(8);
-            if ((++it & 255u) == 0 &&
-                (it > (1u << 19) ||
-                 __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    return ok != 0;
-}
-
-struct PersistArgs {
-    const uint64_t* D;
-    int64_t NQ;
-    int2* mrow;
-    const int32_t* gsize;
-    const int32_t* sigma;
-    FrontState* st;
-    int32_t* countq;
-    unsigned long long* lastq;
-    uint64_t* ckey;
-    int32_t* cq;
-    int32_t* rankU;
-    int32_t* ulist;
-    const int32_t* pos;
-    const int32_t* nseg;
-    int32_t* fstarts;
-    unsigned* bar;  // zeroed before the launch
-    int32_t* err;   // zeroed before the launch
-};
-
-__global__ __launch_bounds__(PP_THREADS) void peel_persistent_kernel(PersistArgs a) {
-    __shared__ PersistLds L;
-    const unsigned nwg = gridDim.x;
-    const int64_t U = a.st->U;  // set by front_init_kernel (an earlier launch)
-    unsigned epoch = 0;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            L.sF = cld<true>(&a.st->F);
-            L.sust = cld<true>(&a.st->ustart);
-            L.snf = cld<true>(&a.st->nfronts);
-            L.sstop = cld<true>(&a.st->done) | cld<true>(&a.st->overflow) |
-                      cld<true>(a.err);
-        }
-        __syncthreads();
-        if (L.sstop) break;  // the same state for every workgroup: all stop together
-        const int32_t sF = L.sF, sust = L.sust, snf = L.snf;
-        const int64_t ntask = a.NQ * PEEL_SLICES;
-        for (int64_t t = blockIdx.x; t < ntask; t += nwg) {
-            const int64_t s = t % a.NQ, y = t / a.NQ;
-            const int64_t nsl = peel_slices(sF, s, a.NQ, PEEL_SLICES);
-            if (y >= nsl) continue;
-            peel_segment<true>(a.D, a.NQ, a.mrow, a.gsize, a.sigma, a.st, a.countq, a.lastq,
-                               a.ckey, a.cq, a.rankU, U, sF, sust, snf, s, y, nsl, L.u.peel, L.ps);
-        }
-        ++epoch;
-        if (front_arrive(a.bar, epoch, nwg, a.err, L.ok)) {
-            order_front<PP_THREADS, PP_CAP, true>(a.st, a.ckey, a.cq, a.ulist, a.mrow, a.pos,
-                                                  a.nseg, a.fstarts, 0, L.u.order, L.part, L.os);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_store(a.bar + 16, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (!front_wait(a.bar, epoch, a.err, L.ok)) {
-            break;
-        }
-    }
-}
-
 __global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, const int32_t* pos,
                                    const int32_t* nseg, int2* mrow) {
     const int64_t F = *Fp;
@@ -1463,13 +1338,12 @@ int64_t fast_dom_words(int64_t U) {
 // 104,640-B LDS kernel runs clean on the same boxes (tools_gpu/lds_probe.hip) —
 // unresolved; DM_BD_MAXM=4 re-enables them for diagnosis.
 // With the bitset pass the peel reads the tables, not a D matrix
-// (peel_tab_kernel), unless DM_PEEL_D / DM_PEEL_PERSIST ask for the D peel.
-bool fast_bitset(int m) {
-    const char* bdmax = std::getenv("DM_BD_MAXM");
-    return m >= 2 && m <= (bdmax ? atoi(bdmax) : 3) && !std::getenv("DM_DOM_TRI");
+// (peel_tab_kernel), unless the DM_DOM_PEEL_D cross-check asks for the D peel.
+bool fast_bitset(const dm_ctx* ctx, int m) {
+    return m >= 2 && m <= ctx->knobs.bd_maxm && ctx->dom_path != DM_DOM_COMPARE;
 }
-bool fast_table_peel(int m) {
-    return fast_bitset(m) && !std::getenv("DM_PEEL_D") && !std::getenv("DM_PEEL_PERSIST");
+bool fast_table_peel(const dm_ctx* ctx, int m) {
+    return fast_bitset(ctx, m) && ctx->dom_path != DM_DOM_PEEL_D;
 }
 
 // Ranks (objective 0 from the population's lexicographic order perm, whose
@@ -1518,10 +1392,10 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
         if ((rc = exclusive_scan_i32(s, flag, vtmp, nb, nullptr, stemp))) return rc;
         rank_scatter_kernel<<<dg1(nb), 256, 0, s>>>(vals, vtmp, flag, pos, U, nb, (int32_t*)S);
     }
-    if (fast_bitset(m)) {  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)
+    if (fast_bitset(ctx, m)) {  // bitset tables (bitdom.hip; DM_TIME_DOMINANCE: its count pass)
         group_reach_kernel<<<dg1(L.ngroups), 256, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg);
         return bitdom_build(ctx, S, m, U, L.NQ, L.ngroups, nseg, sigma,
-                            fast_table_peel(m) ? nullptr : D, count, (int32_t*)(ws + L.countq),
+                            fast_table_peel(ctx, m) ? nullptr : D, count, (int32_t*)(ws + L.countq),
                             (char*)part);
     }
     tri_plan_kernel<<<1, 1024, 0, s>>>(S, m, U, L.NG, L.ngroups, nseg, toff, counter);
@@ -1615,50 +1489,12 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     FrontState* hst = (FrontState*)hbuf;
     int32_t* hfs = (int32_t*)(hbuf + 256);
     const int64_t npre = std::min<int64_t>((2048 - 256) / 4, U + 2);
-    // persistent peel (opt-in, DM_PEEL_PERSIST=1): one cooperative launch per
-    // run of fronts (until done, or until a front exceeds PP_CAP candidates).
-    // Measured slower than the launch pair per front on C5 (7.11 vs 6.44 ms
-    // per generation on one box, profiles/r03d): the sc1 member / key traffic
-    // and the barrier polling cost more than the launches they replace.
-    static const bool persist = std::getenv("DM_PEEL_PERSIST") != nullptr;
     // table-fed peel: the bitset pass's tables in the part region
-    const bool tab = fast_table_peel(m);
+    const bool tab = fast_table_peel(ctx, m);
     const BitdomLayout TL = bitdom_layout(U, m);
     const char* tws = ws + L.part;
-    int grid = 0;
-    if (persist && !tab) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peel_persistent_kernel,
-                                                         PP_THREADS, 0) == hipSuccess)
-            grid = (int)std::min<int64_t>((int64_t)per_cu * ctx->num_cus, L.NQ * PEEL_SLICES);
-    }
-    while (grid > 0) {
-        DM_HIP(hipMemsetAsync(bar, 0, 256, s));
-        PersistArgs pa{D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU, ulist,
-                       pos, nseg, fstarts, bar, perr};
-        void* kargs[] = {&pa};
-        DM_HIP(hipLaunchCooperativeKernel((const void*)peel_persistent_kernel, dim3((unsigned)grid),
-                                          dim3(PP_THREADS), kargs, 0, s));
-        DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
-        DM_HIP(hipMemcpyAsync(hbuf + 200, perr, 4, hipMemcpyDeviceToHost, s));
-        DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));
-        DM_HIP(hipStreamSynchronize(s));
-        if (*(int32_t*)(hbuf + 200)) {
-            set_error("persistent front peel: a grid barrier timed out (grid %d)", grid);
-            return DM_ERR_HIP;
-        }
-        if (hst->done) break;
-        DM_CHECK_ARG(hst->overflow, "persistent front peel stopped before the last front");
-        // a front too large for the in-kernel sort: the radix sort orders its keys
-        const int32_t nc = hst->ncand;
-        DM_HIP(hipMemsetAsync(vals, 0, (size_t)nc * 4, s));
-        int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, nc, 0, 64, rtemp);
-        if (rc) return rc;
-        front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
-        DM_LAUNCH_CHECK();
-    }
-    // multi-launch peel (DM_PEEL_MULTI, or no cooperative grid): first status
-    // check after as many fronts as the previous call needed
+    // launch pairs (peel, order) per front: first status check after as many
+    // fronts as the previous call needed
     // (the previous call's front count + 1, so that a selection like the last
     // one needs a single status read; up to PEEL_BATCH_MAX launch pairs)
     constexpr int PEEL_BATCH_MAX = 96;
@@ -1667,7 +1503,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                         N == ctx->peel_hint_N;
     const int hint = hinted ? ctx->peel_hint : 4;
     int batch = std::max(2, std::min(hint + 1, PEEL_BATCH_MAX));
-    for (; grid == 0;) {
+    for (;;) {
         for (int b = 0; b < batch; ++b) {
             if (tab) {
                 const dim3 g((unsigned)((TL.NG + 7) & ~7ll), PEEL_SLICES);

@@ -115,7 +115,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     // persistent grid (generation_pipe.hpp)
     if (mode == DM_RNG_NATIVE && parents->gtype != DM_BITS && parents->dim > 64 &&
         parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
-        ec != EC_MO && !std::getenv("DM_DISABLE_PIPE")) {
+        ec != EC_MO && !ctx->knobs.disable_pipe) {
         const int nch = parents->dim <= 512 ? 2 : 4;
         PairPlan* plans = (PairPlan*)scratch(ctx, (size_t)npairs * sizeof(PairPlan));
         if (!plans) return DM_ERR_NOMEM;
@@ -147,7 +147,8 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.sigma = a.sigma;
         q.w0 = a.w0;
         q.ev = a.ev;
-        q.ntload = std::getenv("DM_PIPE_NTLOAD") ? atoi(std::getenv("DM_PIPE_NTLOAD")) : 0;
+        q.bpc = ctx->knobs.pipe_bpc;
+        q.depth = ctx->knobs.pipe_depth;
         timing_begin(ctx);
         if (parents->gtype == DM_F64)
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
@@ -162,32 +163,24 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     // counts nevals) + the burst kernel (generation_pipe_bits.hip)
     if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 64 &&
         parents->nobj == 1 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
-        !std::getenv("DM_DISABLE_PIPE")) {
-        if ((sel == DM_SEL_RANDOM || tournsize <= 8) && !std::getenv("DM_BITS_PLAN")) {
+        !ctx->knobs.disable_pipe) {
+        if ((sel == DM_SEL_RANDOM || tournsize <= 8) && !ctx->knobs.bits_plan) {
             // one launch: decisions drawn inside the burst kernel (+ the
             // nevals reduction of its per-workgroup partials)
-            const bool count = ec != EC_NONE && a.nevals && !std::getenv("DM_BITS_NOCOUNT");
+            const bool count = ec != EC_NONE && a.nevals && !ctx->knobs.bits_nocount;
             // tournaments read the parents' fitness through int16 keys (one
             // coalesced pass, timed with the generation kernel)
-            static const bool no_keys = std::getenv("DM_BITS_NOKEYS") != nullptr;
-            const bool keys = sel == DM_SEL_TOURNAMENT && a.w0 != 0.0 && !no_keys;
+            const bool keys = sel == DM_SEL_TOURNAMENT && a.w0 != 0.0 && !ctx->knobs.bits_nokeys;
             if (keys) {
                 int16_t* kb = (int16_t*)scratch(ctx, (size_t)a.np * 2 + 16);
                 if (!kb) return DM_ERR_NOMEM;
                 a.pkeys = kb;
             }
-            static const bool split = std::getenv("DM_BITS_SPLIT") != nullptr;
-            void* bplans = nullptr;
-            if (split && !(bplans = scratch_slot(ctx, 1, gen_bits_split_bytes(a))))
-                return DM_ERR_NOMEM;
+            a.pp4 = ctx->knobs.bits_pp4 ? 1 : 0;
             timing_begin(ctx);
             if (keys) launch_fit_keys(a, (int16_t*)a.pkeys, ctx->stream);
-            if (split)
-                launch_gen_bits_split(a, ec != EC_NONE, bplans,
-                                      count ? ctx->evals_spread : nullptr, ctx->stream);
-            else
-                launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
-                                      ctx->stream);
+            launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,
+                                  ctx->stream);
             timing_end(ctx);
             DM_LAUNCH_CHECK();
             return DM_OK;

@@ -259,7 +259,7 @@ struct PipeArgs {
     int64_t* nevals;
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
-    int32_t ntload;  // non-temporal parent-row loads (DM_PIPE_NTLOAD, A/B)
+    int32_t bpc, depth;  // dm_knobs: workgroups per CU, ring depth (0 = defaults)
     Rng rng;
     uint64_t thr_ind;
     double alpha, mu, sigma, w0;
@@ -311,8 +311,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     double y0[D][4], y1[D][4];
 #pragma unroll
     for (int ch = 0; ch < D; ++ch) {
-        L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch], a.ntload);
-        L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch], a.ntload);
+        L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch]);
+        L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch]);
     }
     for (; p < npairs; p += nw) {
         const bool more = p + nw < npairs;
@@ -343,11 +343,11 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
             {
                 const int ca = ch + D;
                 if (ca < NCH) {
-                    L::load(r0, ca, lane, dim, y0[ch % D], a.ntload);
-                    L::load(r1, ca, lane, dim, y1[ch % D], a.ntload);
+                    L::load(r0, ca, lane, dim, y0[ch % D]);
+                    L::load(r1, ca, lane, dim, y1[ch % D]);
                 } else if (more) {
-                    L::load(n0, ca - NCH, lane, dim, y0[ch % D], a.ntload);
-                    L::load(n1, ca - NCH, lane, dim, y1[ch % D], a.ntload);
+                    L::load(n0, ca - NCH, lane, dim, y0[ch % D]);
+                    L::load(n1, ca - NCH, lane, dim, y1[ch % D]);
                 }
             }
             const uint32_t slot = (uint32_t)((ch << 6) + lane);  // gene_slot of this lane's genes
@@ -478,9 +478,9 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
 // Persistent grid: as many 256-thread workgroups as stay resident on every CU
 // (occupancy API, capped at 6: the admission limit for ~106 SGPRs on gfx950,
 // MI355X_MICROARCH.md §Residency), never more than one wave per pair.
-// DM_PIPE_BPC overrides the per-CU count (A/B experiments).
+// bpc > 0 (dm_knobs, DM_PIPE_BPC) overrides the per-CU count (A/B experiments).
 template <typename K>
-dim3 pipe_grid(K kern, int num_cus, int64_t npairs) {
+dim3 pipe_grid(K kern, int num_cus, int64_t npairs, int bpc) {
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1)
         occ = 1;
@@ -490,21 +490,20 @@ dim3 pipe_grid(K kern, int num_cus, int64_t npairs) {
     // 32/CU 3.10; 48-64/CU 2.88; 128/CU 2.95; one pair per wave 4.84;
     // r01s on a slower box: 32/CU 3.31 ms, 64/CU 3.25)
     occ = 64;
-    if (const char* bpc = std::getenv("DM_PIPE_BPC")) occ = std::max(1, atoi(bpc));
+    if (bpc > 0) occ = bpc;
     const int64_t blocks = std::min<int64_t>((npairs + 3) / 4, (int64_t)num_cus * occ);
     return dim3((unsigned)std::max<int64_t>(blocks, 1));
 }
 template <typename T, int NCH, int CX, int MUT, int EC>
 void launch_pipe_k(const PipeArgs& a, int num_cus, hipStream_t s) {
-    // DM_PIPE_DEPTH=4 (runtime, A/B): whole 1000-gene rows in flight
-    const char* dep = std::getenv("DM_PIPE_DEPTH");
-    if (NCH == 4 && dep && atoi(dep) == 4) {
+    // depth 4 (dm_knobs, DM_PIPE_DEPTH=4, A/B): whole 1000-gene rows in flight
+    if (NCH == 4 && a.depth == 4) {
         auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC, 4>;
-        kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a);
+        kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2, a.bpc), 256, 0, s>>>(a);
         return;
     }
     auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC>;
-    kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2), 256, 0, s>>>(a);
+    kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2, a.bpc), 256, 0, s>>>(a);
 }
 template <typename T, int NCH, int CX, int MUT>
 void launch_pipe_e(const PipeArgs& a, int ec, int num_cus, hipStream_t s) {
@@ -538,11 +537,6 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 // Decisions of every pair (thread per pair), generation_pipe_f64.hip.
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
-// plan + stream form of the fused kernel (same children): plans of
-// gen_bits_split_bytes(a) bytes
-size_t gen_bits_split_bytes(const GenArgs& a);
-void launch_gen_bits_split(const GenArgs& a, bool eval, void* plans, long long* spread,
-                           hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,

@@ -214,7 +214,10 @@ __global__ __launch_bounds__(256) void fit_key_kernel(const double* __restrict__
         if (i < n && valid[i]) {
             const double v = wv[i];
             const double q = rint(v / scale);
-            if (fabs(q) <= 32767.0 && q * scale == v) k[j] = (int16_t)q;
+            // -0.0 (a zero count under a negative weight) has no key: the
+            // rebuild q * |w0| would give +0.0, and clones keep -0.0
+            if (fabs(q) <= 32767.0 && q * scale == v && !(v == 0.0 && signbit(v)))
+                k[j] = (int16_t)q;
         }
     }
     if (i0 + 3 < n) {
@@ -469,7 +472,7 @@ __device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, i
 #define DM_BITS_MINW 1  // minimum waves per SIMD the fused kernel is compiled for (A/B)
 #endif
 
-template <int PP, int CX, int MUT, bool EVAL, bool TOURN, bool PERSIST>
+template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenArgs a,
                                                                            long long* spread) {
     static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
@@ -479,37 +482,15 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t ngroups = (npairs + PP - 1) / PP;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int evals = 0;
-    if (!PERSIST && grp < ngroups) {  // one group per wave
+    if (grp < ngroups) {  // one group per wave
         BitsGroup<PP> g;
         const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
         bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
             flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
         evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
-    } else if (PERSIST && grp < ngroups) {
-        // software pipeline over the wave's groups (one group when the grid
-        // covers them all): the next group's Philox draws and fitness loads
-        // are issued while this group's parent rows are in flight
-        BitsGroup<PP> g;
-        {
-            const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
-            bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
-        }
-        while (true) {
-            const int64_t nxt = grp + nw;
-            const bool more = nxt < ngroups;
-            BitsDraw dn{};
-            if (more) dn = bits_draw<PP, CX, MUT, TOURN>(a, nxt * PP, lane);
-            if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
-                flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
-            evals += bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
-            if (!more) break;
-            bits_resolve<PP, TOURN>(a, dn, nxt * PP, lane, g);
-            grp = nxt;
-        }
     }
     if (EVAL && spread) {  // nevals: workgroup count, folded by the last workgroup
         __shared__ int32_t wave_evals[4];
@@ -522,161 +503,19 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
 }
 
 
-// ---------------------------------------------------------------------------
-// Two-launch form (DM_BITS_SPLIT): bits_plan_kernel runs the decision chain of
-// every group (the same bits_draw / tournament as the fused kernel: identical
-// children) and writes a 128-B plan per group; bits_stream_kernel then starts
-// each wave with one coalesced plan load and issues its parent rows right
-// away, so no wave of the streaming kernel waits on Philox, the aspirants'
-// fitness loads and the tournament shuffles.
-// ---------------------------------------------------------------------------
-struct BitsPlan {
-    int32_t k[16];    // winner of child c (parent row)
-    uint32_t cut[8];  // cxTwoPoint cuts of pair q (cp1 | cp2 << 16)
-    uint32_t cxf;     // bit q: pair q crosses
-    uint32_t mut;     // bit c: child c mutates
-    uint32_t pad[6];
-};
-static_assert(sizeof(BitsPlan) == 128, "one 128-B line per group");
-
-template <int PP, int CX, int MUT, bool TOURN>
-__global__ __launch_bounds__(256) void bits_plan_kernel(GenArgs a, BitsPlan* __restrict__ plans) {
-    constexpr int NCH = 2 * PP;
-    constexpr int CXL = 32, MUTL = 32 + 2 * PP;
-    const int lane = threadIdx.x & 63;
-    const int64_t npairs = (a.nc + 1) / 2;
-    const int64_t ngroups = (npairs + PP - 1) / PP;
-    const int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (grp >= ngroups) return;
-    const int64_t p0 = grp * PP;
-    const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, p0, lane);
-    int32_t k;
-    double f;
-    bits_tournament<PP, TOURN>(d, TOURN ? a.tournsize : 1, lane, k, f);
-    const uint32_t cxf = (uint32_t)(__ballot(d.cxf_l != 0) >> CXL) & ((1u << PP) - 1);
-    const uint32_t mut = (uint32_t)(__ballot(d.mut_l) >> MUTL) & ((1u << NCH) - 1);
-    BitsPlan* pl = plans + grp;
-    if (lane < NCH) pl->k[lane] = k;
-    if (lane >= CXL && lane < CXL + PP) pl->cut[lane - CXL] = d.cuts;
-    if (lane == 0) {
-        pl->cxf = cxf;
-        pl->mut = mut;
-    }
-}
-
-template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
-__global__ __launch_bounds__(256, DM_BITS_MINW) void bits_stream_kernel(
-    GenArgs a, const BitsPlan* __restrict__ plans, long long* spread) {
-    constexpr int NCH = 2 * PP;
-    __shared__ uint64_t flip_lds_all[4 * (FLIP_SLOTS + 1) * 64];
-    uint64_t* flip_lds = flip_lds_all + (threadIdx.x >> 6) * ((FLIP_SLOTS + 1) * 64);
-    const int lane = threadIdx.x & 63;
-    const int64_t npairs = (a.nc + 1) / 2;
-    const int64_t ngroups = (npairs + PP - 1) / PP;
-    const int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    int evals = 0;
-    if (grp < ngroups) {
-        const uint32_t w = lane < 32 ? reinterpret_cast<const uint32_t*>(plans + grp)[lane] : 0u;
-        BitsGroup<PP> g;
-        g.p0 = grp * PP;
-        const uint32_t cxf = (uint32_t)__builtin_amdgcn_readlane((int)w, 24);
-        g.mut_bits = (uint32_t)__builtin_amdgcn_readlane((int)w, 25);
-        const bool lw = lane < a.words64;
-#pragma unroll
-        for (int q = 0; q < PP; ++q) {
-            g.s0[q] = __builtin_amdgcn_readlane((int)w, 2 * q);
-            g.s1[q] = __builtin_amdgcn_readlane((int)w, 2 * q + 1);
-            g.cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)w, 16 + q);
-            g.cxf[q] = (cxf >> q) & 1u;
-            g.y0[q] = 0;
-            g.y1[q] = 0;
-            if (lw && g.p0 + q < npairs) {
-                const uint64_t* r0 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s0[q] * a.pstride);
-                const uint64_t* r1 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s1[q] * a.pstride);
-                g.y0[q] = r0[lane];
-                if (2 * (g.p0 + q) + 1 < a.nc) g.y1[q] = r1[lane];
-            }
-        }
-        // child lanes: the clone's inherited fitness and validity (the
-        // winner's; loaded only where the child is not varied, or when nothing
-        // is evaluated), off the row loads' path
-        const int ch = lane % NCH;
-        const bool live = lane < NCH && 2 * g.p0 + ch < a.nc;
-        const int32_t k = (int32_t)w;
-        g.cx_c = ((cxf >> (ch >> 1)) & 1u) != 0;
-        g.mut = live && ((g.mut_bits >> ch) & 1u);
-        g.f = 0.0;
-        g.v = 1;
-        if (live && (!EVAL || !(g.cx_c || g.mut))) g.f = parent_fit(a, k);
-        if (live && !(g.cx_c || g.mut))
-            g.v = (a.pkeys && a.pkeys[k] != FIT_KEY_NONE) ? 1u : a.pvalid[k];
-        if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
-            flip_rows_to_lds<NCH>(a, 2 * g.p0, g.mut_bits, lane, flip_lds);
-        evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
-    }
-    if (EVAL && spread) {
-        __shared__ int32_t wave_evals[4];
-        if (lane == 0) wave_evals[threadIdx.x >> 6] = evals;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            evals_fold(spread, a.nevals,
-                       (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
-    }
-}
-
-template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
-static void launch_bs(const GenArgs& a, void* plans, long long* wg, hipStream_t s) {
-    const int64_t waves = ((a.nc + 1) / 2 + PP - 1) / PP;
-    const dim3 grid((unsigned)((waves + 3) / 4));
-    bits_plan_kernel<PP, CX, MUT, TOURN><<<grid, 256, 0, s>>>(a, (BitsPlan*)plans);
-    bits_stream_kernel<PP, CX, MUT, EVAL, TOURN><<<grid, 256, 0, s>>>(a, (const BitsPlan*)plans, wg);
-}
-template <int PP, int CX, int MUT>
-static void launch_bs_e(const GenArgs& a, bool eval, void* plans, long long* wg, hipStream_t s) {
-    const bool tourn = a.sel == DM_SEL_TOURNAMENT;
-    if (eval)
-        tourn ? launch_bs<PP, CX, MUT, true, true>(a, plans, wg, s)
-              : launch_bs<PP, CX, MUT, true, false>(a, plans, wg, s);
-    else
-        tourn ? launch_bs<PP, CX, MUT, false, true>(a, plans, wg, s)
-              : launch_bs<PP, CX, MUT, false, false>(a, plans, wg, s);
-}
-template <int PP>
-static void launch_bs_pp(const GenArgs& a, bool eval, void* plans, long long* wg, hipStream_t s) {
-    const bool mf = a.mut == DM_MUT_FLIPBIT;
-    if (a.cx == DM_CX_TWOPOINT)
-        mf ? launch_bs_e<PP, DM_CX_TWOPOINT, DM_MUT_FLIPBIT>(a, eval, plans, wg, s)
-           : launch_bs_e<PP, DM_CX_TWOPOINT, DM_MUT_NONE>(a, eval, plans, wg, s);
-    else
-        mf ? launch_bs_e<PP, DM_CX_NONE, DM_MUT_FLIPBIT>(a, eval, plans, wg, s)
-           : launch_bs_e<PP, DM_CX_NONE, DM_MUT_NONE>(a, eval, plans, wg, s);
-}
-
 // 8 pairs per wave (ONE Philox call per lane draws every decision of the
 // wave: 16 children x 2 selection calls, 8 x 2 crossover calls, 16 mutation
 // flags) when t <= 4; 4 pairs per wave for 4 < t <= 8.
 static int fused_pp(const GenArgs& a) {
-    return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) && !std::getenv("DM_BITS_PP4") ? 8 : 4;
+    return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) && !a.pp4 ? 8 : 4;
 }
 
-// Grid: one wave per group (one-shot) unless DM_BITS_BPC caps the
-// workgroups per CU (persistent, software-pipelined).
+// One-shot grid: one wave per group.
 template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 static void launch_bf(const GenArgs& a, long long* wg, hipStream_t s) {
     const int64_t waves = ((a.nc + 1) / 2 + PP - 1) / PP;
-    int64_t blocks = (waves + 3) / 4;
-    static const int bpc = std::getenv("DM_BITS_BPC") ? std::max(1, atoi(std::getenv("DM_BITS_BPC"))) : 0;
-    if (bpc) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess)
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        blocks = std::min<int64_t>(blocks, (int64_t)cus * bpc);
-        gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, true>
-            <<<dim3((unsigned)blocks), 256, 0, s>>>(a, wg);
-        return;
-    }
-    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, false>
-        <<<dim3((unsigned)blocks), 256, 0, s>>>(a, wg);
+    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN><<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(
+        a, wg);
 }
 template <int PP, int CX, int MUT>
 static void launch_bf_e(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {
@@ -707,19 +546,6 @@ void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipSt
         launch_bf_pp<8>(a, eval, wg, s);
     else
         launch_bf_pp<4>(a, eval, wg, s);
-}
-
-size_t gen_bits_split_bytes(const GenArgs& a) {
-    const int pp = fused_pp(a);
-    return (size_t)(((a.nc + 1) / 2 + pp - 1) / pp) * sizeof(BitsPlan);
-}
-void launch_gen_bits_split(const GenArgs& a, bool eval, void* plans, long long* spread,
-                           hipStream_t s) {
-    long long* wg = (eval && a.nevals) ? spread : nullptr;
-    if (fused_pp(a) == 8)
-        launch_bs_pp<8>(a, eval, plans, wg, s);
-    else
-        launch_bs_pp<4>(a, eval, plans, wg, s);
 }
 
 template <int CX, int MUT, bool EVAL>

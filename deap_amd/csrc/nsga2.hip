@@ -35,7 +35,7 @@ int fast_dom_build(dm_ctx* ctx, const double* wv, int m, int64_t n,
                    const double* ufit, int64_t U, uint64_t* D, int32_t* count, char* ws);
 int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, const int32_t* ui,
                    const int32_t* order, int64_t T, int32_t* rk);
-bool fast_table_peel(int m);
+bool fast_table_peel(const dm_ctx* ctx, int m);
 int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, const int32_t* F0,
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
@@ -565,8 +565,9 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     // populations hold near-clones equal in objective 0 and a few ulps apart
     // in the others: the full redo cost 24 radix passes per selection.)
     int32_t* tieflag = small + 6;
-    static const bool full_lex = std::getenv("DM_LEX_FULL") != nullptr;
-    const bool quick = m > 1 && !full_lex;
+    const bool full_lex = ctx->knobs.lex_full;
+    // the in-place run sort keys objectives 1..3 (LexRest): up to 4 objectives
+    const bool quick = m > 1 && m <= 4 && !full_lex;
     int rc;
     DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
     auto group = [&](int nlex) -> int {
@@ -595,10 +596,10 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     }
     const int64_t U = hostv[0];
     const bool has_nan = hostv[2] != 0;
-    // integer ranks + symmetric tiles + device-driven peel (dominance.hip);
-    // DM_DOM_LDS / DM_DOM_BALLOT select the fp64 kernels (cross-checks)
-    const bool fast = m >= 2 && m <= 4 && !has_nan && !std::getenv("DM_DOM_LDS") &&
-                      !std::getenv("DM_DOM_BALLOT");
+    // integer ranks + bitset tables + device-driven peel (dominance.hip);
+    // the cross-check paths DM_DOM_LDS / DM_DOM_BALLOT select the fp64 kernels
+    const bool fast = m >= 2 && m <= 4 && !has_nan && ctx->dom_path != DM_DOM_LDS &&
+                      ctx->dom_path != DM_DOM_BALLOT;
     const int64_t W = (U + 63) / 64;
     const int64_t tiles = (W + PEEL_WORDS - 1) / PEEL_WORDS;
     const double dbytes = (double)U * (double)W * 8.0;
@@ -626,7 +627,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         return DM_ERR_INVALID;
     }
     uint64_t* D = (uint64_t*)scratch_slot(
-        ctx, 1, fast ? (fast_table_peel(m) ? 256 : (size_t)fast_dom_words(U) * 8) : (size_t)U * W * 8);
+        ctx, 1, fast ? (fast_table_peel(ctx, m) ? 256 : (size_t)fast_dom_words(U) * 8) : (size_t)U * W * 8);
     if (!D) return DM_ERR_NOMEM;
     char* fwork = nullptr;  // fast path workspace (dominance.hip)
     if (fast) {
@@ -642,7 +643,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         if ((rc = fast_dom_build(ctx, wv, m, n, perm, segin, uidx, ufit, U, D, count,
                                  fwork)))
             return rc;
-    } else if (m >= 2 && m <= 4 && !std::getenv("DM_DOM_LDS")) {
+    } else if (m >= 2 && m <= 4 && ctx->dom_path != DM_DOM_LDS) {
         const int64_t ngroups = (W + DB_WPW - 1) / DB_WPW;
         int32_t* cpart = (int32_t*)scratch_slot(ctx, 4, (size_t)ngroups * U * 4);
         if (!cpart) return DM_ERR_NOMEM;
@@ -747,7 +748,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     }
     res->U = U;
     res->rank_keys = false;
-    if (rank_keys && fast && !std::getenv("DM_CROWD_FP")) {
+    if (rank_keys && fast) {
         if ((rc = fast_rank_keys(ctx, fwork, n, U, m, ui, order, sorted_inds, rank_keys)))
             return rc;
         res->rank_keys = true;
@@ -908,6 +909,102 @@ __global__ void crowd_desc_key_kernel(const double* crowd, const int32_t* vals, 
     GRID_LOOP(j, T) keys[j] = ~ordered_key(crowd[vals[j]]);
 }
 
+// selNSGA2's choice from sorted fronts (emo.py:38-48): the fronts before the
+// last one whole, then the last front (its L individuals at the end of
+// order[0, T)) by decreasing crowding distance, stable (sorted(...,
+// reverse=True) keeps equal distances in front order).
+static int take_chosen(dm_ctx* ctx, const int32_t* order, const SortResult& r, int64_t k,
+                       const double* crowd, int32_t* out_idx) {
+    const int64_t chosen = r.nfronts > 0 ? r.nsorted - r.last_inds : 0;
+    if (chosen > 0)
+        DM_HIP(hipMemcpyAsync(out_idx, order, (size_t)std::min(chosen, k) * 4,
+                              hipMemcpyDeviceToDevice, ctx->stream));
+    const int64_t rem = k - chosen;
+    if (rem > 0 && r.nfronts > 0) {
+        const int64_t L = r.last_inds;  // last front size
+        char* base = (char*)scratch(ctx, 2 * align_up((size_t)L * 8, 256) +
+                                             2 * align_up((size_t)L * 4, 256) +
+                                             radix_sort_temp_bytes(L) + 4096);
+        if (!base) return DM_ERR_NOMEM;
+        Bump bp{base};
+        uint64_t* keys = bp.take<uint64_t>(L);
+        uint64_t* ktmp = bp.take<uint64_t>(L);
+        int32_t* vals = bp.take<int32_t>(L);
+        int32_t* vtmp = bp.take<int32_t>(L);
+        void* rtemp = bp.take<char>(radix_sort_temp_bytes(L));
+        DM_HIP(hipMemcpyAsync(vals, order + chosen, (size_t)L * 4, hipMemcpyDeviceToDevice,
+                              ctx->stream));
+        crowd_desc_key_kernel<<<g1(L), 256, 0, ctx->stream>>>(crowd, vals, keys, L);
+        int rc = radix_sort_pairs(ctx->stream, keys, vals, ktmp, vtmp, L, 0, 64, rtemp);
+        if (rc) return rc;
+        DM_HIP(hipMemcpyAsync(out_idx + chosen, vals, (size_t)std::min(rem, L) * 4,
+                              hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// sortLogNondominated order (emo.py:246-276).  Fortin's sort computes the
+// same Pareto ranks as the standard one, so the ranks come
+// from sort_nondominated_impl; the log version's fronts list the unique
+// fitnesses in ``fitnesses.sort(reverse=True)`` order (descending
+// lexicographic wvalues, emo.py:257) and each one's individuals in population
+// order (``unique_fits[...].append``, emo.py:249-250): a stable descending
+// lexicographic sort of the rows (ties = equal fitnesses keep index order),
+// then a stable sort by rank (rows outside the emitted fronts last).
+// ---------------------------------------------------------------------------
+__global__ void log_rank_key_kernel(const int32_t* rank, const int32_t* perm, int64_t n,
+                                    uint64_t unsorted, uint64_t* keys) {
+    GRID_LOOP(j, n) {
+        const int32_t r = rank[perm[j]];
+        keys[j] = r < 0 ? unsorted : (uint64_t)(uint32_t)r;
+    }
+}
+__global__ void log_front_start_kernel(const uint64_t* keys, int64_t T, int32_t nf,
+                                       int32_t* fstart) {
+    GRID_LOOP(j, T) {
+        if (j == 0 || keys[j] != keys[j - 1]) fstart[keys[j]] = (int32_t)j;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) fstart[nf] = (int32_t)T;
+}
+
+// order [n] / fstart [n + 1]: device outputs, not in scratch slots 0, 1, 3, 4.
+static int log_sort_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, bool first_only,
+                         int32_t* order, int32_t* fstart, SortResult* res) {
+    hipStream_t s = ctx->stream;
+    const int64_t n = pop->n;
+    int32_t* w = (int32_t*)scratch_slot(ctx, 3, (size_t)(3 * n + 4) * 4);
+    if (!w) return DM_ERR_NOMEM;
+    int32_t* rank = w;
+    int32_t* perm = w + n;
+    int32_t* std_fstart = w + 2 * n;  // the standard front starts (unused)
+    int rc = sort_nondominated_impl(ctx, pop, k, first_only, order, std_fstart, rank, res);
+    if (rc) return rc;
+    if ((rc = sort_by_fitness(ctx, pop->wvalues, pop->nobj, n, true, perm))) return rc;
+    const size_t kb = align_up((size_t)n * 8, 256), vb = align_up((size_t)n * 4, 256);
+    char* t = (char*)scratch(ctx, 2 * kb + vb + radix_sort_temp_bytes(n));
+    if (!t) return DM_ERR_NOMEM;
+    uint64_t* keys = (uint64_t*)t;
+    uint64_t* ktmp = (uint64_t*)(t + kb);
+    int32_t* vtmp = (int32_t*)(t + 2 * kb);
+    void* rtemp = t + 2 * kb + vb;
+    int bits = 8;
+    while (bits < 32 && (1ll << bits) <= (int64_t)res->nfronts) bits += 8;
+    log_rank_key_kernel<<<g1(n), 256, 0, s>>>(rank, perm, n, (1ull << bits) - 1, keys);
+    if ((rc = radix_sort_pairs(s, keys, perm, ktmp, vtmp, n, 0, bits, rtemp))) return rc;
+    const int64_t T = res->nsorted;
+    if (T > 0) DM_HIP(hipMemcpyAsync(order, perm, (size_t)T * 4, hipMemcpyDeviceToDevice, s));
+    log_front_start_kernel<<<g1(std::max<int64_t>(T, 1)), 256, 0, s>>>(keys, T, res->nfronts,
+                                                                      fstart);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+__global__ void gather_f64_kernel(const double* src, const int32_t* idx, int64_t n, double* dst) {
+    GRID_LOOP(i, n) dst[i] = src[idx[i]];
+}
+
 }  // namespace dm
 
 using namespace dm;
@@ -924,6 +1021,27 @@ extern "C" int dm_sort_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
     SortResult r;
     rc = sort_nondominated_impl(ctx, pop, k, first_front_only != 0, order, front_start, rank, &r);
     if (rc) return rc;
+    *nsorted = r.nsorted;
+    *nfronts = r.nfronts;
+    return DM_OK;
+}
+
+extern "C" int dm_sort_log_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
+                                        int32_t first_front_only, int32_t* order,
+                                        int32_t* front_start, int64_t* nsorted,
+                                        int32_t* nfronts) {
+    DM_CHECK_ARG(ctx && order && front_start && nsorted && nfronts, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0, "negative k");
+    DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    *nsorted = 0;
+    *nfronts = 0;
+    if (pop->n == 0 || k == 0) return DM_OK;
+    SortResult r;
+    rc = log_sort_impl(ctx, pop, k, first_front_only != 0, order, front_start, &r);
+    if (rc) return rc;
+    DM_HIP(hipStreamSynchronize(ctx->stream));
     *nsorted = r.nsorted;
     *nfronts = r.nfronts;
     return DM_OK;
@@ -964,33 +1082,35 @@ extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weight
     rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd,
                        r.rank_keys ? rkeys : nullptr, r.U);
     if (rc) return rc;
-    // fronts before the last one are taken whole (emo.py:38-40); the sort
-    // reports the emitted individuals and the last front's size on the host
-    const int64_t chosen = r.nfronts > 0 ? r.nsorted - r.last_inds : 0;
-    if (chosen > 0)
-        DM_HIP(hipMemcpyAsync(out_idx, order, (size_t)std::min(chosen, k) * 4,
-                              hipMemcpyDeviceToDevice, ctx->stream));
-    const int64_t rem = k - chosen;
-    if (rem > 0 && r.nfronts > 0) {
-        const int64_t L = r.last_inds;  // last front size
-        char* base = (char*)scratch(ctx, 2 * align_up((size_t)L * 8, 256) +
-                                             2 * align_up((size_t)L * 4, 256) +
-                                             radix_sort_temp_bytes(L) + 4096);
-        if (!base) return DM_ERR_NOMEM;
-        Bump bp{base};
-        uint64_t* keys = bp.take<uint64_t>(L);
-        uint64_t* ktmp = bp.take<uint64_t>(L);
-        int32_t* vals = bp.take<int32_t>(L);
-        int32_t* vtmp = bp.take<int32_t>(L);
-        void* rtemp = bp.take<char>(radix_sort_temp_bytes(L));
-        DM_HIP(hipMemcpyAsync(vals, order + chosen, (size_t)L * 4, hipMemcpyDeviceToDevice,
-                              ctx->stream));
-        crowd_desc_key_kernel<<<g1(L), 256, 0, ctx->stream>>>(crowd, vals, keys, L);
-        rc = radix_sort_pairs(ctx->stream, keys, vals, ktmp, vtmp, L, 0, 64, rtemp);
-        if (rc) return rc;
-        DM_HIP(hipMemcpyAsync(out_idx + chosen, vals, (size_t)std::min(rem, L) * 4,
-                              hipMemcpyDeviceToDevice, ctx->stream));
-    }
+    return take_chosen(ctx, order, r, k, crowd, out_idx);
+}
+
+extern "C" int dm_sel_nsga2_log(dm_ctx* ctx, const dm_pop* pop, const double* weights, int64_t k,
+                                int32_t* out_idx, double* crowd) {
+    DM_CHECK_ARG(ctx && pop && weights && out_idx && crowd, "null argument");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    DM_CHECK_ARG(k >= 0, "negative k");
+    DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
+    const int64_t n = pop->n;
+    if (n == 0 || k == 0) return DM_OK;
+    int32_t* order = (int32_t*)scratch_slot(ctx, 2, (size_t)(2 * n + 2) * 4);
+    if (!order) return DM_ERR_NOMEM;
+    int32_t* fstart = order + n;
+    SortResult r;
+    if ((rc = log_sort_impl(ctx, pop, k, false, order, fstart, &r))) return rc;
+    // crowding on every front in its log order (emo.py:41-42)
+    rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd);
+    if (rc) return rc;
+    return take_chosen(ctx, order, r, k, crowd, out_idx);
+}
+
+extern "C" int dm_gather_f64(dm_ctx* ctx, const double* src, const int32_t* idx, int64_t n,
+                             double* dst) {
+    DM_CHECK_ARG(ctx && (n == 0 || (src && idx && dst)), "null argument");
+    DM_CHECK_ARG(n >= 0, "negative n");
+    if (n == 0) return DM_OK;
+    gather_f64_kernel<<<g1(n), 256, 0, ctx->stream>>>(src, idx, n, dst);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

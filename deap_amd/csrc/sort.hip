@@ -709,7 +709,7 @@ static int sel_sorted(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_id
     DM_CHECK_ARG(pop->n < (1ll << 31), "population too large");
     // small k of a single objective (migRing emigrants, HallOfFame candidates)
     if (pop->nobj == 1 && k <= TOPK_MAX && pop->n > 4 * k &&
-        !std::getenv("DM_SELBEST_FULLSORT"))
+        !ctx->knobs.selbest_fullsort)
         return sel_topk(ctx, pop, k, out_idx, best);
     int32_t* full = out_idx;
     if (k < pop->n) {

@@ -15,6 +15,7 @@ The buffers are PyTorch tensors (buffer ownership only); every computation on
 them goes through ``libdeapmi.so``.
 """
 import array as _array
+import contextlib
 import ctypes
 
 import numpy as np
@@ -95,6 +96,20 @@ class Context:
 
     def sync(self):
         _lib.check(_lib.load().dm_ctx_sync(self.handle), "dm_ctx_sync")
+
+
+@contextlib.contextmanager
+def dominance_path(name, device=None):
+    """Run sortNondominated / selNSGA2 on one of the library's cross-check
+    dominance paths (``"compare"``, ``"peel_d"``, ``"ballot"``, ``"lds"``;
+    ``"default"`` is the product path) inside the block -- test and
+    measurement use: every path gives the same fronts."""
+    ctx = Context.get(device)
+    _lib.call("dm_ctx_set_dom_path", ctx.handle, _lib.DM_DOM_PATHS[name])
+    try:
+        yield
+    finally:
+        _lib.call("dm_ctx_set_dom_path", ctx.handle, 0)
 
 
 def gtype_of(individual_class=None, typecode=None, gtype=None):

@@ -124,29 +124,26 @@ class _SelNSGA2(DeviceOperator):
 
 
 def _log_fronts(individuals, k, first_front_only):
-    """Fronts in sortLogNondominated's order (emo.py:246-276): the Pareto ranks
-    come from the device sort (Fortin et al.'s divide and conquer computes the
-    same ranks); inside a front the unique fitnesses follow
-    ``fitnesses.sort(reverse=True)`` (lexicographic wvalues, descending) and
-    equal fitnesses keep population order (``unique_fits[...].append``).
-    Ordering: stable device sorts, last objective first, then by rank."""
+    """Fronts in sortLogNondominated's order (emo.py:246-276), ordered in the
+    library (dm_sort_log_nondominated): the Pareto ranks of the device sort
+    (Fortin et al.'s divide and conquer computes the same ranks); inside a
+    front the unique fitnesses follow ``fitnesses.sort(reverse=True)``
+    (lexicographic wvalues, descending) and equal fitnesses keep population
+    order (``unique_fits[...].append``)."""
     torch = _torch()
     n = len(individuals)
-    _order, _fstart, rank, _ns, nf = _sort(individuals, k, first_front_only)
-    r = rank[:n].long()
-    perm = torch.nonzero(r >= 0).flatten()  # ascending row index
-    wv = individuals.wvalues[:n].reshape(n, individuals.nobj)
-    for j in reversed(range(individuals.nobj)):
-        _, o = torch.sort(wv[perm, j], descending=True, stable=True)
-        perm = perm[o]
-    _, o = torch.sort(r[perm], stable=True)
-    perm = perm[o].to(torch.int32)
-    counts = torch.bincount(r[perm.long()], minlength=nf)[:nf].cpu().tolist()
-    fronts, at = [], 0
-    for c in counts:
-        fronts.append(perm[at:at + c])
-        at += c
-    return fronts
+    dev = individuals.device
+    order = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
+    fstart = torch.empty((max(n, 1) + 1,), dtype=torch.int32, device=dev)
+    nsorted = ctypes.c_int64(0)
+    nfronts = ctypes.c_int32(0)
+    ctx = individuals.ctx.bind()
+    _lib.call("dm_sort_log_nondominated", ctx, ctypes.byref(individuals.c_pop()), int(k),
+              int(bool(first_front_only)), ctypes.c_void_p(order.data_ptr()),
+              ctypes.c_void_p(fstart.data_ptr()), ctypes.byref(nsorted), ctypes.byref(nfronts))
+    nf = nfronts.value
+    bounds = fstart[: nf + 1].cpu().tolist()
+    return [order[bounds[f]:bounds[f + 1]] for f in range(nf)]
 
 
 class _SortLogNondominated(DeviceOperator):
@@ -163,21 +160,23 @@ class _SortLogNondominated(DeviceOperator):
 
 
 def _sel_nsga2_log(individuals, k):
-    """selNSGA2(nd='log') (emo.py:15-50 over sortLogNondominated): crowding on
-    every front in its log order, all fronts but the last, then the last one
-    by decreasing crowding distance (stable, as ``sorted(..., reverse=True)``)."""
+    """selNSGA2(nd='log') (emo.py:15-50 over sortLogNondominated), in the
+    library (dm_sel_nsga2_log): crowding on every front in its log order, all
+    fronts but the last, then the last one by decreasing crowding distance
+    (stable, as ``sorted(..., reverse=True)``)."""
     torch = _torch()
-    if k == 0 or len(individuals) == 0:
-        return torch.empty((0,), dtype=torch.int32, device=individuals.device)
-    fronts = _log_fronts(individuals, k, False)
-    crowd = assignCrowdingDist(individuals, fronts)
-    chosen = fronts[:-1]
-    rest = k - sum(len(f) for f in chosen)
-    if rest > 0:
-        last = fronts[-1]
-        _, o = torch.sort(crowd[last.long()], descending=True, stable=True)
-        chosen = chosen + [last[o][:rest]]
-    return torch.cat(chosen) if chosen else fronts[0][:0]
+    n = len(individuals)
+    out = torch.empty((max(k, 1),), dtype=torch.int32, device=individuals.device)
+    if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
+        individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
+                                                device=individuals.device)
+    if k == 0 or n == 0:
+        return out[:0]
+    ctx = individuals.ctx.bind()
+    _lib.call("dm_sel_nsga2_log", ctx, ctypes.byref(individuals.c_pop()), _weights(individuals),
+              k, ctypes.c_void_p(out.data_ptr()),
+              ctypes.c_void_p(individuals.crowding_dist.data_ptr()))
+    return out[: min(k, n)]
 
 
 class _SelTournamentDCD(DeviceOperator):

@@ -158,6 +158,22 @@ int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count);
  * kernel of dm_sort_nondominated / dm_sel_nsga2). */
 enum dm_time_target { DM_TIME_GENERATION = 0, DM_TIME_DOMINANCE = 1 };
 int dm_ctx_set_timing_target(dm_ctx* ctx, int32_t target);
+/* Dominance path of dm_sort_nondominated / dm_sel_nsga2 (and the log
+ * versions): DM_DOM_DEFAULT (bitset tables + table-fed peel for 2-3
+ * objectives, integer compare kernel + D-matrix peel for 4, fp64 kernels
+ * with NaN or more objectives) or a cross-check path the parity tests
+ * compare the default against.  Every path gives the same fronts. */
+enum dm_dom_path {
+    DM_DOM_DEFAULT = 0,
+    DM_DOM_COMPARE = 1,  /* integer compare kernel + D-matrix peel (2-4 objectives) */
+    DM_DOM_PEEL_D = 2,   /* bitset rows written as D + D-matrix peel (bitset objectives) */
+    DM_DOM_BALLOT = 3,   /* fp64 ballot kernel + peel (2-4 objectives) */
+    DM_DOM_LDS = 4       /* fp64 LDS-tiled kernel + peel (any objectives) */
+};
+int dm_ctx_set_dom_path(dm_ctx* ctx, int32_t path);
+/* 1 when the context's dominance pass for nobj objectives (NaN-free
+ * fitnesses) is the bitset-table pass, else 0 (introspection for tests). */
+int dm_ctx_dom_bitset(dm_ctx* ctx, int32_t nobj);
 
 /* ---- RNG (test + init) ---------------------------------------------------- */
 /* Raw Philox4x32-10 blocks: out[i*4..i*4+3] = philox(ctr_i, key) with
@@ -238,6 +254,24 @@ int dm_crowding_dist(dm_ctx* ctx, const dm_pop* pop, const double* weights,
  * Host-synchronising. */
 int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                  int64_t k, int32_t* out_idx, double* crowd);
+/* sortLogNondominated (emo.py:234-276): the same fronts as
+ * dm_sort_nondominated (Fortin's sort computes the same Pareto ranks) in the
+ * log version's order: inside a front, unique fitnesses by descending
+ * lexicographic wvalues (emo.py:257 fitnesses.sort(reverse=True)), equal
+ * fitnesses in population order (emo.py:249-250).  order [n], front_start
+ * [n+1] as dm_sort_nondominated.  Host-synchronising. */
+int dm_sort_log_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
+                             int32_t first_front_only, int32_t* order,
+                             int32_t* front_start, int64_t* nsorted,
+                             int32_t* nfronts);
+/* selNSGA2(nd='log') (emo.py:15-50 over sortLogNondominated): as
+ * dm_sel_nsga2 with crowding on the log-ordered fronts. */
+int dm_sel_nsga2_log(dm_ctx* ctx, const dm_pop* pop, const double* weights,
+                     int64_t k, int32_t* out_idx, double* crowd);
+/* dst[i] = src[idx[i]] for i < n (fitness.crowding_dist carried with a
+ * selection's clones, algorithms.py:329 select + base.py:252-261). */
+int dm_gather_f64(dm_ctx* ctx, const double* src, const int32_t* idx, int64_t n,
+                  double* dst);
 
 /* selTournamentDCD (emo.py:145-195): out_idx[4*ceil(k/4)] — for every group
  * of four slots, tournaments (P1[i],P1[i+1]), (P1[i+2],P1[i+3]),

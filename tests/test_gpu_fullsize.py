@@ -115,24 +115,23 @@ def _sphere_fitness(n, m, seed):
 
 
 @pytest.mark.parametrize("m", [3, 2])
-def test_sel_nsga2_at_full_size(gpu, monkeypatch, m):
+def test_sel_nsga2_at_full_size(gpu, m):
     """C5 at its benched size (selNSGA2 over 2N = 2^18 DTLZ2-shaped fitnesses
-    -> N = 2^17, deap/tools/emo.py:15-50): the integer-rank lower-triangle
-    dominance + device peel (default) against the fp64 ballot kernel
-    (DM_DOM_BALLOT): the same fronts, chosen indices and crowding distances."""
+    -> N = 2^17, deap/tools/emo.py:15-50): the bitset dominance + table peel
+    (default) against the fp64 ballot kernel (the DM_DOM_BALLOT cross-check
+    path): the same fronts, chosen indices and crowding distances."""
     import torch
     from deap_amd import tools
+    from deap_amd.device import dominance_path
     n = 1 << 18
     wv = -_sphere_fitness(n, m, 100 + m)  # minimisation: weights -1
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=(-1.0,) * m, gtype="f64",
                            wvalues=wv, valid=np.ones(n))
     got = []
-    for env in (None, "DM_DOM_BALLOT"):
-        monkeypatch.delenv("DM_DOM_BALLOT", raising=False)
-        if env:
-            monkeypatch.setenv(env, "1")
-        fronts = [f.cpu().numpy() for f in tools.sortNondominated(pop, n // 2)]
-        chosen = tools.selNSGA2(pop, n // 2).cpu().numpy()
+    for path in ("default", "ballot"):
+        with dominance_path(path):
+            fronts = [f.cpu().numpy() for f in tools.sortNondominated(pop, n // 2)]
+            chosen = tools.selNSGA2(pop, n // 2).cpu().numpy()
         crowd = pop.crowding_dist[:n].cpu().numpy().copy()
         got.append((fronts, chosen, crowd))
     (f0, c0, d0), (f1, c1, d1) = got
@@ -143,7 +142,7 @@ def test_sel_nsga2_at_full_size(gpu, monkeypatch, m):
     torch.cuda.synchronize()
 
 
-def test_sort_nondominated_objective0_ties(gpu, monkeypatch):
+def test_sort_nondominated_objective0_ties(gpu):
     """Objective 0 takes 7 values only (most block pairs straddle a tie, the
     full-compare path), the others are continuous: fast path == LDS kernel."""
     from deap_amd import tools
@@ -154,9 +153,10 @@ def test_sort_nondominated_objective0_ties(gpu, monkeypatch):
     wv[rng.integers(0, n, 500)] = wv[rng.integers(0, n, 500)]  # duplicated fitnesses
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=(1.0, -1.0, 1.0), gtype="f64",
                            wvalues=wv, valid=np.ones(n))
+    from deap_amd.device import dominance_path
     fast = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
-    monkeypatch.setenv("DM_DOM_LDS", "1")
-    ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
+    with dominance_path("lds"):
+        ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)]
     assert fast == ref
     assert sum(len(f) for f in fast) == n
 
@@ -171,27 +171,86 @@ def _shell_fitness(n, m, seed, levels=12):
     return d * (1.0 + 0.02 * rng.integers(0, levels, size=(n, 1)))
 
 
-@pytest.mark.parametrize("n,m,kind", [(1 << 18, 3, "sphere"), (40000, 3, "shells"),
-                                      (40000, 2, "shells")])
+def _dup_shell_fitness(n, m, seed, levels=6):
+    """Shells of ~n/levels unique members each (fronts of ~9,500 unique fits:
+    the table peel splits every chunk's members into 2-4 slices, >= 2 x 2,048
+    members), 5 % of the rows duplicates of other rows (equal fitnesses,
+    emo.py:72-75 grouping)."""
+    rng = np.random.default_rng(seed)
+    wv = _shell_fitness(n, m, seed + 1, levels)
+    wv[rng.integers(0, n, n // 20)] = wv[rng.integers(0, n, n // 20)]
+    return wv
+
+
+def _grid_fitness(n, m, seed):
+    """Directions rounded to a 1/64 grid: duplicated fitnesses and equal
+    crowding distances everywhere (ties at the selNSGA2 cut)."""
+    return np.round(_sphere_fitness(n, m, seed) * 64.0) / 64.0
+
+
+def _port_ranks(wv, fronts):
+    """Pareto rank per unique fit (oracle.nsga2_closed order) from the port's
+    log fronts (the ranks of the Fortin sort, emo.py:234-276); fits beyond
+    the last front get one rank past it."""
+    from oracle import nsga2_closed
+    ufit, ui = nsga2_closed.unique_first_appearance(wv)
+    urank = np.full(len(ufit), len(fronts), np.int64)
+    for r, f in enumerate(fronts):
+        urank[ui[np.asarray(f, np.int64)]] = r
+    return urank, ui
+
+
+def _check_standard_order(pop, wv, weights, k, ref_fronts):
+    """The benched standard path against the closed form (SURVEY §8a-a21,
+    oracle/nsga2_closed.py): every sortNondominated front equal IN ORDER, and
+    the standard selNSGA2 chosen ORDER equal to emo.py:40-48 on those fronts
+    (crowding by oracle.ops, the stable reverse sort of the last front, ties
+    at the cut included); crowding distances bitwise."""
+    from deap_amd import tools
+    from oracle import nsga2_closed
+    urank, ui = _port_ranks(wv, ref_fronts)
+    want = nsga2_closed.sort_nondominated(wv, k, ranks=urank)
+    got = [f.cpu().numpy() for f in tools.sortNondominated(pop, k)]
+    assert [len(f) for f in got] == [len(f) for f in want]
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert np.array_equal(a, b), "front %d differs from the closed form" % i
+    want_c, want_crowd = nsga2_closed.sel_nsga2(wv, weights, k, fronts=want)
+    chosen = tools.selNSGA2(pop, k).cpu().numpy()
+    assert chosen.tolist() == want_c
+    crowd = pop.crowding_dist[:len(wv)].cpu().numpy()
+    assert np.array_equal(crowd[chosen], np.array([want_crowd[i] for i in want_c]))
+    # the unique-fit sizes of the fronts (the table peel's slicing input)
+    return [len(np.unique(ui[f])) for f in want], want, want_crowd
+
+
+@pytest.mark.parametrize("n,m,kind", [(1 << 18, 3, "sphere"), (1 << 18, 2, "sphere"),
+                                      (40000, 3, "shells"), (40000, 2, "shells"),
+                                      (60000, 3, "dupshells"), (60000, 2, "dupshells"),
+                                      (60000, 3, "grid")])
 def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
-    """C5 at its benched size against a reference-pinned restatement (VERDICT r2
-    item 2): ``oracle/deap_port.py``'s Fortin log sort and selNSGA2 (bit-exact
-    with the reference on tests/golden/nsga2*.npz, test_support_port.py) on
-    the same 2N fitnesses (deap/tools/emo.py:15-50, 53-117, 234-276):
+    """C5 at its benched size against reference-pinned restatements (VERDICT
+    r2 item 2, r3 item 1): ``oracle/deap_port.py``'s Fortin log sort and
+    selNSGA2 (bit-exact with the reference on tests/golden/nsga2*.npz,
+    test_support_port.py) and the closed form of the standard order
+    (``oracle/nsga2_closed.py``, checked against oracle.ops and nsga2.npz in
+    test_oracle.py) on the same 2N fitnesses (deap/tools/emo.py:15-117,
+    234-276):
 
     * device ``sortLogNondominated`` fronts == the port's, member for member;
     * device ``selNSGA2(nd='log')`` chosen order == the port's;
-    * every device ``sortNondominated`` front (integer-rank dominance tiles +
-      device peel, the benched path) == the port's front as a set (the ranks
-      are identical; only the order inside a front differs between the two
-      reference sorts);
-    * the standard selNSGA2's crowding distances == the port's, bitwise, and
-      its chosen set == the port's whenever the crowding value at the cut of
-      the last front is not tied across the cut."""
+    * every device ``sortNondominated`` front (bitset dominance + table peel,
+      the benched path) == the closed form IN ORDER, with the ranks of the
+      port's sort;
+    * the standard ``selNSGA2`` chosen order == emo.py:40-48 on those fronts,
+      ties at the cut included, crowding distances bitwise."""
     from deap_amd import tools
     from oracle import deap_port
     k = n // 2
-    wv = -(_sphere_fitness(n, m, 500 + m) if kind == "sphere" else _shell_fitness(n, m, 600 + m))
+    base = {"sphere": lambda: _sphere_fitness(n, m, 500 + m),
+            "shells": lambda: _shell_fitness(n, m, 600 + m),
+            "dupshells": lambda: _dup_shell_fitness(n, m, 700 + m),
+            "grid": lambda: _grid_fitness(n, m, 800 + m)}[kind]
+    wv = -base()
     weights = (-1.0,) * m
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=weights, gtype="f64", wvalues=wv,
                            valid=np.ones(n))
@@ -202,26 +261,64 @@ def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
     ref_fronts = [[row[id(x)] for x in f] for f in ref_fronts]
     ref_chosen = [row[id(x)] for x in ref_chosen]
     ref_crowd = np.array([getattr(x.fitness, "crowding_dist", np.nan) for x in inds])
-    if kind == "shells":
-        assert max(len(f) for f in ref_fronts) > 1024, [len(f) for f in ref_fronts]
     # log sort: exact order
     got_log = [f.cpu().numpy().tolist() for f in tools.sortLogNondominated(pop, k)]
     assert [len(f) for f in got_log] == [len(f) for f in ref_fronts]
     assert got_log == ref_fronts
     assert tools.selNSGA2(pop, k, nd="log").cpu().numpy().tolist() == ref_chosen
-    # standard sort (the benched path): same fronts as sets
-    got_std = [f.cpu().numpy() for f in tools.sortNondominated(pop, k)]
-    assert len(got_std) == len(ref_fronts)
-    for i, (a, b) in enumerate(zip(got_std, ref_fronts)):
-        assert len(a) == len(b) and set(a.tolist()) == set(b), "front %d" % i
-    chosen = tools.selNSGA2(pop, k).cpu().numpy()
-    crowd = pop.crowding_dist[:n].cpu().numpy()
-    assert np.array_equal(crowd[chosen], ref_crowd[chosen])
-    last = np.array(ref_fronts[-1])
-    need = k - sum(len(f) for f in ref_fronts[:-1])
-    cut = np.sort(ref_crowd[last])[::-1]
-    if need < len(last) and cut[need - 1] != cut[need]:
-        assert set(chosen.tolist()) == set(ref_chosen)
+    # standard sort (the benched path): exact order against the closed form
+    usizes, want, want_crowd = _check_standard_order(pop, wv, weights, k, ref_fronts)
+    # crowding of a front depends on its order only through duplicates: the
+    # port's (log-order) distances agree on rows without an equal twin
+    if kind in ("shells", "dupshells"):
+        assert max(usizes) > 2 * 2048, usizes  # the table peel's member slices
+    if kind == "dupshells":
+        assert max(usizes) >= 8192, usizes
+    if kind == "grid":
+        last = want[-1]
+        need = k - sum(len(f) for f in want[:-1])
+        cut = np.sort([want_crowd[i] for i in last.tolist()])[::-1]
+        assert 0 < need < len(last) and cut[need - 1] == cut[need], "no tie at the cut"
+
+
+def test_nsga2_on_an_evolved_c5_population(gpu):
+    """The C5 benched workload itself: 2^17 DTLZ2 (M=3, D=12) individuals after
+    12 eaMuPlusLambda generations on the device (cxBlend of clones leaves
+    near-clones and exact duplicates), plus one varOr batch -> 2N = 2^18
+    (bench.py's stage breakdown input).  The standard sortNondominated /
+    selNSGA2 on the device against the closed form with the port's ranks,
+    every front in order and the chosen order (emo.py:15-117)."""
+    import ctypes
+    from deap_amd import _lib, algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    from oracle import deap_port
+    n, m, dim = 1 << 17, 3, 12
+    stream = RandomStream(1234)
+    pop = tools.initPopulation(n=n, dim=dim, low=0.0, high=1.0, gtype="f64",
+                               weights=(-1.0,) * m, stream=stream)
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.dtlz2, obj=m)
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("mutate", tools.mutGaussian, mu=0, sigma=0.1, indpb=1.0 / dim)
+    tb.register("select", tools.selNSGA2)
+    benchmarks.dtlz2(pop, obj=m)
+    step = algorithms.MuPlusLambdaStep(pop, tb, n, n, 0.6, 0.3)
+    for _ in range(12):
+        step.step(stream)
+    comb = step.combined
+    two = pop.like(2 * n, capacity=2 * n)
+    ctx = comb.ctx.bind()
+    _lib.call("dm_gather", ctx, ctypes.byref(comb.c_pop()), None, ctypes.byref(two.c_pop(0, n)))
+    off = algorithms.varOr(comb, tb, n, 0.6, 0.3, evaluate=True, stream=stream)
+    _lib.call("dm_gather", ctx, ctypes.byref(off.c_pop()), None, ctypes.byref(two.c_pop(n, n)))
+    wv = two.wvalues[:2 * n].cpu().numpy().copy()
+    weights = (-1.0,) * m
+    inds = deap_port.nsga2_population(wv, weights)
+    row = {id(ind): i for i, ind in enumerate(inds)}
+    ref_fronts = [[row[id(x)] for x in f] for f in deap_port.sort_log_nondominated(inds, n)]
+    usizes, want, _ = _check_standard_order(two, wv, weights, n, ref_fronts)
+    assert len(np.unique(wv, axis=0)) < 2 * n  # the population holds duplicates
+    assert len(want) > 5
 
 
 def _row_hashes(pop):

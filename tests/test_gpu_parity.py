@@ -383,7 +383,7 @@ def _near_clone_fitness(rng, m, nbase, long_mixed):
     return wv[rng.permutation(len(wv))]
 
 
-@pytest.mark.parametrize("m", [2, 3, 4])
+@pytest.mark.parametrize("m", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("long_mixed", [False, True])
 def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed):
     """The grouping sorts by objective 0 and then sorts, in place, only the
@@ -391,10 +391,17 @@ def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed):
     (nsga2.hip lex_bad_kernel / lex_run_sort_kernel), falling back to the full
     lexicographic sort for such a run over 64 rows: fronts and selNSGA2 equal
     the oracle (deap/tools/emo.py:15-50, 53-117) exactly on near-clone
-    populations."""
+    populations.  m = 5 and 8: rows tied in objectives 0-3 and out of order
+    only in the later ones (the run sort keys objectives 1-3 only, so those
+    objective counts take the full lexicographic sort)."""
     from deap_amd import tools
     rng = np.random.default_rng(70 + 10 * m + long_mixed)
     wv = _near_clone_fitness(rng, m, 500, long_mixed)
+    if m > 4:  # near-clones that differ only in objectives 4..m-1
+        tail = rng.choice(len(wv), len(wv) // 3, replace=False)
+        wv[tail, 1:4] = wv[tail, 0:1]
+        wv[tail[1::2]] = wv[tail[::2]][:len(tail[1::2])]
+        wv[tail[1::2], 4:] = np.nextafter(wv[tail[1::2], 4:], -1.0)
     n = len(wv)
     w = (-1.0,) * m
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
@@ -428,12 +435,14 @@ def test_sort_nondominated_with_nan_fitness(gpu, m):
 
 
 @pytest.mark.parametrize("m", [2, 3, 4])
-def test_dominance_paths_agree_large(gpu, monkeypatch, m):
-    """At sizes the oracle cannot finish: the integer-rank symmetric dominance
-    with the device-driven peel (default), the fp64 ballot kernel
-    (DM_DOM_BALLOT) and the LDS-tiled kernel (DM_DOM_LDS) give identical
-    fronts and selNSGA2 choices."""
+def test_dominance_paths_agree_large(gpu, m):
+    """At sizes the oracle cannot finish: the default path (bitset tables +
+    table peel for 2-3 objectives, integer compare kernel + D peel for 4) and
+    the cross-check paths (dm_ctx_set_dom_path: integer compare kernel, bitset
+    rows + D peel, fp64 ballot kernel, fp64 LDS kernel) give identical fronts
+    and selNSGA2 choices."""
     from deap_amd import tools
+    from deap_amd.device import dominance_path
     rng = np.random.default_rng(31 + m)
     n = 30011
     wv = np.round(rng.uniform(0, 1, size=(n, m)), 2)  # many equal fitnesses
@@ -441,15 +450,12 @@ def test_dominance_paths_agree_large(gpu, monkeypatch, m):
     pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
                            valid=np.ones(n))
     got = []
-    for env in (None, "DM_DOM_TRI", "DM_DOM_BALLOT", "DM_DOM_LDS", "DM_PEEL_D"):
-        for e in ("DM_DOM_TRI", "DM_DOM_BALLOT", "DM_DOM_LDS", "DM_PEEL_D"):
-            monkeypatch.delenv(e, raising=False)
-        if env:
-            monkeypatch.setenv(env, "1")
-        fronts = tools.sortNondominated(pop, n)
-        got.append(([f.cpu().numpy().tolist() for f in fronts],
-                    tools.selNSGA2(pop, n // 2).cpu().numpy().tolist(),
-                    [len(f) for f in tools.sortNondominated(pop, n // 3)]))
+    for path in ("default", "compare", "ballot", "lds", "peel_d"):
+        with dominance_path(path):
+            fronts = tools.sortNondominated(pop, n)
+            got.append(([f.cpu().numpy().tolist() for f in fronts],
+                        tools.selNSGA2(pop, n // 2).cpu().numpy().tolist(),
+                        [len(f) for f in tools.sortNondominated(pop, n // 3)]))
     assert got[0] == got[1] == got[2] == got[3] == got[4]
     assert sum(len(f) for f in got[0][0]) == n
 
@@ -469,15 +475,18 @@ def _tie_fitness(rng, n, m, kind):
 
 @pytest.mark.parametrize("m", [2, 3, 4])
 @pytest.mark.parametrize("n", [1, 37, 511, 513, 1100, 2900, 9001])
-def test_bitset_dominance_equals_compare_kernel(gpu, monkeypatch, m, n):
+def test_bitset_dominance_equals_compare_kernel(gpu, m, n):
     """The bitset-table dominance pass with the table-fed peel (bitdom.hip,
-    the default), the same pass writing D for the D-reading peel (DM_PEEL_D)
-    and the integer compare kernel (DM_DOM_TRI), and, up to n = 3,000, the oracle
+    the default for 2-3 objectives and for 4 since round 4), the same pass
+    writing D for the D-reading peel (DM_DOM_PEEL_D) and the integer compare
+    kernel (DM_DOM_COMPARE), and, up to n = 3,000, the oracle
     (deap/tools/emo.py:53-117): identical fronts, member for member and in
     order, on continuous fitnesses, ties in every objective, and objective-0
     tie groups wider than a 512-v chunk (the prefix / suffix masks), at sizes
     around one chunk and with a partial last chunk."""
-    from deap_amd import tools
+    from deap_amd import _lib, tools
+    from deap_amd.device import Context, dominance_path
+    ctx = Context.get()
     rng = np.random.default_rng(1000 * m + n)
     w = (1.0, -1.0, 1.0, -1.0)[:m]
     for kind in ("cont", "ties", "obj0"):
@@ -485,21 +494,19 @@ def test_bitset_dominance_equals_compare_kernel(gpu, monkeypatch, m, n):
         pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
                                valid=np.ones(n))
         got = []
-        for env in (None, "DM_DOM_TRI", "DM_PEEL_D"):
-            for e in ("DM_DOM_TRI", "DM_PEEL_D"):
-                monkeypatch.delenv(e, raising=False)
-            if env:
-                monkeypatch.setenv(env, "1")
-            got.append([f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)])
-        for e in ("DM_DOM_TRI", "DM_PEEL_D"):
-            monkeypatch.delenv(e, raising=False)
+        for path in ("default", "compare", "peel_d"):
+            with dominance_path(path):
+                got.append([f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)])
         assert got[0] == got[1] == got[2], kind
         assert sum(len(f) for f in got[0]) == n
         if n <= 3000:
             assert got[0] == ops.sort_nondominated(wv, n), kind
+    # the default path of every m here is the bitset pass (not the compare
+    # kernel it is checked against)
+    assert _lib.load().dm_ctx_dom_bitset(ctx.handle, m) == 1
 
 
-def test_front_larger_than_the_lds_sort(gpu, monkeypatch):
+def test_front_larger_than_the_lds_sort(gpu):
     """A second front of 20,000 unique fitnesses (beyond the 16,384 the
     one-workgroup LDS sort orders) goes through the host's radix-sort
     fallback; fronts equal the fp64 LDS path."""
@@ -511,9 +518,10 @@ def test_front_larger_than_the_lds_sort(gpu, monkeypatch):
     wv = np.concatenate([front1, front0, front1[:7]])[np.random.default_rng(2).permutation(2 * k + 7)]
     pop = _dp().from_numpy(np.zeros((len(wv), 1)), weights=(1.0, 1.0), gtype="f64",
                            wvalues=wv, valid=np.ones(len(wv)))
+    from deap_amd.device import dominance_path
     fast = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, len(wv))]
-    monkeypatch.setenv("DM_DOM_LDS", "1")
-    ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, len(wv))]
+    with dominance_path("lds"):
+        ref = [f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, len(wv))]
     assert [len(f) for f in fast] == [k, k + 7]
     assert fast == ref
 
@@ -579,6 +587,28 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
     assert np.array_equal(ok1, ok2)
     assert _rel_close(wv1, wv2, 1e-12)
     assert nev1 == nev2
+
+
+def test_clones_keep_negative_zero_fitness(gpu):
+    """Minimised OneMax: an all-zero genome has wvalues (-0.0,) (base.py:187-198,
+    0 * -1.0).  The fused packed-bit kernel's tournaments read int16 fitness
+    keys; a clone must still inherit -0.0 exactly as deepcopy does
+    (base.py:252-261), so fitness.values stays 0.0 and not -0.0."""
+    from deap_amd import algorithms, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim = 4001, 256
+    genes = np.zeros((n, dim), np.uint8)
+    genes[1::2, :3] = 1  # half the rows count 3
+    pop = _dp().from_numpy(genes, weights=(-1.0,), gtype="bits")
+    benchmarks.onemax(pop)
+    wv0 = pop.wvalues[:n, 0].cpu().numpy()
+    assert np.signbit(wv0[0]) and wv0[0] == 0.0
+    tb = _toolbox("twopoint", "flipbit", 0.05, 0.5, evaluate="onemax")
+    pop, _ = algorithms.eaSimple(pop, tb, 0.0, 0.0, 1, verbose=False, stream=RandomStream(5))
+    wv = pop.wvalues[:n, 0].cpu().numpy()
+    zero = wv == 0.0
+    assert zero.sum() > n // 4
+    assert np.signbit(wv[zero]).all()
 
 
 @pytest.mark.parametrize("maxsize,weights", [(1, (1.0,)), (5, (1.0,)), (12, (1.0, -1.0)),

@@ -126,6 +126,52 @@ def test_nsga2_matches_reference():
         assert len(ops.sort_nondominated(wv, kk, first_front_only=True)[0]) == d[k + "first"][0]
 
 
+def test_closed_form_order_matches_reference_goldens():
+    """oracle/nsga2_closed.py (the vectorised closed form of emo.py:53-117's
+    front order, the checker of the benched size) == the reference-generated
+    nsga2.npz order and selNSGA2 choice."""
+    from oracle import nsga2_closed
+    d = golden("nsga2.npz")
+    for j in range(6):
+        k = "nd%d_" % j
+        wv, weights, kk = d[k + "wv"], tuple(d[k + "weights"]), int(d[k + "k"])
+        fronts = nsga2_closed.sort_nondominated(wv, kk)
+        assert np.concatenate(fronts).tolist() == d[k + "order"].tolist(), j
+        assert np.cumsum([0] + [len(f) for f in fronts]).tolist() == d[k + "fstart"].tolist()
+        chosen, crowd = nsga2_closed.sel_nsga2(wv, weights, kk, fronts=fronts)
+        assert chosen == d[k + "chosen"].tolist(), j
+        assert np.array_equal([crowd[i] for i in np.concatenate(fronts).tolist()], d[k + "crowd"])
+        ff = nsga2_closed.sort_nondominated(wv, kk, first_front_only=True)
+        assert len(ff) == 1 and len(ff[0]) == d[k + "first"][0]
+
+
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_closed_form_order_matches_the_restatement(m):
+    """The closed form == oracle.ops.sort_nondominated (emo.py:53-117 line by
+    line) and its selNSGA2, on continuous, tied, duplicated and signed-zero
+    fitnesses, for k = n, n/2, 1, 0 and first_front_only."""
+    from oracle import nsga2_closed
+    rng = np.random.default_rng(40 + m)
+    for trial in range(12):
+        n = int(rng.integers(1, 500))
+        kind = trial % 3
+        if kind == 0:
+            wv = rng.uniform(0, 1, (n, m))
+        else:
+            wv = rng.integers(0, 6, (n, m)).astype(np.float64)
+            wv[rng.integers(0, n, n // 5)] = wv[rng.integers(0, n, n // 5)]
+            if kind == 2:
+                wv[rng.random((n, m)) < 0.2] *= -0.0
+        w = tuple(rng.choice([-1.0, 1.0, 2.0], m))
+        for k in (n, n // 2 + 1, 1, 0):
+            want = ops.sort_nondominated(wv, k)
+            assert [f.tolist() for f in nsga2_closed.sort_nondominated(wv, k)] == want
+            if k:
+                assert (nsga2_closed.sort_nondominated(wv, k, True)[0].tolist()
+                        == ops.sort_nondominated(wv, k, True)[0])
+                assert nsga2_closed.sel_nsga2(wv, w, k)[0] == ops.sel_nsga2(wv, w, k)[0]
+
+
 def test_mig_ring_matches_reference():
     d = golden("migration.npz")
     for j in range(3):
