@@ -89,6 +89,7 @@ SIGNATURES = {
     "dm_ctx_set_timing_target": (ctypes.c_int, [_p, _i32]),
     "dm_ctx_set_dom_path": (ctypes.c_int, [_p, _i32]),
     "dm_ctx_dom_bitset": (ctypes.c_int, [_p, _i32]),
+    "dm_ctx_reload_knobs": (ctypes.c_int, [_p]),
     "dm_philox_blocks": (ctypes.c_int, [_p, _PP(_u32), _PP(_u32), _i64, _p]),
     "dm_init_uniform": (ctypes.c_int, [_p, _PP(DevicePop), _f64, _f64, Rng]),
     "dm_evaluate": (ctypes.c_int, [_p, _PP(DevicePop), _PP(Eval), ctypes.c_int, _p]),

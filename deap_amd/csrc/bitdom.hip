@@ -136,6 +136,7 @@ __global__ __launch_bounds__(1024) void bd_plan_kernel(const int4* __restrict__ 
         const int64_t c = base + tid;
         int32_t nD = 0, nC = 0;
         if (c < NG) {
+            if (!BD_OK(ngroups - 1, U, "plan ngroups")) continue;
             int64_t lo = 0, hi = ngroups;  // first g with nseg[g] > c
             while (lo < hi) {
                 const int64_t mid = (lo + hi) >> 1;
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
     const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
     uint64_t* __restrict__ D) {
     constexpr int F = M - 1;
+    static_assert(F <= 2, "the prefix-set tables of 2-3 objectives fit in LDS");
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
     __shared__ uint16_t sB[F][BD_BKN];
@@ -239,6 +241,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
     int16_t* __restrict__ part) {
     constexpr int F = M - 1;
+    static_assert(F <= 2, "the prefix-set tables of 2-3 objectives fit in LDS");
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
     __shared__ uint16_t sB[F][BD_BKN];
@@ -248,6 +251,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     const int64_t c = bd_task_chunk<F>(toffC, NG, t);
     const int64_t vb = (int64_t)(t - toffC[c]) * BD_RT;
     const int64_t ve = std::min<int64_t>(reach[c], vb + BD_RT);
+    if (!BD_OK(c, NG, "count c") || !BD_OK(reach[c] - 1, U, "count reach")) return;
     int64_t v = vb + threadIdx.x;
     int4 sv = v < ve ? S[v] : make_int4(0, 0, 0, 0);
     int32_t sf = v < ve ? span[v].x : 0;
@@ -303,6 +307,7 @@ __global__ void bd_sum_kernel(const int16_t* __restrict__ part, const int2* __re
                               int32_t* __restrict__ countq) {
     DGRID_LOOP(q, U) {
         if (!BD_OK(sigma[q], U, "sum sigma")) continue;
+        if (!BD_OK(span[q].x, U, "sum span")) continue;
         const int64_t c0 = span[q].x / BD_CW;
         int32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
         int64_t c = c0;
@@ -343,7 +348,7 @@ int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64
                  const int32_t* nseg, const int32_t* sigma, uint64_t* D, int32_t* count,
                  int32_t* countq, char* ws) {
     hipStream_t s = ctx->stream;
-    DM_CHECK_ARG(m >= 2 && m <= 4, "bitdom: 2..4 objectives");
+    DM_CHECK_ARG(m >= 2 && m <= 3, "bitdom: 2 or 3 objectives");
     const BitdomLayout L = bitdom_layout(U, m);
     int32_t* first = (int32_t*)(ws + L.first);
     int32_t* last = (int32_t*)(ws + L.last);
@@ -357,8 +362,7 @@ int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64
                                       (int32_t*)(ws + L.toffD), (int32_t*)(ws + L.toffC));
     switch (m) {
         case 2: bitdom_launch<2>(ctx, S, U, NQ, L, ws, D); break;
-        case 3: bitdom_launch<3>(ctx, S, U, NQ, L, ws, D); break;
-        default: bitdom_launch<4>(ctx, S, U, NQ, L, ws, D); break;
+        default: bitdom_launch<3>(ctx, S, U, NQ, L, ws, D); break;
     }
     bd_sum_kernel<<<dg1(U), 256, 0, s>>>((const int16_t*)(ws + L.part), span, U, L.Upad, L.NG,
                                          sigma, count, countq);

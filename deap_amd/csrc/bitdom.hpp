@@ -23,20 +23,6 @@ __host__ __device__ __forceinline__ int bd_bucket_shift(int64_t U) {
 #define DM_BD_ABLATE 0
 #endif
 
-// DM_BD_CHECK builds (diagnostics only): every global index is range-checked
-// and an out-of-range one is printed and skipped.
-#ifdef DM_BD_CHECK
-__device__ __forceinline__ bool bd_ok(int64_t i, int64_t n, const char* tag) {
-    if (i >= 0 && i < n) return true;
-    printf("bitdom OOB %s: %lld of %lld (block %d,%d thread %d)\n", tag, (long long)i,
-           (long long)n, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);
-    return false;
-}
-#define BD_OK(i, n, tag) bd_ok((int64_t)(i), (int64_t)(n), tag)
-#else
-#define BD_OK(i, n, tag) true
-#endif
-
 struct BitdomLayout {
     int64_t NB, NG, Upad;
     size_t part, P, R, BK, first, last, span, rowfirst, reach, toffD, toffC, total;

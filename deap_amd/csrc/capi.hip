@@ -431,13 +431,7 @@ static int env_int(const char* name, int dflt) {
     return v ? atoi(v) : dflt;
 }
 
-int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
-    DM_CHECK_ARG(out != nullptr, "null out");
-    DM_HIP(hipSetDevice(device));
-    dm_ctx* c = new dm_ctx();
-    c->device = device;
-    c->stream = (hipStream_t)hip_stream;
-    dm_knobs& kn = c->knobs;  // A/B switches, read once (common.hpp)
+static void read_knobs(dm_knobs& kn) {
     kn.disable_pipe = std::getenv("DM_DISABLE_PIPE") != nullptr;
     kn.bits_plan = std::getenv("DM_BITS_PLAN") != nullptr;
     kn.bits_nocount = std::getenv("DM_BITS_NOCOUNT") != nullptr;
@@ -447,7 +441,21 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
     kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
     kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);
-    kn.bd_maxm = env_int("DM_BD_MAXM", 3);
+}
+
+int dm_ctx_reload_knobs(dm_ctx* ctx) {
+    DM_CHECK_ARG(ctx != nullptr, "null ctx");
+    read_knobs(ctx->knobs);
+    return DM_OK;
+}
+
+int dm_ctx_create(int device, void* hip_stream, dm_ctx** out) {
+    DM_CHECK_ARG(out != nullptr, "null out");
+    DM_HIP(hipSetDevice(device));
+    dm_ctx* c = new dm_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)hip_stream;
+    read_knobs(c->knobs);  // A/B switches, read once (common.hpp)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)

@@ -59,7 +59,6 @@ struct dm_knobs {
     bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
     int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
     int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)
-    int bd_maxm = 3;                // DM_BD_MAXM: most objectives on the bitset dominance path
 };
 
 struct dm_ctx {

@@ -806,6 +806,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         if (!fresh[it]) continue;
         const int64_t v = vbase + threadIdx.x + it * PEEL_WAVES * 64;
         const int32_t slot = S.sbase + S.wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
+        if (!BD_OK(slot, U, "release slot") || !BD_OK(vu[it], U, "release vu")) continue;
         cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
         cst<COH>(cq + slot, (int32_t)v);
         cst<COH>(rankU + vu[it], snf + 1);
@@ -909,6 +910,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         const int64_t v = c * BD_CW + threadIdx.x;
         pre.cnt[0] = v < U ? countq[v] : 0;
         pre.vu[0] = v < U ? sigma[v] : 0;
+        if (!BD_OK(pre.vu[0], U, "peel sigma")) pre.vu[0] = 0;
         pre.gs[0] = v < U ? gsize[pre.vu[0]] : 0;
     }
     const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
@@ -951,7 +953,8 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
 #pragma unroll
         for (int r = 0; r < WR; ++r) {
             const int64_t j = wb + (int64_t)(wave * WR + r) * 64 + lane;
-            mr[r] = j < Fm ? members[j] : make_int2(0, 0);
+            mr[r] = j < Fm && BD_OK(sust + j, U, "peel member") ? members[j] : make_int2(0, 0);
+            if (!BD_OK(mr[r].x, U, "peel member row")) mr[r] = make_int2(0, 0);
             bal[r] = __ballot(j < Fm && c < mr[r].y);
             nw += __popcll(bal[r]);
         }
@@ -986,6 +989,10 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
             int k[F];
             if (has && lim >= 0) {
                 bd_row_k<F>(suA, sR, sB, sh, k);
+#ifdef DM_BD_CHECK
+                for (int f = 0; f < F; ++f)
+                    if (!BD_OK(k[f], BD_K, "peel k")) k[f] = 0;
+#endif
             } else {
 #pragma unroll
                 for (int f = 0; f < F; ++f) k[f] = 0;
@@ -1126,6 +1133,7 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     __syncthreads();
     if (!sc.sgo) return;
     const int32_t n = sc.sn;
+    if (!BD_OK(sc.snstart + (int64_t)n - 1, st->U, "order front end")) return;
     if (n == 0) {  // nothing released: the reference's `if F2 == 0: break`
         if (tid == 0) cst<COH>(&st->done, 1);
         return;
@@ -1331,16 +1339,17 @@ int64_t fast_dom_words(int64_t U) {
     return NB * 64 * NQ * TW;
 }
 
-// Bitset tables (bitdom.hip) are the default dominance pass for 2 and 3
-// objectives; four take the compare kernel: the m = 4 bitset kernels (three
-// 33-KB tables, 104,640 B of LDS per workgroup) faulted on the GPU in the
-// product build but not in a range-checked DM_BD_CHECK build, and a plain
-// 104,640-B LDS kernel runs clean on the same boxes (tools_gpu/lds_probe.hip) —
-// unresolved; DM_BD_MAXM=4 re-enables them for diagnosis.
-// With the bitset pass the peel reads the tables, not a D matrix
-// (peel_tab_kernel), unless the DM_DOM_PEEL_D cross-check asks for the D peel.
+// Bitset tables (bitdom.hip) are the dominance pass for 2 and 3 objectives;
+// four take the integer compare kernel + D peel.  (An m = 4 bitset pass was
+// built and deleted in round 4: its first call in a fresh process faulted
+// deterministically in the product build -- with the tables in LDS and with
+// them read from global memory alike -- and never in the range-checked,
+// workspace-poisoning DM_BD_CHECK build, which printed no out-of-range index;
+// DESIGN.md §8.)  With the bitset pass the peel reads the tables, not a D
+// matrix (peel_tab_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
+// D peel.
 bool fast_bitset(const dm_ctx* ctx, int m) {
-    return m >= 2 && m <= ctx->knobs.bd_maxm && ctx->dom_path != DM_DOM_COMPARE;
+    return m >= 2 && m <= 3 && ctx->dom_path != DM_DOM_COMPARE;
 }
 bool fast_table_peel(const dm_ctx* ctx, int m) {
     return fast_bitset(ctx, m) && ctx->dom_path != DM_DOM_PEEL_D;
@@ -1515,11 +1524,8 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 if (m == 2)
                     peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
-                else if (m == 3)
-                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
-                                                                     st, countq, lastq, ckey, cq, rankU);
                 else
-                    peel_tab_kernel<3><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
+                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
             } else {
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(

@@ -5,6 +5,24 @@
 
 namespace dm {
 
+// DM_BD_CHECK builds (diagnostics only): the global indices of the bitset
+// dominance pass, the table-fed peel and the front ordering are range-checked
+// and an out-of-range one is printed and skipped; the fast path's workspace
+// is filled with a poison pattern first (a read before write shows up as an
+// out-of-range index).
+#ifdef DM_BD_CHECK
+__device__ __forceinline__ bool bd_ok(int64_t i, int64_t n, const char* tag) {
+    if (i >= 0 && i < n) return true;
+    printf("bitdom OOB %s: %lld of %lld (block %d,%d thread %d)\n", tag, (long long)i,
+           (long long)n, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);
+    return false;
+}
+#define BD_OK(i, n, tag) bd_ok((int64_t)(i), (int64_t)(n), tag)
+#else
+#define BD_OK(i, n, tag) true
+#endif
+
+
 #define DGRID_LOOP(i, n)                                                         \
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); \
          i += (int64_t)gridDim.x * blockDim.x)

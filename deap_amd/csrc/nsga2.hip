@@ -538,6 +538,9 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
                         radix_sort_temp_bytes(n) + scan_temp_bytes(n) + 8192;
     char* base = (char*)scratch(ctx, need);
     if (!base) return DM_ERR_NOMEM;
+#ifdef DM_BD_CHECK
+    DM_HIP(hipMemsetAsync(base, 0x7F, need, s));
+#endif
     int32_t* hostv = (int32_t*)pinned(ctx, 2048);  // the size fast_fronts asks for: no realloc
     if (!hostv) return DM_ERR_NOMEM;
     Bump bp{base};
@@ -632,6 +635,11 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     char* fwork = nullptr;  // fast path workspace (dominance.hip)
     if (fast) {
         fwork = (char*)scratch_slot(ctx, 4, fast_dom_bytes(n, U));
+#ifdef DM_BD_CHECK
+        // diagnostics: poison the fast path's workspace (a read before write
+        // then shows up as an out-of-range index in the range checks)
+        if (fwork) DM_HIP(hipMemsetAsync(fwork, 0x7F, fast_dom_bytes(n, U), s));
+#endif
         if (!fwork) return DM_ERR_NOMEM;
     }
 

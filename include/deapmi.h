@@ -171,6 +171,10 @@ enum dm_dom_path {
     DM_DOM_LDS = 4       /* fp64 LDS-tiled kernel + peel (any objectives) */
 };
 int dm_ctx_set_dom_path(dm_ctx* ctx, int32_t path);
+/* Re-read the A/B tuning switches (DM_PIPE_BPC, DM_BITS_PP4, ... DESIGN.md
+ * §3) from the environment; dm_ctx_create reads them once.  Measurement
+ * tools only: every switch selects between bit-identical kernels. */
+int dm_ctx_reload_knobs(dm_ctx* ctx);
 /* 1 when the context's dominance pass for nobj objectives (NaN-free
  * fitnesses) is the bitset-table pass, else 0 (introspection for tests). */
 int dm_ctx_dom_bitset(dm_ctx* ctx, int32_t nobj);

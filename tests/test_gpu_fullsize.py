@@ -270,9 +270,9 @@ def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
     usizes, want, want_crowd = _check_standard_order(pop, wv, weights, k, ref_fronts)
     # crowding of a front depends on its order only through duplicates: the
     # port's (log-order) distances agree on rows without an equal twin
-    if kind in ("shells", "dupshells"):
-        assert max(usizes) > 2 * 2048, usizes  # the table peel's member slices
-    if kind == "dupshells":
+    if kind == "shells":  # fronts of ~3,500 unique fits: one slice per chunk
+        assert max(usizes) > 1024, usizes
+    if kind == "dupshells":  # >= 2 x 2,048: the table peel's member slices
         assert max(usizes) >= 8192, usizes
     if kind == "grid":
         last = want[-1]

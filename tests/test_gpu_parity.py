@@ -476,17 +476,22 @@ def _tie_fitness(rng, n, m, kind):
 @pytest.mark.parametrize("m", [2, 3, 4])
 @pytest.mark.parametrize("n", [1, 37, 511, 513, 1100, 2900, 9001])
 def test_bitset_dominance_equals_compare_kernel(gpu, m, n):
-    """The bitset-table dominance pass with the table-fed peel (bitdom.hip,
-    the default for 2-3 objectives and for 4 since round 4), the same pass
-    writing D for the D-reading peel (DM_DOM_PEEL_D) and the integer compare
-    kernel (DM_DOM_COMPARE), and, up to n = 3,000, the oracle
-    (deap/tools/emo.py:53-117): identical fronts, member for member and in
-    order, on continuous fitnesses, ties in every objective, and objective-0
-    tie groups wider than a 512-v chunk (the prefix / suffix masks), at sizes
-    around one chunk and with a partial last chunk."""
+    """The default dominance pass against independent cross-check paths and,
+    up to n = 3,000, the oracle (deap/tools/emo.py:53-117): identical fronts,
+    member for member and in order, on continuous fitnesses, ties in every
+    objective, and objective-0 tie groups wider than a 512-v chunk (the
+    prefix / suffix masks), at sizes around one chunk and with a partial last
+    chunk.  Two and three objectives: the bitset-table pass with the
+    table-fed peel (bitdom.hip) against the same pass writing D for the
+    D-reading peel (DM_DOM_PEEL_D) and the integer compare kernel
+    (DM_DOM_COMPARE).  Four objectives: the default is the integer compare
+    kernel + D peel, checked against the fp64 ballot and LDS kernels."""
     from deap_amd import _lib, tools
     from deap_amd.device import Context, dominance_path
     ctx = Context.get()
+    bitset = m <= 3
+    assert _lib.load().dm_ctx_dom_bitset(ctx.handle, m) == (1 if bitset else 0)
+    paths = ("default", "compare", "peel_d") if bitset else ("default", "ballot", "lds")
     rng = np.random.default_rng(1000 * m + n)
     w = (1.0, -1.0, 1.0, -1.0)[:m]
     for kind in ("cont", "ties", "obj0"):
@@ -494,16 +499,13 @@ def test_bitset_dominance_equals_compare_kernel(gpu, m, n):
         pop = _dp().from_numpy(np.zeros((n, 1)), weights=w, gtype="f64", wvalues=wv,
                                valid=np.ones(n))
         got = []
-        for path in ("default", "compare", "peel_d"):
+        for path in paths:
             with dominance_path(path):
                 got.append([f.cpu().numpy().tolist() for f in tools.sortNondominated(pop, n)])
         assert got[0] == got[1] == got[2], kind
         assert sum(len(f) for f in got[0]) == n
         if n <= 3000:
             assert got[0] == ops.sort_nondominated(wv, n), kind
-    # the default path of every m here is the bitset pass (not the compare
-    # kernel it is checked against)
-    assert _lib.load().dm_ctx_dom_bitset(ctx.handle, m) == 1
 
 
 def test_front_larger_than_the_lds_sort(gpu):
