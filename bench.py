@@ -374,6 +374,17 @@ def main(argv=None):
     for p in pops:
         assert bool(p.valid[:n].bool().all()), "invalid fitness left after a generation"
         assert bool(torch.isfinite(p.wvalues[:n]).all()), "non-finite fitness"
+    # correctness fingerprint of every deme after the last step (outside the
+    # timed region): the Philox streams are keyed by the deme id and the
+    # migration is exact, so a deme's digest depends only on (seed, deme id,
+    # islands, steps, migration schedule), never on how the demes are spread
+    # over ranks -- runs of the same --islands on 1, 2, 4 or 8 GPUs must print
+    # the same digests (tests/test_gpu_islands_mp.py checks the rows themselves)
+    digests = {d: deme_digest(p, n) for d, p in zip(ids, pops)}
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, digests)
+        digests = {d: h for part in parts for d, h in part.items()}
 
     total = n * args.steps * n_demes
     value = total / elapsed
@@ -407,6 +418,9 @@ def main(argv=None):
         out["migration"] = {"ms_per_migration": round(mig_ms, 4), "every": args.mig_every,
                             "k": args.mig_k,
                             "frac_of_time": round(mig_ms * len(mig_events) / (elapsed * 1e3), 5)}
+    out["deme_digests"] = {"after_generation": args.warmup + args.steps, "seed": args.seed,
+                           "islands": n_demes,
+                           "digest": {str(d): digests[d] for d in sorted(digests)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(problem, args.cpu_sample)
     else:
@@ -417,6 +431,27 @@ def main(argv=None):
         from deap_amd import islands
         islands.close_comms()
         dist.destroy_process_group()
+
+
+def deme_digest(pop, n):
+    """64-bit fingerprint of a deme (test infrastructure for the scaling runs):
+    a wrapping multiply-add of every genome word (fixed odd multipliers per
+    word position and per row) plus the bits of every wvalue and valid byte,
+    computed on the device in slices of rows."""
+    import numpy as np
+    import torch
+    g = pop.genes[:n].view(torch.int64)
+    rng = np.random.default_rng(20261017)
+    mw = torch.from_numpy(rng.integers(1, 2**62, size=g.shape[1], dtype=np.int64) | 1).to(g.device)
+    acc = torch.zeros((), dtype=torch.int64, device=g.device)
+    for a in range(0, n, 1 << 16):
+        b = min(n, a + (1 << 16))
+        rows = (g[a:b] * mw).sum(dim=1)
+        mr = torch.arange(a + 1, b + 1, dtype=torch.int64, device=g.device) * (0x9E3779B97F4A7C15 - 2**64)
+        acc += (rows * (mr | 1)).sum()
+    w = pop.wvalues[:n].contiguous().view(torch.int64)
+    acc += (w * 0x632BE59BD9B4E019).sum() + pop.valid[:n].to(torch.int64).sum()
+    return "%016x" % (int(acc.item()) & (2**64 - 1))
 
 
 def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):

@@ -48,12 +48,17 @@ def _evolve(ids, n_demes=N_DEMES, migarray=None):
     return {d: p.to_numpy() for d, p in zip(ids, demes)}, log
 
 
-def _worker(rank, world, port, ids_by_rank, migarray, q):
+def _worker(rank, world, port, ids_by_rank, migarray, q, backend="gloo"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo: both ranks on the one GPU of the box; nccl (RCCL): one GPU per rank
+    torch.cuda.set_device(rank if backend == "nccl" else 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", rank))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         got, log = _evolve(ids_by_rank[rank], migarray=migarray)
         q.put((rank, {d: (g, wv) for d, (g, wv, _) in got.items()},
@@ -62,6 +67,8 @@ def _worker(rank, world, port, ids_by_rank, migarray, q):
         q.put((rank, repr(e), None))
         raise
     finally:
+        from deap_amd import islands
+        islands.close_comms()
         dist.destroy_process_group()
 
 
@@ -78,12 +85,16 @@ def _free_port():
     ([[3], [0, 1, 2]], [2, 3, 1, 0]),  # uneven split, another permutation
 ])
 def test_two_ranks_equal_one_process(gpu, ids_by_rank, migarray):
+    _run_two_ranks(ids_by_rank, migarray, "gloo")
+
+
+def _run_two_ranks(ids_by_rank, migarray, backend):
     import torch.multiprocessing as mp
     want, want_log = _evolve(list(range(N_DEMES)), migarray=migarray)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, ids_by_rank, migarray, q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ids_by_rank, migarray, q, backend))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -105,6 +116,28 @@ def test_two_ranks_equal_one_process(gpu, ids_by_rank, migarray):
         assert np.array_equal(got[d][0], want[d][0]), "deme %d genomes" % d
         assert np.array_equal(got[d][1], want[d][1]), "deme %d fitness" % d
     assert sorted(logs) == sorted((r["gen"], r["deme"], r["evals"]) for r in want_log)
+
+
+@pytest.mark.parametrize("ids_by_rank,migarray", [
+    ([[0, 1], [2, 3]], None),          # even split, the ring crosses GPUs twice
+    ([[0, 2], [1, 3]], None),          # interleaved: every hop crosses GPUs
+    ([[0, 1, 2, 3], []], None),        # GPU 1 holds no deme, joins every exchange
+    ([[3], [0, 1, 2]], [2, 3, 1, 0]),  # uneven split, another permutation
+])
+def test_two_gpus_rccl_equal_one_process(gpu, ids_by_rank, migarray):
+    """The cross-GPU exchange itself: two ranks on two
+    GPUs with the ``nccl`` (RCCL) process group, so every cross-rank hop goes
+    through ``dm_mig_ring_rccl`` (the ranks' agreement ``ncclAllReduce``, the
+    grouped ``ncclSend`` / ``ncclRecv`` of the packed emigrants over xGMI,
+    the placement on the receiver).  ``eaSimpleDemes`` with 4 OneMax demes
+    and migRing every 5 generations (examples/ga/onemax_island.py:140-154,
+    deap/tools/migration.py:4-51) must equal the single-process run row for
+    row, which test_gpu_islands.py replays in the oracle.  Skips on a box
+    with one GPU (RCCL refuses two ranks on one device)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    _run_two_ranks(ids_by_rank, migarray, "nccl")
 
 
 def test_second_hop_into_a_deme_has_no_identity_match(gpu):
