@@ -160,18 +160,30 @@ def _reference_tools():
     return ref_tools
 
 
-def to_reference_types(halloffame, logbook, tools_module):
+def _as_class(ind, individual_class):
+    """A hall entry as ``individual_class`` (e.g. DEAP's creator.Individual):
+    the same genes, the same weighted fitness when it is valid."""
+    out = individual_class(ind)
+    if ind.fitness.valid:
+        out.fitness.wvalues = tuple(ind.fitness.wvalues)
+    return out
+
+
+def to_reference_types(halloffame, logbook, tools_module, individual_class=None):
     """Rebuild a hall of fame and a logbook as ``tools_module.HallOfFame`` /
-    ``tools_module.Logbook`` objects (DEAP's classes when exporting for DEAP:
-    unpickling them then needs DEAP only, not deap_amd).  The hall keeps its
-    order (insertion worst first re-creates equal-fitness order exactly,
-    support.py:550-560); the logbook keeps header, records, chapters and the
-    stream position."""
+    ``tools_module.Logbook`` objects (DEAP's classes when exporting for DEAP).
+    With ``individual_class`` (a DEAP creator class) the hall's entries are
+    rebuilt as that class too, so unpickling needs DEAP only; without it they
+    stay the hall's own individuals (deap_amd host individuals when the hall
+    was filled from a DevicePopulation without a creator class).  The hall
+    keeps its order (insertion worst first re-creates equal-fitness order
+    exactly, support.py:550-560); the logbook keeps header, records, chapters
+    and the stream position."""
     hof = lb = None
     if halloffame is not None:
         hof = tools_module.HallOfFame(halloffame.maxsize, halloffame.similar)
         for ind in reversed(list(halloffame)):
-            hof.insert(ind)
+            hof.insert(ind if individual_class is None else _as_class(ind, individual_class))
     if logbook is not None:
         lb = _copy_logbook(logbook, tools_module.Logbook)
     return hof, lb
@@ -208,7 +220,7 @@ def export_reference_dict(population, generation=None, halloffame=None, logbook=
     import random
     tm = tools_module if tools_module is not None else _reference_tools()
     if tm is not None:
-        halloffame, logbook = to_reference_types(halloffame, logbook, tm)
+        halloffame, logbook = to_reference_types(halloffame, logbook, tm, individual_class)
     return {"population": population.to_individuals(individual_class),
             "generation": generation, "halloffame": halloffame, "logbook": logbook,
             "rndstate": random.getstate(),

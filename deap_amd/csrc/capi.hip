@@ -441,6 +441,7 @@ static void read_knobs(dm_knobs& kn) {
     kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
     kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);
+    kn.pipe_noorder = std::getenv("DM_PIPE_NOORDER") != nullptr;
 }
 
 int dm_ctx_reload_knobs(dm_ctx* ctx) {

@@ -59,6 +59,7 @@ struct dm_knobs {
     bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
     int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
     int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)
+    bool pipe_noorder = false;      // DM_PIPE_NOORDER: C3 plans in pair order (no parent order)
 };
 
 struct dm_ctx {

@@ -45,11 +45,12 @@ typedef __attribute__((address_space(4))) const uint32_t c4_u32;
 struct PairPlan {
     int32_t s0, s1;    // parent rows
     uint32_t cuts;     // cxTwoPoint slice [cp1, cp2): cp1 | cp2 << 16
-    uint32_t flags;    // PF_*
+    uint32_t flags;    // PF_*; bits PF_PAIR_SHIFT.. = the pair index (parent-ordered plans)
     double f0, f1;     // parents' wvalues[0] (inherited by an unchanged clone)
 };
 static_assert(sizeof(PairPlan) == 32, "PairPlan layout");
 enum : uint32_t { PF_CX = 1, PF_MUT0 = 2, PF_MUT1 = 4, PF_HAS1 = 8, PF_INV0 = 16, PF_INV1 = 32 };
+constexpr int PF_PAIR_SHIFT = 8;  // parent-ordered plans: up to 2^24 pairs
 
 // Scalar (SMEM) load of a plan: wave-uniform index, tracked by lgkmcnt.
 __device__ __forceinline__ PairPlan load_plan(const PairPlan* plans, int64_t p) {
@@ -260,6 +261,10 @@ struct PipeArgs {
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
     int32_t bpc, depth;  // dm_knobs: workgroups per CU, ring depth (0 = defaults)
+    // 1: the plans are in parent order (plan_order_kernel), each carries its
+    // pair index, and a wave takes a contiguous run of them (pairs that share
+    // a parent row back to back: its second read is a cache hit)
+    int32_t ordered;
     Rng rng;
     uint64_t thr_ind;
     double alpha, mu, sigma, w0;
@@ -299,14 +304,28 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (p >= npairs) return;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // plan slots of this wave: j = wid, wid + nw, ... (pair order), or a
+    // contiguous run (parent order); the pair of slot j is j, or the index the
+    // ordered plan carries
+    int64_t j, jend, jstep;
+    if (a.ordered) {
+        const int64_t per = (npairs + nw - 1) / nw;
+        j = wid * per;
+        jend = std::min<int64_t>(npairs, j + per);
+        jstep = 1;
+    } else {
+        j = wid;
+        jend = npairs;
+        jstep = nw;
+    }
+    if (j >= jend) return;
     int64_t evals = 0;
     const int dim = a.dim;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
-    PairPlan pl = load_plan(a.plans, p);
-    PairPlan nx = load_plan(a.plans, p + nw < npairs ? p + nw : p);
+    PairPlan pl = load_plan(a.plans, j);
+    PairPlan nx = load_plan(a.plans, j + jstep < jend ? j + jstep : j);
     // ring of D chunk slots over the chunk sequence (p,0..NCH-1), (p+W,0..), ...
     double y0[D][4], y1[D][4];
 #pragma unroll
@@ -314,10 +333,11 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
         L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch]);
         L::load(a.pgenes + (int64_t)pl.s1 * a.pstride, ch, lane, dim, y1[ch]);
     }
-    for (; p < npairs; p += nw) {
-        const bool more = p + nw < npairs;
-        const int64_t p2 = p + 2 * nw;
-        const PairPlan nn = load_plan(a.plans, p2 < npairs ? p2 : p);  // two ahead
+    for (; j < jend; j += jstep) {
+        const bool more = j + jstep < jend;
+        const int64_t j2 = j + 2 * jstep;
+        const PairPlan nn = load_plan(a.plans, j2 < jend ? j2 : j);  // two ahead
+        const int64_t p = a.ordered ? (int64_t)(pl.flags >> PF_PAIR_SHIFT) : j;
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const uint32_t fl = pl.flags;
         const bool cx = fl & PF_CX, mut0 = fl & PF_MUT0, mut1 = fl & PF_MUT1;
@@ -534,8 +554,15 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
     }
 }
 
-// Decisions of every pair (thread per pair), generation_pipe_f64.hip.
-void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s);
+// Decisions of every pair (thread per pair), generation_pipe_f64.hip.  With
+// keys / hist (zeroed, one counter per parent row): key[p] = the plan's
+// sort key (its fitter parent) and hist[key] counts the plans per key.
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
+                       int32_t* keys = nullptr, int32_t* hist = nullptr);
+// The plans in key order: cursor = the exclusive scan of hist (consumed);
+// ordered[pos] = plans[p] with p in its flags (PF_PAIR_SHIFT).
+void launch_plan_order(const PairPlan* plans, const int32_t* keys, int32_t* cursor,
+                       PairPlan* ordered, int64_t npairs, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).

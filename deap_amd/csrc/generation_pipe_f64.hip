@@ -12,7 +12,8 @@ namespace dm {
 // (algorithms.py:75-81 `del fitness.values`, algorithms.py:155-158).
 // Decisions of pair p -> plans[p]; returns the plan's flags.
 __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
-                                             int64_t p) {
+                                             int64_t p, int32_t* __restrict__ keys,
+                                             int32_t* __restrict__ hist) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
     const int m = a.nobj;
@@ -72,6 +73,13 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     pl.f0 = a.pwv[(int64_t)s[0] * m];
     pl.f1 = a.pwv[(int64_t)s[1] * m];
     plans[p] = pl;
+    if (keys) {
+        // sort key: the fitter parent (tournament winners repeat with their
+        // fitness: a fitter row is the likelier one to recur in other pairs)
+        const int32_t key = pl.f1 > pl.f0 ? s[1] : s[0];
+        keys[p] = key;
+        atomicAdd(hist + key, 1);
+    }
     return fl;
 }
 
@@ -80,13 +88,15 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
 // algorithms.py:171-174) into a.nevals: one ballot per wave, evals_fold per
 // workgroup.
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
-                                                        long long* __restrict__ count_evals) {
+                                                        long long* __restrict__ count_evals,
+                                                        int32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ hist) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p);
+        if (p < npairs) fl = plan_one(a, plans, p, keys, hist);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -96,12 +106,35 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p);
+    if (p < npairs) plan_one(a, plans, p, keys, hist);
 }
 
-void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s) {
+void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
+                       int32_t* keys, int32_t* hist) {
     const int64_t npairs = (a.nc + 1) / 2;
-    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals);
+    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals,
+                                                                           keys, hist);
+}
+
+// Counting-sort scatter of the plans by key.  The order inside a key's run
+// is whatever the atomics give: the processing order never changes a result
+// (every child is a function of its own plan and counters).
+__global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restrict__ plans,
+                                                         const int32_t* __restrict__ keys,
+                                                         int32_t* __restrict__ cursor,
+                                                         PairPlan* __restrict__ ordered,
+                                                         int64_t npairs) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npairs) return;
+    PairPlan pl = plans[p];
+    pl.flags |= (uint32_t)p << PF_PAIR_SHIFT;
+    ordered[atomicAdd(cursor + keys[p], 1)] = pl;
+}
+
+void launch_plan_order(const PairPlan* plans, const int32_t* keys, int32_t* cursor,
+                       PairPlan* ordered, int64_t npairs, hipStream_t s) {
+    plan_order_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(plans, keys, cursor,
+                                                                            ordered, npairs);
 }
 
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,

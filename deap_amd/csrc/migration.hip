@@ -197,7 +197,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
                                                       int64_t words, unsigned long long* bitmap,
                                                       const uint8_t* E, const int32_t* first,
                                                       int32_t* slots, int32_t* content,
-                                                      unsigned long long* dirty, int32_t* err) {
+                                                      unsigned long long* dirty,
+                                                      const int32_t* self_rows, int32_t* err) {
     Block em = block_view((void*)em_block, stride, nobj, k);
     __shared__ int64_t best;
     __shared__ int32_t placed_slot[4096];
@@ -230,7 +231,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
             if (lane == 0) {
                 valid[slot] = em.valid[j];
                 slots[j] = (int32_t)slot;
-                if (dirty) atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+                if (dirty && !(self_rows && self_rows[j] == slot))
+                    atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
             }
         }
         return;
@@ -284,7 +286,11 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
         if (threadIdx.x < nobj) wv[slot * nobj + threadIdx.x] = em.wv[j * nobj + threadIdx.x];
         if (threadIdx.x == 0) {
             valid[slot] = em.valid[j];
-            if (dirty) atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+            // a self hop (migarray[d] == d) that puts a row's own object back
+            // in that row keeps its identity (list.index's `is` test of a later
+            // hop still matches it): not dirty
+            if (dirty && !(self_rows && self_rows[j] == slot))
+                atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
         }
         // the row no longer holds its original genome
         for (int64_t jj = j + 1 + threadIdx.x; jj < k; jj += blockDim.x)
@@ -323,9 +329,12 @@ namespace dm {
 // dirty (nullable, ceil(n/64) words): rows overwritten by earlier hops into
 // this deme in the same migration (read by the identity test, and the rows
 // this placement overwrites are added).
+// self_rows (nullable): for a hop from the deme into itself, the emigrants'
+// rows in it.
 static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block,
                            const void* emigrant_block, int64_t k, int32_t* out_slots,
-                           unsigned long long* dirty, int32_t* err) {
+                           unsigned long long* dirty, int32_t* err,
+                           const int32_t* self_rows = nullptr) {
     const int64_t n = pop->n;
     const int64_t words = (n + 63) / 64;
     const size_t bm = align_up((size_t)k * words * 8, 256);
@@ -351,7 +360,7 @@ static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block
         emigrant_block, immigrant_block, k, pop->stride, pop->dim, pop->gtype, pop->nobj, E);
     resolve_kernel<<<1, 256, 0, s>>>((char*)pop->genes, pop->wvalues, pop->valid, n, pop->stride,
                                      pop->nobj, emigrant_block, k, words, bitmap, E, first,
-                                     out_slots, content, dirty, err);
+                                     out_slots, content, dirty, self_rows, err);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -666,8 +675,9 @@ static int mig_ring_impl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* de
         if (!incoming[h]) continue;
         const int32_t t = local_of[hops[h].to];
         int32_t* slots = out_slots && out_slots[t] ? out_slots[t] : slot_scratch;
+        const bool self_hop = hops[h].kind == DM_HOP_LOCAL && hops[h].from == hops[h].to;
         if ((rc = mig_place_async(ctx, &demes[t], immig[t], incoming[h], k, slots, dirty[t],
-                                  errs + h)))
+                                  errs + h, self_hop ? emig_idx[t] : nullptr)))
             return rc;
     }
     std::vector<int32_t> herr(hops.size(), 0);

@@ -152,3 +152,10 @@ def test_checkpoint_reference_types_keep_order_and_chapters():
     assert l2.chapters["fit"].select("max") == [1.0, 2.0]
     h3, l3 = checkpoint.to_reference_types(None, None, tools)
     assert h3 is None and l3 is None
+    # entries of another class (deap_amd host individuals of a DevicePopulation
+    # without a creator class) come back as the given individual_class
+    creator.create("IndC2", list, fitness=creator.FMaxC)
+    h4, _ = checkpoint.to_reference_types(hof, None, tools, creator.IndC2)
+    assert all(type(i) is creator.IndC2 for i in h4)
+    assert [list(i) for i in h4] == [list(i) for i in hof]
+    assert [i.fitness.values for i in h4] == [i.fitness.values for i in hof]

@@ -176,3 +176,30 @@ def test_second_hop_into_a_deme_has_no_identity_match(gpu):
     g1, _, _ = demes[1].to_numpy()
     assert np.array_equal(g1[2], genes[0][2])
     del torch
+
+
+def test_self_hop_keeps_identity_for_a_later_hop(gpu):
+    """migarray [0, 0]: deme 0 sends to itself, then deme 1 sends into deme 0
+    (ADVICE r3).  Deme 0's emigrant (row 2, a NaN genome: list.index finds it
+    only by identity) goes back into its own row on the self hop -- the same
+    object, so the second hop still finds that immigrant by identity and
+    replaces it with deme 1's emigrant (deap/tools/migration.py:48-51,
+    restated below with Python lists of the same objects).  The device must
+    keep that row matchable after the self hop."""
+    from deap_amd import tools
+    from deap_amd.device import DevicePopulation
+
+    genes = [np.arange(12, dtype=np.float64).reshape(3, 4) + 100 * d for d in range(2)]
+    genes[0][2, 0] = np.nan
+    demes = [DevicePopulation.from_numpy(g, (1.0,), wvalues=g[:, 1:2], valid=np.ones(3))
+             for g in genes]
+    host = [[list(r) for r in g] for g in genes]
+    em = [[host[0][2]], [host[1][2]]]  # selBest(k=1): row 2 of each deme
+    for frm, to in enumerate([0, 0]):
+        for i, imm in enumerate(em[to]):
+            host[to][host[to].index(imm)] = em[frm][i]
+    assert host[0][2] is em[1][0]  # the reference replaced the NaN row
+    tools.migRing(demes, 1, tools.selBest, migarray=[0, 0])
+    g0, _, _ = demes[0].to_numpy()
+    assert np.array_equal(g0, np.array(host[0]), equal_nan=True)
+    assert np.array_equal(g0[2], genes[1][2])

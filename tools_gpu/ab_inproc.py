@@ -4,7 +4,7 @@ rounds, so the buffer-placement effect cannot bias the
 comparison as it does across processes.
 
   python tools_gpu/ab_inproc.py CONFIG VAR VALUE [VALUE ...]
-e.g.  python tools_gpu/ab_inproc.py c3 DM_PIPE_BPC 32 64
+e.g.  python tools_gpu/ab_inproc.py c3 DM_PIPE_BPC 32 64   (value "unset" removes the variable)
 Prints each value's mean generation-kernel time (library HIP events)."""
 import ctypes
 import os
@@ -45,7 +45,10 @@ torch.cuda.synchronize()
 res = {v: [] for v in values}
 for r in range(rounds):
     for v in values:
-        os.environ[var] = v
+        if v == "unset":
+            os.environ.pop(var, None)
+        else:
+            os.environ[var] = v
         _lib.call("dm_ctx_reload_knobs", ctx)  # the switches are read per context
         _lib.call("dm_ctx_set_timing", ctx, G)
         for _ in range(G):
