@@ -490,6 +490,48 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
     return out
 
 
+VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9  # wave64 VALU instructions/s: SIMD-32, 2 clk each
+
+
+def peel_report(peel_us, usz):
+    """C5's dominant kernel, the table-fed front peel (dominance.hip
+    peel_tab_kernel): one launch per front; launch i peels front i (usz[i]
+    unique fitnesses) and releases front i + 1, the launches after the last
+    front exit at once.  It is VALU-issue and latency bound (64 x 64 bit
+    transposes of the members' rows), so its roofline is VALU
+    wave-instructions issued per second against the issue peak (256 CU x 4
+    SIMD x 2.4 GHz / 2 clk per wave64 instruction on SIMD-32): the
+    instructions per selection come from the PMC pass committed in
+    profiles/c5_peel_pmc.json (SQ_INSTS_VALU summed over one selection's peel
+    launches), the time from the live events.  Also: microseconds per launch
+    against the front size (floor + slope)."""
+    import numpy as np
+    nf = len(usz)
+    work = [(usz[i], peel_us[i]) for i in range(min(nf, len(peel_us)))]
+    tot_ms = sum(peel_us) / 1e3
+    fit = np.polyfit([w[0] for w in work], [w[1] for w in work], 1) if len(work) > 2 else (0, 0)
+    fronts = {"launches": len(peel_us), "fronts": nf, "ms_per_selection": round(tot_ms, 4),
+              "us_per_launch_mean": round(sum(peel_us) / max(1, len(peel_us)), 2),
+              "us_floor": round(float(fit[1]), 2), "us_per_1000_members": round(float(fit[0]) * 1e3, 2),
+              "by_front": [[int(a), round(b, 1)] for a, b in work]}
+    pmc = None
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "c5_peel_pmc.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            pmc = json.load(f)
+    roof = {"bound": "valu-issue", "kernel": "peel_tab_kernel<2>", "unit": "Ginstr/s",
+            "peak": round(VALU_PEAK_GINSTR, 1), "kernel_ms": round(tot_ms, 4),
+            "peak_basis": "wave64 VALU instructions: 256 CU x 4 SIMD-32 x 2.4 GHz / 2 clk",
+            "traffic": None, "achieved": None, "frac": None}
+    if pmc:
+        instr = float(pmc["SQ_INSTS_VALU_per_selection"])
+        ach = instr / (tot_ms * 1e-3) / 1e9
+        roof.update(achieved=round(ach, 1), frac=round(ach / VALU_PEAK_GINSTR, 4),
+                    valu_instr_per_selection=instr, pmc_source=pmc.get("source"),
+                    wave_cycles_valu_frac=pmc.get("SQ_ACTIVE_INST_VALU_over_SQ_WAVE_CYCLES"))
+    return {"roofline": roof, "fronts": fronts}
+
+
 def replica_setup(args, world, local):
     """C5 / C5x at N > 1: replicas only (no exchange step), one
     process per GPU; the process group is used for the barrier and the
@@ -603,6 +645,23 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     assert cnt.value == reps, "expected one dominance kernel per selection, got %d" % cnt.value
     dom_ms = sorted(times[1:])[(reps - 1) // 2]
     sel_ms = sorted(sel_ms[1:])[(reps - 1) // 2]
+    # the front peel, the selection's dominant kernel: every peel launch of one
+    # selNSGA2 timed by HIP events the library records around it, in front order
+    cap = 1024
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_PEEL)
+    _lib.call("dm_ctx_set_timing", ctx, cap)
+    tools.selNSGA2(two, n)
+    torch.cuda.synchronize()
+    ptimes = (ctypes.c_float * cap)()
+    pcnt = ctypes.c_int32(0)
+    _lib.call("dm_ctx_kernel_times", ctx, ptimes, cap, ctypes.byref(pcnt))
+    _lib.call("dm_ctx_set_timing", ctx, 0)
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_GENERATION)
+    peel_us = [t * 1e3 for t in ptimes[:min(cap, pcnt.value)]]
+    sel_fronts = tools.sortNondominated(two, n)
+    wvh = two.wvalues[:2 * n].cpu().numpy()
+    usz = [int(len(np.unique(wvh[f.cpu().numpy()], axis=0))) for f in sel_fronts]
+    peel = peel_report(peel_us, usz)
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
     ufit = torch.unique(wv, dim=0).cpu().numpy()
@@ -629,16 +688,17 @@ def bench_nsga2(args, world=1, rank=0, local=0):
                       "operators": "varOr cxBlend(0.5) mutGaussian(0,0.1,1/D) cxpb=0.6 mutpb=0.3",
                       "parallelism": "replicas%d" % world},
            "gen_ms_events": round(gen_ms, 4),
-           "roofline": {"bound": "lds", "achieved": round(achieved, 1), "peak": lds_peak,
-                        "unit": "GB/s", "frac": round(achieved / lds_peak, 4),
-                        "traffic": None, "kernel": "bd_count_kernel<3>",
-                        "kernel_ms": round(dom_ms, 4), "lds_bytes_per_launch": lds_bytes,
-                        "count": "sum_c reach_c x (M-1) x (11 probes x 4 B + 64-B prefix set)",
-                        "peak_basis": "LDS reads: 256 CU x 256 B/clk x 2.4 GHz",
-                        "compares_per_launch": cmp_per_sel,
-                        "compare_rate_G": round(cmp_rate, 1),
-                        "compare_rate_vs_valu_compare_peak": round(cmp_rate / valu_peak, 4),
-                        "unique_fits": uniq, "fronts": len(fronts)},
+           "roofline": peel["roofline"],
+           "peel": peel["fronts"],
+           "count_pass": {"bound": "lds", "achieved": round(achieved, 1), "peak": lds_peak,
+                          "unit": "GB/s", "frac": round(achieved / lds_peak, 4),
+                          "kernel": "bd_count_kernel<3>",
+                          "kernel_ms": round(dom_ms, 4), "lds_bytes_per_launch": lds_bytes,
+                          "count": "sum_c reach_c x (M-1) x (11 probes x 4 B + 64-B prefix set)",
+                          "peak_basis": "LDS reads: 256 CU x 256 B/clk x 2.4 GHz",
+                          "compares_per_launch": cmp_per_sel,
+                          "compare_rate_G": round(cmp_rate, 1),
+                          "unique_fits": uniq, "fronts": len(fronts)},
            "selection": {"ms": round(sel_ms, 4),
                          "what": "whole selNSGA2(2N -> N): ranks, bitset tables, counts, peel, "
                                  "crowding, last-front selection"},

@@ -1521,12 +1521,14 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 const uint32_t* P = (const uint32_t*)(tws + TL.P);
                 const int32_t* R = (const int32_t*)(tws + TL.R);
                 const uint16_t* BK = (const uint16_t*)(tws + TL.BK);
+                timing_begin(ctx, DM_TIME_PEEL);
                 if (m == 2)
                     peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
                 else
                     peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
                                                                      st, countq, lastq, ckey, cq, rankU);
+                timing_end(ctx, DM_TIME_PEEL);
             } else {
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
                     D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);

@@ -118,32 +118,33 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
         ec != EC_MO && !ctx->knobs.disable_pipe) {
         const int nch = parents->dim <= 512 ? 2 : 4;
-        // parent order: the plans sorted by their fitter parent,
-        // so the pairs that share that row are varied back to back by one wave
-        // and the row's repeated reads hit the caches instead of HBM
-        const bool ordered = !ctx->knobs.pipe_noorder && npairs >= 4096 &&
-                             npairs < (1ll << (32 - PF_PAIR_SHIFT));
+        // parent order: the plans' slots sorted by their fitter
+        // parent, so the pairs that share that row are varied together and the
+        // row's repeated reads hit the L2 instead of HBM
+        const bool ordered = !ctx->knobs.pipe_noorder && npairs >= 4096;
         const size_t pb = align_up((size_t)npairs * sizeof(PairPlan), 256);
         const size_t hb = align_up((size_t)(a.np + 1) * 4, 256);
         const size_t kb = align_up((size_t)npairs * 4, 256);
-        char* w = (char*)scratch(ctx, ordered ? 2 * pb + 2 * hb + kb + scan_temp_bytes(a.np) : pb);
+        char* w = (char*)scratch(ctx, ordered ? pb + 2 * hb + 3 * kb + scan_temp_bytes(a.np) : pb);
         if (!w) return DM_ERR_NOMEM;
         PairPlan* plans = (PairPlan*)w;
+        int32_t* order = nullptr;
         // nevals is counted by the plan kernel (spread counters + fold): one
         // same-address atomic per hot-kernel wave serialised 65,536 atomics
         const bool count = ec != EC_NONE && a.nevals;
         if (ordered) {
-            int32_t* hist = (int32_t*)(w + 2 * pb);
-            int32_t* cursor = (int32_t*)(w + 2 * pb + hb);
-            int32_t* keys = (int32_t*)(w + 2 * pb + 2 * hb);
-            void* stemp = w + 2 * pb + 2 * hb + kb;
+            int32_t* hist = (int32_t*)(w + pb);
+            int32_t* start = (int32_t*)(w + pb + hb);
+            int32_t* keys = (int32_t*)(w + pb + 2 * hb);
+            int32_t* tick = (int32_t*)(w + pb + 2 * hb + kb);
+            order = (int32_t*)(w + pb + 2 * hb + 2 * kb);
+            void* stemp = w + pb + 2 * hb + 3 * kb;
             DM_HIP(hipMemsetAsync(hist, 0, (size_t)a.np * 4, ctx->stream));
             launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
-                              hist);
-            int rc = exclusive_scan_i32(ctx->stream, hist, cursor, a.np, nullptr, stemp);
+                              hist, tick);
+            int rc = exclusive_scan_i32(ctx->stream, hist, start, a.np, nullptr, stemp);
             if (rc) return rc;
-            plans = (PairPlan*)(w + pb);
-            launch_plan_order((const PairPlan*)w, keys, cursor, plans, npairs, ctx->stream);
+            launch_plan_order(keys, tick, start, order, npairs, ctx->stream);
         } else {
             launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         }
@@ -173,7 +174,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.ev = a.ev;
         q.bpc = ctx->knobs.pipe_bpc;
         q.depth = ctx->knobs.pipe_depth;
-        q.ordered = ordered ? 1 : 0;
+        q.order = order;
         timing_begin(ctx);
         if (parents->gtype == DM_F64)
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);

@@ -45,12 +45,11 @@ typedef __attribute__((address_space(4))) const uint32_t c4_u32;
 struct PairPlan {
     int32_t s0, s1;    // parent rows
     uint32_t cuts;     // cxTwoPoint slice [cp1, cp2): cp1 | cp2 << 16
-    uint32_t flags;    // PF_*; bits PF_PAIR_SHIFT.. = the pair index (parent-ordered plans)
+    uint32_t flags;    // PF_*
     double f0, f1;     // parents' wvalues[0] (inherited by an unchanged clone)
 };
 static_assert(sizeof(PairPlan) == 32, "PairPlan layout");
 enum : uint32_t { PF_CX = 1, PF_MUT0 = 2, PF_MUT1 = 4, PF_HAS1 = 8, PF_INV0 = 16, PF_INV1 = 32 };
-constexpr int PF_PAIR_SHIFT = 8;  // parent-ordered plans: up to 2^24 pairs
 
 // Scalar (SMEM) load of a plan: wave-uniform index, tracked by lgkmcnt.
 __device__ __forceinline__ PairPlan load_plan(const PairPlan* plans, int64_t p) {
@@ -261,10 +260,11 @@ struct PipeArgs {
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
     int32_t bpc, depth;  // dm_knobs: workgroups per CU, ring depth (0 = defaults)
-    // 1: the plans are in parent order (plan_order_kernel), each carries its
-    // pair index, and a wave takes a contiguous run of them (pairs that share
-    // a parent row back to back: its second read is a cache hit)
-    int32_t ordered;
+    // parent order (nullable): slot j varies pair order[j] (plan_order_kernel);
+    // a workgroup takes a contiguous run of slots, its waves interleaved, so
+    // the pairs that share a parent row are varied together on one CU and the
+    // row's repeated reads hit its L2
+    const int32_t* order;
     Rng rng;
     uint64_t thr_ind;
     double alpha, mu, sigma, w0;
@@ -309,11 +309,12 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     // contiguous run (parent order); the pair of slot j is j, or the index the
     // ordered plan carries
     int64_t j, jend, jstep;
-    if (a.ordered) {
-        const int64_t per = (npairs + nw - 1) / nw;
-        j = wid * per;
-        jend = std::min<int64_t>(npairs, j + per);
-        jstep = 1;
+    if (a.order) {
+        const int64_t wpb = blockDim.x >> 6;
+        const int64_t per = ((npairs + gridDim.x - 1) / gridDim.x + wpb - 1) / wpb * wpb;
+        j = (int64_t)blockIdx.x * per + (threadIdx.x >> 6);
+        jend = std::min<int64_t>(npairs, (int64_t)blockIdx.x * per + per);
+        jstep = wpb;
     } else {
         j = wid;
         jend = npairs;
@@ -324,8 +325,14 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     const int dim = a.dim;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
-    PairPlan pl = load_plan(a.plans, j);
-    PairPlan nx = load_plan(a.plans, j + jstep < jend ? j + jstep : j);
+    // the pair of slot j: j, or order[j] (scalar loads, like the plans)
+    auto pair_of = [&](int64_t jj) -> int64_t {
+        return a.order ? (int64_t)((const c4_u32*)(const void*)a.order)[jj] : jj;
+    };
+    int64_t pcur = pair_of(j);
+    int64_t pnx = pair_of(j + jstep < jend ? j + jstep : j);
+    PairPlan pl = load_plan(a.plans, pcur);
+    PairPlan nx = load_plan(a.plans, pnx);
     // ring of D chunk slots over the chunk sequence (p,0..NCH-1), (p+W,0..), ...
     double y0[D][4], y1[D][4];
 #pragma unroll
@@ -336,8 +343,9 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     for (; j < jend; j += jstep) {
         const bool more = j + jstep < jend;
         const int64_t j2 = j + 2 * jstep;
-        const PairPlan nn = load_plan(a.plans, j2 < jend ? j2 : j);  // two ahead
-        const int64_t p = a.ordered ? (int64_t)(pl.flags >> PF_PAIR_SHIFT) : j;
+        const int64_t pnn = pair_of(j2 < jend ? j2 : j);
+        const PairPlan nn = load_plan(a.plans, pnn);  // two ahead
+        const int64_t p = pcur;
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const uint32_t fl = pl.flags;
         const bool cx = fl & PF_CX, mut0 = fl & PF_MUT0, mut1 = fl & PF_MUT1;
@@ -486,6 +494,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
         }
         pl = nx;
         nx = nn;
+        pcur = pnx;
+        pnx = pnn;
     }
     if (a.nevals && EC != EC_NONE) {
         int64_t tot = evals;
@@ -555,14 +565,16 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 }
 
 // Decisions of every pair (thread per pair), generation_pipe_f64.hip.  With
-// keys / hist (zeroed, one counter per parent row): key[p] = the plan's
-// sort key (its fitter parent) and hist[key] counts the plans per key.
+// keys / hist (zeroed, one counter per parent row): key[p] = the plan's sort
+// key (its fitter parent), tick[p] = its place among the plans of that key
+// (the counter's old value) and hist[key] their count.
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
-                       int32_t* keys = nullptr, int32_t* hist = nullptr);
-// The plans in key order: cursor = the exclusive scan of hist (consumed);
-// ordered[pos] = plans[p] with p in its flags (PF_PAIR_SHIFT).
-void launch_plan_order(const PairPlan* plans, const int32_t* keys, int32_t* cursor,
-                       PairPlan* ordered, int64_t npairs, hipStream_t s);
+                       int32_t* keys = nullptr, int32_t* hist = nullptr,
+                       int32_t* tick = nullptr);
+// Parent order: order[start[key[p]] + tick[p]] = p (start = the exclusive scan
+// of hist).
+void launch_plan_order(const int32_t* keys, const int32_t* tick, const int32_t* start,
+                       int32_t* order, int64_t npairs, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).

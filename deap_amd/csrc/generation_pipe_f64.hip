@@ -13,7 +13,8 @@ namespace dm {
 // Decisions of pair p -> plans[p]; returns the plan's flags.
 __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
                                              int64_t p, int32_t* __restrict__ keys,
-                                             int32_t* __restrict__ hist) {
+                                             int32_t* __restrict__ hist,
+                                             int32_t* __restrict__ tick) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
     const int m = a.nobj;
@@ -78,7 +79,7 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         // fitness: a fitter row is the likelier one to recur in other pairs)
         const int32_t key = pl.f1 > pl.f0 ? s[1] : s[0];
         keys[p] = key;
-        atomicAdd(hist + key, 1);
+        tick[p] = atomicAdd(hist + key, 1);
     }
     return fl;
 }
@@ -90,13 +91,14 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
                                                         long long* __restrict__ count_evals,
                                                         int32_t* __restrict__ keys,
-                                                        int32_t* __restrict__ hist) {
+                                                        int32_t* __restrict__ hist,
+                                                        int32_t* __restrict__ tick) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p, keys, hist);
+        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -106,35 +108,33 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p, keys, hist);
+    if (p < npairs) plan_one(a, plans, p, keys, hist, tick);
 }
 
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
-                       int32_t* keys, int32_t* hist) {
+                       int32_t* keys, int32_t* hist, int32_t* tick) {
     const int64_t npairs = (a.nc + 1) / 2;
     pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals,
-                                                                           keys, hist);
+                                                                           keys, hist, tick);
 }
 
-// Counting-sort scatter of the plans by key.  The order inside a key's run
-// is whatever the atomics give: the processing order never changes a result
-// (every child is a function of its own plan and counters).
-__global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restrict__ plans,
-                                                         const int32_t* __restrict__ keys,
-                                                         int32_t* __restrict__ cursor,
-                                                         PairPlan* __restrict__ ordered,
+// Counting-sort placement by key: slot start[key] + tick of pair p.  The order
+// inside a key's run is whatever the plan kernel's atomics gave: the
+// processing order never changes a result (every child is a function of its
+// own plan and counters).
+__global__ __launch_bounds__(256) void plan_order_kernel(const int32_t* __restrict__ keys,
+                                                         const int32_t* __restrict__ tick,
+                                                         const int32_t* __restrict__ start,
+                                                         int32_t* __restrict__ order,
                                                          int64_t npairs) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npairs) return;
-    PairPlan pl = plans[p];
-    pl.flags |= (uint32_t)p << PF_PAIR_SHIFT;
-    ordered[atomicAdd(cursor + keys[p], 1)] = pl;
+    if (p < npairs) order[start[keys[p]] + tick[p]] = (int32_t)p;
 }
 
-void launch_plan_order(const PairPlan* plans, const int32_t* keys, int32_t* cursor,
-                       PairPlan* ordered, int64_t npairs, hipStream_t s) {
-    plan_order_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(plans, keys, cursor,
-                                                                            ordered, npairs);
+void launch_plan_order(const int32_t* keys, const int32_t* tick, const int32_t* start,
+                       int32_t* order, int64_t npairs, hipStream_t s) {
+    plan_order_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(keys, tick, start,
+                                                                            order, npairs);
 }
 
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
