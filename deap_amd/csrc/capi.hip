@@ -442,6 +442,7 @@ static void read_knobs(dm_knobs& kn) {
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
     kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);
     kn.pipe_noorder = std::getenv("DM_PIPE_NOORDER") != nullptr;
+    kn.pipe_key_fitter = std::getenv("DM_PIPE_KEY_FITTER") != nullptr;
 }
 
 int dm_ctx_reload_knobs(dm_ctx* ctx) {

@@ -60,6 +60,7 @@ struct dm_knobs {
     int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
     int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)
     bool pipe_noorder = false;      // DM_PIPE_NOORDER: C3 plans in pair order (no parent order)
+    bool pipe_key_fitter = false;   // DM_PIPE_KEY_FITTER: parent order keyed by the fitter parent
 };
 
 struct dm_ctx {

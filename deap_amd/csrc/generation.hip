@@ -118,33 +118,44 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
         ec != EC_MO && !ctx->knobs.disable_pipe) {
         const int nch = parents->dim <= 512 ? 2 : 4;
-        // parent order: the plans' slots sorted by their fitter
-        // parent, so the pairs that share that row are varied together and the
-        // row's repeated reads hit the L2 instead of HBM
-        const bool ordered = !ctx->knobs.pipe_noorder && npairs >= 4096;
+        // parent order: the plans sorted by a key parent -- of
+        // the two, the one in more pair slots of this generation (a greedy
+        // vertex cover of the pairs) -- so the pairs that share that row are
+        // varied together and the row's repeated reads hit the L2, not HBM
+        const bool ordered = !ctx->knobs.pipe_noorder && npairs >= 4096 &&
+                             npairs < (1ll << (32 - PF_PAIR_SHIFT));
         const size_t pb = align_up((size_t)npairs * sizeof(PairPlan), 256);
         const size_t hb = align_up((size_t)(a.np + 1) * 4, 256);
         const size_t kb = align_up((size_t)npairs * 4, 256);
-        char* w = (char*)scratch(ctx, ordered ? pb + 2 * hb + 3 * kb + scan_temp_bytes(a.np) : pb);
+        char* w = (char*)scratch(ctx, ordered ? 2 * pb + 3 * hb + 2 * kb +
+                                                    align_up(scan_temp_bytes(a.np), 256) : pb);
         if (!w) return DM_ERR_NOMEM;
         PairPlan* plans = (PairPlan*)w;
-        int32_t* order = nullptr;
         // nevals is counted by the plan kernel (spread counters + fold): one
         // same-address atomic per hot-kernel wave serialised 65,536 atomics
         const bool count = ec != EC_NONE && a.nevals;
         if (ordered) {
-            int32_t* hist = (int32_t*)(w + pb);
-            int32_t* start = (int32_t*)(w + pb + hb);
-            int32_t* keys = (int32_t*)(w + pb + 2 * hb);
-            int32_t* tick = (int32_t*)(w + pb + 2 * hb + kb);
-            order = (int32_t*)(w + pb + 2 * hb + 2 * kb);
-            void* stemp = w + pb + 2 * hb + 3 * kb;
+            PairPlan* sorted = (PairPlan*)(w + pb);
+            int32_t* hist = (int32_t*)(w + 2 * pb);
+            int32_t* start = (int32_t*)(w + 2 * pb + hb);
+            int32_t* keys = (int32_t*)(w + 2 * pb + 2 * hb);
+            int32_t* tick = (int32_t*)(w + 2 * pb + 2 * hb + kb);
+            void* stemp = w + 2 * pb + 2 * hb + 2 * kb;
             DM_HIP(hipMemsetAsync(hist, 0, (size_t)a.np * 4, ctx->stream));
-            launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
-                              hist, tick);
+            if (!ctx->knobs.pipe_key_fitter) {
+                int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
+                DM_HIP(hipMemsetAsync(deg, 0, (size_t)a.np * 4, ctx->stream));
+                launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
+                                  nullptr, deg, nullptr);
+                launch_plan_degree_keys(plans, deg, keys, tick, hist, npairs, ctx->stream);
+            } else {
+                launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
+                                  hist, tick);
+            }
             int rc = exclusive_scan_i32(ctx->stream, hist, start, a.np, nullptr, stemp);
             if (rc) return rc;
-            launch_plan_order(keys, tick, start, order, npairs, ctx->stream);
+            launch_plan_order(plans, keys, tick, start, sorted, npairs, ctx->stream);
+            plans = sorted;
         } else {
             launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
         }
@@ -174,7 +185,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.ev = a.ev;
         q.bpc = ctx->knobs.pipe_bpc;
         q.depth = ctx->knobs.pipe_depth;
-        q.order = order;
+        q.ordered = ordered ? 1 : 0;
         timing_begin(ctx);
         if (parents->gtype == DM_F64)
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);

@@ -45,11 +45,12 @@ typedef __attribute__((address_space(4))) const uint32_t c4_u32;
 struct PairPlan {
     int32_t s0, s1;    // parent rows
     uint32_t cuts;     // cxTwoPoint slice [cp1, cp2): cp1 | cp2 << 16
-    uint32_t flags;    // PF_*
+    uint32_t flags;    // PF_*; parent-ordered plans: the pair index << PF_PAIR_SHIFT
     double f0, f1;     // parents' wvalues[0] (inherited by an unchanged clone)
 };
 static_assert(sizeof(PairPlan) == 32, "PairPlan layout");
 enum : uint32_t { PF_CX = 1, PF_MUT0 = 2, PF_MUT1 = 4, PF_HAS1 = 8, PF_INV0 = 16, PF_INV1 = 32 };
+constexpr int PF_PAIR_SHIFT = 8;  // parent-ordered plans: the pair index above the flags
 
 // Scalar (SMEM) load of a plan: wave-uniform index, tracked by lgkmcnt.
 __device__ __forceinline__ PairPlan load_plan(const PairPlan* plans, int64_t p) {
@@ -260,11 +261,11 @@ struct PipeArgs {
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
     int32_t bpc, depth;  // dm_knobs: workgroups per CU, ring depth (0 = defaults)
-    // parent order (nullable): slot j varies pair order[j] (plan_order_kernel);
-    // a workgroup takes a contiguous run of slots, its waves interleaved, so
-    // the pairs that share a parent row are varied together on one CU and the
-    // row's repeated reads hit its L2
-    const int32_t* order;
+    // 1: the plans are in parent order (plan_order_kernel), each carries its
+    // pair index (flags >> PF_PAIR_SHIFT); a workgroup takes a contiguous run
+    // of them, its waves interleaved, so the pairs that share a parent row are
+    // varied together on one CU and the row's repeated reads hit its L2
+    int32_t ordered;
     Rng rng;
     uint64_t thr_ind;
     double alpha, mu, sigma, w0;
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     // contiguous run (parent order); the pair of slot j is j, or the index the
     // ordered plan carries
     int64_t j, jend, jstep;
-    if (a.order) {
+    if (a.ordered) {
         const int64_t wpb = blockDim.x >> 6;
         const int64_t per = ((npairs + gridDim.x - 1) / gridDim.x + wpb - 1) / wpb * wpb;
         j = (int64_t)blockIdx.x * per + (threadIdx.x >> 6);
@@ -325,14 +326,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     const int dim = a.dim;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
-    // the pair of slot j: j, or order[j] (scalar loads, like the plans)
-    auto pair_of = [&](int64_t jj) -> int64_t {
-        return a.order ? (int64_t)((const c4_u32*)(const void*)a.order)[jj] : jj;
-    };
-    int64_t pcur = pair_of(j);
-    int64_t pnx = pair_of(j + jstep < jend ? j + jstep : j);
-    PairPlan pl = load_plan(a.plans, pcur);
-    PairPlan nx = load_plan(a.plans, pnx);
+    PairPlan pl = load_plan(a.plans, j);
+    PairPlan nx = load_plan(a.plans, j + jstep < jend ? j + jstep : j);
     // ring of D chunk slots over the chunk sequence (p,0..NCH-1), (p+W,0..), ...
     double y0[D][4], y1[D][4];
 #pragma unroll
@@ -343,9 +338,8 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     for (; j < jend; j += jstep) {
         const bool more = j + jstep < jend;
         const int64_t j2 = j + 2 * jstep;
-        const int64_t pnn = pair_of(j2 < jend ? j2 : j);
-        const PairPlan nn = load_plan(a.plans, pnn);  // two ahead
-        const int64_t p = pcur;
+        const PairPlan nn = load_plan(a.plans, j2 < jend ? j2 : j);  // two ahead
+        const int64_t p = a.ordered ? (int64_t)(pl.flags >> PF_PAIR_SHIFT) : j;
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const uint32_t fl = pl.flags;
         const bool cx = fl & PF_CX, mut0 = fl & PF_MUT0, mut1 = fl & PF_MUT1;
@@ -494,8 +488,6 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
         }
         pl = nx;
         nx = nn;
-        pcur = pnx;
-        pnx = pnn;
     }
     if (a.nevals && EC != EC_NONE) {
         int64_t tot = evals;
@@ -571,10 +563,15 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
                        int32_t* keys = nullptr, int32_t* hist = nullptr,
                        int32_t* tick = nullptr);
-// Parent order: order[start[key[p]] + tick[p]] = p (start = the exclusive scan
-// of hist).
-void launch_plan_order(const int32_t* keys, const int32_t* tick, const int32_t* start,
-                       int32_t* order, int64_t npairs, hipStream_t s);
+// Parent order: ordered[start[key[p]] + tick[p]] = plans[p] with p in its
+// flags (start = the exclusive scan of hist).
+void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
+                       const int32_t* start, PairPlan* ordered, int64_t npairs, hipStream_t s);
+// Degree keys (the default; DM_PIPE_KEY_FITTER keys by the fitter parent in
+// the plan kernel instead): after launch_pair_plans(..., hist = deg) counted
+// every parent slot, key[p] = the parent of more slots, ticketed into hist2.
+void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, int32_t* keys,
+                             int32_t* tick, int32_t* hist2, int64_t npairs, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).

@@ -74,12 +74,16 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     pl.f0 = a.pwv[(int64_t)s[0] * m];
     pl.f1 = a.pwv[(int64_t)s[1] * m];
     plans[p] = pl;
-    if (keys) {
+    if (keys && tick) {
         // sort key: the fitter parent (tournament winners repeat with their
         // fitness: a fitter row is the likelier one to recur in other pairs)
         const int32_t key = pl.f1 > pl.f0 ? s[1] : s[0];
         keys[p] = key;
         tick[p] = atomicAdd(hist + key, 1);
+    } else if (hist) {
+        // degree keys (plan_degree_key_kernel): count both parents' slots
+        atomicAdd(hist + s[0], 1);
+        if (has1) atomicAdd(hist + s[1], 1);
     }
     return fl;
 }
@@ -118,23 +122,51 @@ void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals
                                                                            keys, hist, tick);
 }
 
-// Counting-sort placement by key: slot start[key] + tick of pair p.  The order
-// inside a key's run is whatever the plan kernel's atomics gave: the
-// processing order never changes a result (every child is a function of its
-// own plan and counters).
-__global__ __launch_bounds__(256) void plan_order_kernel(const int32_t* __restrict__ keys,
+// Counting-sort placement of the plans by key: slot start[key] + tick of pair
+// p, the plan copied with p in its flags (the hot kernel then reads its plans
+// contiguously; an index array read before each plan was 1.2 % slower,
+// profiles/r04i).  The order inside a key's run is whatever the plan
+// kernel's atomics gave: the processing order never changes a result (every
+// child is a function of its own plan and counters).
+__global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restrict__ plans,
+                                                         const int32_t* __restrict__ keys,
                                                          const int32_t* __restrict__ tick,
                                                          const int32_t* __restrict__ start,
-                                                         int32_t* __restrict__ order,
+                                                         PairPlan* __restrict__ ordered,
                                                          int64_t npairs) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < npairs) order[start[keys[p]] + tick[p]] = (int32_t)p;
+    if (p >= npairs) return;
+    PairPlan pl = plans[p];
+    pl.flags |= (uint32_t)p << PF_PAIR_SHIFT;
+    ordered[start[keys[p]] + tick[p]] = pl;
 }
 
-void launch_plan_order(const int32_t* keys, const int32_t* tick, const int32_t* start,
-                       int32_t* order, int64_t npairs, hipStream_t s) {
-    plan_order_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(keys, tick, start,
-                                                                            order, npairs);
+// Degree keys: the parent that appears in more pair slots of this generation
+// (a greedy vertex cover of the pairs: fewer distinct key rows than the fitter
+// parent gives), ticketed into the zeroed hist2.
+__global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __restrict__ plans,
+                                                              const int32_t* __restrict__ deg,
+                                                              int32_t* __restrict__ keys,
+                                                              int32_t* __restrict__ tick,
+                                                              int32_t* __restrict__ hist2,
+                                                              int64_t npairs) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npairs) return;
+    const int32_t s0 = plans[p].s0, s1 = plans[p].s1;
+    const int32_t key = deg[s1] > deg[s0] ? s1 : s0;
+    keys[p] = key;
+    tick[p] = atomicAdd(hist2 + key, 1);
+}
+void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, int32_t* keys,
+                             int32_t* tick, int32_t* hist2, int64_t npairs, hipStream_t s) {
+    plan_degree_key_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
+        plans, deg, keys, tick, hist2, npairs);
+}
+
+void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
+                       const int32_t* start, PairPlan* ordered, int64_t npairs, hipStream_t s) {
+    plan_order_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(plans, keys, tick,
+                                                                            start, ordered, npairs);
 }
 
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
