@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-4 GPU-box runner.  STEPS (space separated) picks the steps, e.g.
+#   STEPS="pytest smoke bench_c3" TAG=r04k tools_gpu/r04.sh
+# Every GPU step runs under its own timeout; the script stops at the first
+# failing step (fault / abort / timeout / test failure) and starts nothing
+# more on the GPU.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r04}
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "$name rc=$rc"; tail -15 $OUT/$name.err; tail -15 $OUT/$name.out; exit $rc; fi
+  tail -2 $OUT/$name.out | cut -c1-700
+}
+KT="rocprofv3 --kernel-trace --stats --output-format csv -o run"
+for s in ${STEPS:-pytest smoke bench_c3}; do
+  case $s in
+    pytest) step pytest 900 python -u -m pytest tests -m gpu -v -rf -x --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench_c3) step bench_c3 400 python bench.py --steps 20 --warmup 5 ;;
+    bench_c3q) step bench_c3q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_c2) step bench_c2 200 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline ;;
+    bench_c4) step bench_c4 400 python bench.py --islands 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_c5) step bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
+    bench_c5q) step bench_c5q 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    bench_c5x) step bench_c5x 600 python bench.py --config c5x --steps 5 --warmup 2 ;;
+    kt_c3) step kt_c3 300 $KT -d $OUT/kt_c3 -- python3 bench.py --steps 12 --warmup 2 --no-cpu-baseline ;;
+    kt_c2) step kt_c2 300 $KT -d $OUT/kt_c2 -- python3 bench.py --config c2 --steps 20 --warmup 2 --no-cpu-baseline ;;
+    kt_c4) step kt_c4 400 $KT -d $OUT/kt_c4 -- python3 bench.py --islands 8 --steps 10 --warmup 0 --no-cpu-baseline ;;
+    kt_c5) step kt_c5 400 $KT -d $OUT/kt_c5 -- python3 bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_c3|pmc_c2)
+      cfg=${s#pmc_}
+      for pmc in FETCH_SIZE WRITE_SIZE; do
+        step pmc_${cfg}_$pmc 180 rocprofv3 --pmc $pmc -d $OUT/pmc_${cfg}_$pmc -o run --output-format csv -- python3 bench.py --config $cfg --steps 6 --warmup 1 --no-cpu-baseline
+      done ;;
+    pmc_c5peel)
+      step pmc_c5peel 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d $OUT/pmc_c5peel -o run --output-format csv -- python3 bench.py --config c5 --steps 3 --warmup 2 --no-cpu-baseline
+      step c5peel_json 60 python3 tools_gpu/c5_peel_pmc.py $OUT/pmc_c5peel $OUT/c5_peel_pmc.json "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU, bench.py --config c5 (gpurun_out/$(basename $OUT))"
+      mkdir -p profiles && cp $OUT/c5_peel_pmc.json profiles/c5_peel_pmc.json ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
