@@ -630,13 +630,21 @@ template <int IT>
 struct PeelPre {
     int32_t cnt[IT], vu[IT], gs[IT];
 };
+// The table peel's member records (MemberTab): a released v's record qrec[v]
+// is copied to crec[slot] beside its candidate key, so that the ordering
+// reads it in slot order with the key instead of gathering it by q.
+struct CandRec {
+    const int4* qrec;
+    int4* crec;
+};
 template <bool COH, int PW>
 __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW], int64_t vbase,
                              const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
                              int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
-                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre = nullptr);
+                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre = nullptr,
+                             CandRec cr = CandRec{nullptr, nullptr});
 
 // Slice y of the nsl slices of row segment s for the front of sF unique
 // fitnesses starting at sust in ulist / mrow (front number snf).
@@ -727,7 +735,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
                              int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
-                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre) {
+                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre, CandRec cr) {
     constexpr int PEEL_IT = PeelSmallT<PW * 64>::IT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -741,6 +749,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
     // waves on the large fronts)
     bool fresh[PEEL_IT];
     int32_t lk[PEEL_IT], vu[PEEL_IT];
+    int4 rq[PEEL_IT];
     unsigned long long fm[PEEL_IT];
 #pragma unroll
     for (int it = 0; it < PEEL_IT; ++it) {
@@ -776,6 +785,8 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
             }
         }
         lk[it] = l;
+        // in flight across the slot reservation below (barriers wait on LDS only)
+        if (cr.crec && fresh[it]) rq[it] = cr.qrec[v];
         vu[it] = fresh[it] ? (pre ? pre->vu[it] : sigma[v]) : 0;
         fm[it] = __ballot(fresh[it]);
         int64_t gs = fresh[it] ? (pre ? pre->gs[it] : gsize[vu[it]]) : 0;
@@ -809,6 +820,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         if (!BD_OK(slot, U, "release slot") || !BD_OK(vu[it], U, "release vu")) continue;
         cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
         cst<COH>(cq + slot, (int32_t)v);
+        if (cr.crec) cr.crec[slot] = rq[it];
         cst<COH>(rankU + vu[it], snf + 1);
     }
     __syncthreads();  // the LDS is reused by the caller's next task
@@ -867,11 +879,10 @@ __device__ unsigned int g_pprof_n;
 #endif
 template <int F>
 __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_kernel(
-    const int4* __restrict__ S, const int2* __restrict__ span, const uint32_t* __restrict__ P,
-    const int32_t* __restrict__ R, const uint16_t* __restrict__ BK, const int2* __restrict__ mrow,
-    const int32_t* __restrict__ gsize,
+    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
+    const int4* __restrict__ mtab, const int32_t* __restrict__ gsize,
     const int32_t* __restrict__ sigma, FrontState* st, int32_t* countq, unsigned long long* lastq,
-    uint64_t* ckey, int32_t* cq, int32_t* rankU) {
+    uint64_t* ckey, int32_t* cq, int32_t* rankU, CandRec cr) {
     static_assert(PEEL_WAVES * 64 == BD_CW, "one thread per v of the chunk (sorted ranks, release)");
     constexpr int PW = BD_CW / 64;  // words of a chunk
     __shared__ int32_t sR[F][BD_RP];
@@ -916,13 +927,15 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
     const int64_t j0s = blockIdx.y * slen;
     const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
-    const int2* members = mrow + sust;  // (row in q order, 512-v halves it reaches)
+    // (reach, last q of the objective-0 tie group, ranks 1 and 2) per member,
+    // front order: gathered once per front by the ordering (member_tab)
+    const int4* members = mtab + sust;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int STEP = PEEL_WAVES * 64;
     constexpr int WIN = 2048;       // 4 members per thread (8 spilled, and so did
                                     // loading the first window in the prologue)
     constexpr int WR = WIN / STEP;  // members per thread per window
-    static_assert(WIN * sizeof(int2) <= sizeof(PeelLdsT<BD_CW>), "window list in the release's LDS");
+    static_assert(WIN * sizeof(int4) <= sizeof(PeelLdsT<BD_CW>), "window list in the release's LDS");
 #pragma unroll
     for (int f = 0; f < F; ++f) sR[f][bd_rpad(threadIdx.x)] = rr[f];
     bd_load_buckets<F>(BK, c, sB);
@@ -937,25 +950,25 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     }
     const int64_t v0 = c * BD_CW;
     // The slice is taken in windows of WIN members.  A window's members whose
-    // row reaches chunk c are compacted, in front order, into LDS as (row,
-    // front position) -- the release's LDS, not yet in use -- and processed
+    // row reaches chunk c are compacted, in front order, into LDS as (ranks,
+    // tie-group end, front position) -- the release's LDS, not yet in use --
+    // and processed
     // 64 at a time, so no group carries members that do not reach the chunk
     // (a front's members reach chunks up to their objective-0 position: in
     // front order about half of a group's lanes were idle on the high
     // chunks).  Positions rise within a group, so the top set bit of a
     // transposed word is its last dominator, read back by a lane shuffle.
-    int2* sM = reinterpret_cast<int2*>(&L);
+    int4* sM = reinterpret_cast<int4*>(&L);
     PPROF_T(pt1);
     for (int64_t wb = j0s; wb < Fm; wb += WIN) {
         uint64_t bal[WR];
-        int2 mr[WR];
+        int4 mr[WR];
         int nw = 0;
 #pragma unroll
         for (int r = 0; r < WR; ++r) {
             const int64_t j = wb + (int64_t)(wave * WR + r) * 64 + lane;
-            mr[r] = j < Fm && BD_OK(sust + j, U, "peel member") ? members[j] : make_int2(0, 0);
-            if (!BD_OK(mr[r].x, U, "peel member row")) mr[r] = make_int2(0, 0);
-            bal[r] = __ballot(j < Fm && c < mr[r].y);
+            mr[r] = j < Fm && BD_OK(sust + j, U, "peel member") ? members[j] : make_int4(0, 0, 0, 0);
+            bal[r] = __ballot(j < Fm && c < mr[r].x);
             nw += __popcll(bal[r]);
         }
         if (lane == 0) Sm.wcnt[0][wave] = nw;
@@ -972,20 +985,18 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
         for (int r = 0; r < WR; ++r) {
             if ((bal[r] >> lane) & 1)
                 sM[base + __popcll(bal[r] & below)] =
-                    make_int2(mr[r].x, (int32_t)(wb - j0s + (int64_t)(wave * WR + r) * 64 + lane));
+                    make_int4(mr[r].z, mr[r].w, mr[r].y,
+                              (int32_t)(wb - j0s + (int64_t)(wave * WR + r) * 64 + lane));
             base += __popcll(bal[r]);
         }
         __syncthreads();
-        auto mget = [&](int g) { return g < total ? sM[g] : make_int2(0, -1); };
-        int2 mA = mget(wave * 64 + lane);
-        int4 suA = S[mA.x];
-        int2 spA = span[mA.x];
+        // (rank 1, rank 2, tie-group end, front position in the slice)
+        auto mget = [&](int g) { return g < total ? sM[g] : make_int4(0, 0, 0, -1); };
         for (int g0 = wave * 64; g0 < total; g0 += STEP) {
-            const int2 mB = mget(g0 + STEP + lane);
-            const int4 suB = S[mB.x];
-            const int2 spB = span[mB.x];
-            const bool has = mA.y >= 0;
-            const int32_t lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)spA.y - v0, BD_CW));
+            const int4 mA = mget(g0 + lane);
+            const bool has = mA.w >= 0;
+            const int4 suA = make_int4(mA.x, mA.y, 0, 0);
+            const int32_t lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mA.z - v0, BD_CW));
             int k[F];
             if (has && lim >= 0) {
                 bd_row_k<F>(suA, sR, sB, sh, k);
@@ -1009,7 +1020,7 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
                 hi[2 * i + 1] = w[i].w;
             }
             tr.run<8>(lo, hi);  // lane v: bit i <-> group member i dominates v
-            const int32_t posA = (int32_t)(j0s + mA.y);
+            const int32_t posA = (int32_t)(j0s + mA.w);
 #pragma unroll
             for (int w2 = 0; w2 < 8; ++w2) {
                 dec[w2] += __popc(lo[w2]) + __popc(hi[w2]);
@@ -1017,15 +1028,12 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
                 const int32_t pt = __shfl(posA, top);
                 if (lo[w2] | hi[w2]) last[w2] = pt;
             }
-            mA = mB;
-            suA = suB;
-            spA = spB;
         }
         __syncthreads();  // the window's list is read out before the next (or the release) reuses it
     }
     PPROF_T(pt2);
     peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
-                            snf, nsl, L, Sm, &pre);
+                            snf, nsl, L, Sm, &pre, cr);
 #ifdef DM_PEEL_PROF
     PPROF_T(pt3);
     if (threadIdx.x == 0) {
@@ -1045,10 +1053,27 @@ __device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const 
     const int32_t r = pos[u];
     return make_int2(r, nseg[r / (64 * TD_WPW)]);
 }
+// What the table-fed peel needs of a member -- (reach, last q of its
+// objective-0 tie group, ranks of objectives 1 and 2) -- built per q once per
+// selection (member_rec_kernel) and copied into front order by the ordering,
+// instead of gathered from three arrays by every chunk's workgroup.
+struct MemberTab {
+    int4* out;          // [U] records in front order (null: the D peel, which reads mrow)
+    const int4* qrec;   // [U] records in q order
+    const int4* crec;   // the candidates' records in slot order (peel_release)
+};
+__global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t* nseg, int64_t U,
+                                  int4* qrec) {
+    DGRID_LOOP(q, U) {
+        const int4 s = S[q];
+        qrec[q] = make_int4(nseg[q / (64 * TD_WPW)], span[q].y, s.x, s.y);
+    }
+}
 
 template <int NT, int E, bool COH>
 __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2* mout,
-                             const int32_t* pos, const int32_t* nseg, uint64_t* lds) {
+                             const int32_t* pos, const int32_t* nseg, uint64_t* lds,
+                             const MemberTab& mt, int4* tout) {
     uint64_t k[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -1062,7 +1087,11 @@ __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2
         if (i < n) {
             const int32_t u = (int32_t)(uint32_t)k[e];
             cst<COH>(out + i, u);
-            cst2<COH>(mout + i, member_row(u, pos, nseg));
+            if (tout) {
+                tout[i] = mt.qrec[pos[u]];
+            } else {
+                cst2<COH>(mout + i, member_row(u, pos, nseg));
+            }
         }
     }
 }
@@ -1120,7 +1149,7 @@ template <int NT, int CAP, bool COH>
 __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t* cq,
                             int32_t* ulist, int2* mrow, const int32_t* pos, const int32_t* nseg,
                             int32_t* fstarts, int presorted, OrderLds<CAP>& lds, int32_t* part,
-                            OrderScalars& sc) {
+                            OrderScalars& sc, const MemberTab& mt) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         const int32_t done = cld<COH>(&st->done), ovf = cld<COH>(&st->overflow);
@@ -1144,12 +1173,17 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     }
     int32_t* out = ulist + sc.snstart;
     int2* mout = mrow + sc.snstart;
+    int4* tout = mt.out ? mt.out + sc.snstart : nullptr;
     bool sorted_here = false;
     if (presorted) {
         for (int i = tid; i < n; i += NT) {
             const int32_t u = (int32_t)(uint32_t)cld<COH>(ckey + i);
             cst<COH>(out + i, u);
-            cst2<COH>(mout + i, member_row(u, pos, nseg));
+            if (tout) {
+                tout[i] = mt.qrec[pos[u]];
+            } else {
+                cst2<COH>(mout + i, member_row(u, pos, nseg));
+            }
         }
         sorted_here = true;
     } else if (sc.sF <= CAP) {
@@ -1159,14 +1193,24 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
         __syncthreads();
         uint64_t key[E];
         int32_t qv[E], slot[E];
+        // the first PF candidates' records (slot order, beside the keys) are
+        // fetched here, in flight across the binning's barriers (they wait
+        // on LDS only)
+        constexpr int PF = E < 4 ? E : 4;
+        int4 rec[PF];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int i = tid + e * NT;
             if (i < n) {
                 key[e] = cld<COH>(ckey + i);
                 qv[e] = cld<COH>(cq + i);
-                slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
+                if (e < PF && tout) rec[e] = mt.crec[i];
             }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = tid + e * NT;
+            if (i < n) slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
         }
         __syncthreads();
         // exclusive prefix of the bin counts: thread t owns C consecutive bins
@@ -1194,6 +1238,7 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
                 if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
             }
             __syncthreads();
+            // ranks first, then the record copies as one batch of loads
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const int i = tid + e * NT;
@@ -1203,7 +1248,17 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
                     int32_t r = beg;
                     for (int32_t j = beg; j < end; ++j) r += lds.cs.tmp[j] < vu ? 1 : 0;
                     cst<COH>(out + r, vu);
-                    cst2<COH>(mout + r, make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
+                    slot[e] = r;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = tid + e * NT;
+                if (i < n) {
+                    if (tout)
+                        tout[slot[e]] = e < PF ? rec[e] : mt.crec[i];
+                    else
+                        cst2<COH>(mout + slot[e], make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
                 }
             }
             sorted_here = true;
@@ -1213,16 +1268,16 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     if (!sorted_here) {
         uint64_t* keys = lds.keys;
         if (n <= NT) {
-            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys);
+            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
         } else if (n <= 2 * NT) {
-            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys);
+            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
         } else if (n <= 4 * NT) {
-            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys);
+            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
         } else if (n <= 8 * NT) {
-            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys);
+            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
         } else {
             static_assert(CAP <= 16 * NT, "order capacity exceeds the bitonic sizes");
-            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys);
+            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
         }
     }
     if (tid == 0) {
@@ -1250,18 +1305,23 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
                                                            const int32_t* cq, int32_t* ulist,
                                                            int2* mrow, const int32_t* pos,
                                                            const int32_t* nseg, int32_t* fstarts,
-                                                           int presorted) {
+                                                           int presorted, MemberTab mt) {
     __shared__ OrderLds<ORDER_CAP> lds;
     __shared__ int32_t part[1024];
     __shared__ OrderScalars sc;
     order_front<1024, ORDER_CAP, false>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, presorted,
-                                        lds, part, sc);
+                                        lds, part, sc, mt);
 }
 
 __global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, const int32_t* pos,
-                                   const int32_t* nseg, int2* mrow) {
+                                   const int32_t* nseg, int2* mrow, MemberTab mt) {
     const int64_t F = *Fp;
-    DGRID_LOOP(j, F) mrow[j] = member_row(ulist[j], pos, nseg);
+    DGRID_LOOP(j, F) {
+        if (mt.out)
+            mt.out[j] = mt.qrec[pos[ulist[j]]];
+        else
+            mrow[j] = member_row(ulist[j], pos, nseg);
+    }
 }
 
 __global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int64_t* sorted0p,
@@ -1290,7 +1350,7 @@ __global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int6
 // last front, then the scratch shared by the rank sorts and the peel loop.
 struct FastLayout {
     int64_t NB, NG, NQ, ngroups, Upad;  // NG: 512-v segments (tri_dom), NQ: TW-word lines (peel)
-    size_t part, S, sigma, pos, nseg, toff, counter, mrow, countq, cq, work, total;
+    size_t part, S, sigma, pos, nseg, toff, counter, mrow, mtab, qrec, crec, countq, cq, work, total;
 };
 // elements of the rank pass's key / value buffers: the population (objective
 // 0's q order) or the M-1 <= 3 objectives' unique values sorted as one batch
@@ -1327,6 +1387,9 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
     L.toff = take((size_t)(L.ngroups + 1) * 4);
     L.counter = take(4);
     L.mrow = take((size_t)U * 8);
+    L.mtab = take((size_t)U * 16);
+    L.qrec = take((size_t)U * 16);
+    L.crec = take((size_t)U * 16);
     L.countq = take((size_t)U * 4);
     L.cq = take((size_t)U * 4);
     L.work = take(std::max(ranks_work_bytes(n, U), fronts_work_bytes(U)));
@@ -1490,7 +1553,19 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     void* rtemp = p;
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
-    member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
+    // table-fed peel: the bitset pass's tables in the part region
+    const bool tab = fast_table_peel(ctx, m);
+    const BitdomLayout TL = bitdom_layout(U, m);
+    const char* tws = ws + L.part;
+    int4* mtab = (int4*)(ws + L.mtab);
+    int4* qrec = (int4*)(ws + L.qrec);
+    int4* crec = (int4*)(ws + L.crec);
+    if (tab)
+        member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
+                                                 nseg, U, qrec);
+    const MemberTab mt{tab ? mtab : nullptr, qrec, crec};
+    const CandRec cr{qrec, crec};
+    member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow, mt);
     // status word and the first front starts come back together: when the
     // peel is done they are usually all that is needed (one round trip)
     char* hbuf = (char*)pinned(ctx, 2048);
@@ -1498,10 +1573,6 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     FrontState* hst = (FrontState*)hbuf;
     int32_t* hfs = (int32_t*)(hbuf + 256);
     const int64_t npre = std::min<int64_t>((2048 - 256) / 4, U + 2);
-    // table-fed peel: the bitset pass's tables in the part region
-    const bool tab = fast_table_peel(ctx, m);
-    const BitdomLayout TL = bitdom_layout(U, m);
-    const char* tws = ws + L.part;
     // launch pairs (peel, order) per front: first status check after as many
     // fronts as the previous call needed
     // (the previous call's front count + 1, so that a selection like the last
@@ -1516,24 +1587,22 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
         for (int b = 0; b < batch; ++b) {
             if (tab) {
                 const dim3 g((unsigned)((TL.NG + 7) & ~7ll), PEEL_SLICES);
-                const int4* S = (const int4*)(ws + L.S);
-                const int2* span = (const int2*)(tws + TL.span);
                 const uint32_t* P = (const uint32_t*)(tws + TL.P);
                 const int32_t* R = (const int32_t*)(tws + TL.R);
                 const uint16_t* BK = (const uint16_t*)(tws + TL.BK);
                 timing_begin(ctx, DM_TIME_PEEL);
                 if (m == 2)
-                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
-                                                                     st, countq, lastq, ckey, cq, rankU);
+                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(P, R, BK, mtab, gsize, sigma,
+                                                                     st, countq, lastq, ckey, cq, rankU, cr);
                 else
-                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(S, span, P, R, BK, mrow, gsize, sigma,
-                                                                     st, countq, lastq, ckey, cq, rankU);
+                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(P, R, BK, mtab, gsize, sigma,
+                                                                     st, countq, lastq, ckey, cq, rankU, cr);
                 timing_end(ctx, DM_TIME_PEEL);
             } else {
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
                     D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
             }
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0, mt);
         }
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
@@ -1546,7 +1615,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
             DM_HIP(hipMemsetAsync(vals, 0, (size_t)nc * 4, s));
             int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, nc, 0, 64, rtemp);
             if (rc) return rc;
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1, mt);
             DM_LAUNCH_CHECK();
         }
         // next batch from what is left: fronts grow along the peel, so the
