@@ -89,6 +89,12 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #define DM_BITS_NTLOAD 0  // non-temporal parent-row loads in the fused kernel (A/B)
 #endif
 
+// Wave priority over the decision chain (0 disables; A/B r04 c2prio: 1 and
+// 3 both -1.3 to -2 % kernel time; keeping it through the flip masks: no gain)
+#ifndef DM_BITS_PRIO
+#define DM_BITS_PRIO 1
+#endif
+
 #ifndef DM_BITS_PP
 #define DM_BITS_PP 4  // pairs per wave (tools_gpu/bwtest5.hip: 2-4 best)
 #endif
@@ -486,8 +492,16 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
     int evals = 0;
     if (grp < ngroups) {  // one group per wave
         BitsGroup<PP> g;
+#if DM_BITS_PRIO
+        // the decision chain (Philox -> aspirant keys -> tournament) gates the
+        // wave's row loads: it issues ahead of the other waves' streaming work
+        __builtin_amdgcn_s_setprio(DM_BITS_PRIO);
+#endif
         const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
         bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
+#if DM_BITS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
             flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
         evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
