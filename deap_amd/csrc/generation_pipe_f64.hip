@@ -20,7 +20,60 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     const int m = a.nobj;
     const uint32_t np = (uint32_t)a.np;
     int32_t s[2];
-    for (int h = 0; h < (has1 ? 2 : 1); ++h) {
+    // One objective, t <= 8 (C3, C4): every aspirant of both tournaments is
+    // drawn first and their fitnesses / validities loaded together, then the
+    // tournaments run in registers -- one round of random loads instead of a
+    // chain of 2t dependent ones (the same aspirants, the same first-drawn-wins
+    // rule).
+    bool fast = a.sel == DM_SEL_TOURNAMENT && m == 1 && a.tournsize >= 1 && a.tournsize <= 8;
+    double fw[2] = {0.0, 0.0};
+    uint8_t vw[2] = {1, 1};
+    if (fast) {
+        constexpr int TM = 8;
+        const int t = a.tournsize;
+        int32_t kk[2][TM];
+        double ff[2][TM];
+        uint8_t vv[2][TM];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = (uint32_t)(h ? c1 : c0);
+            u32x4 w{};
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                if (j < t && (h == 0 || has1)) {
+                    if (!(j & 1)) w = a.rng(ST_SEL, c, (uint32_t)(j >> 1));
+                    kk[h][j] = (int32_t)((j & 1) ? bounded64(w.z, w.w, np) : bounded64(w.x, w.y, np));
+                } else {
+                    kk[h][j] = 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+                if (j < t && (h == 0 || has1)) {
+                    ff[h][j] = a.pwv[kk[h][j]];
+                    vv[h][j] = a.pvalid[kk[h][j]];
+                }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int32_t best = kk[h][0];
+            double fb = ff[h][0];
+            uint8_t vb = vv[h][0];
+#pragma unroll
+            for (int j = 1; j < TM; ++j)
+                if (j < t && (h == 0 || has1) && !(ff[h][j] == fb) && !(ff[h][j] <= fb)) {
+                    best = kk[h][j];
+                    fb = ff[h][j];
+                    vb = vv[h][j];
+                }
+            s[h] = best;
+            fw[h] = fb;
+            vw[h] = vb;
+        }
+    }
+    for (int h = 0; h < (has1 ? 2 : 1) && !fast; ++h) {
         const uint32_t c = (uint32_t)(h ? c1 : c0);
         if (a.sel == DM_SEL_RANDOM) {
             const u32x4 w = a.rng(ST_SEL, c, 0);
@@ -64,15 +117,24 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         if (has1 && (uint64_t)a.rng(ST_MUT, (uint32_t)c1, 0).x < a.thr_mut) fl |= PF_MUT1;
     }
     const bool cx = fl & PF_CX;
-    if (cx || (fl & PF_MUT0) || !a.pvalid[s[0]]) fl |= PF_INV0;
-    if (has1 && (cx || (fl & PF_MUT1) || !a.pvalid[s[1]])) fl |= PF_INV1;
+    if (!fast) {
+        vw[0] = a.pvalid[s[0]];
+        vw[1] = a.pvalid[s[1]];
+        fw[0] = a.pwv[(int64_t)s[0] * m];
+        fw[1] = a.pwv[(int64_t)s[1] * m];
+    } else if (!has1) {
+        vw[1] = vw[0];
+        fw[1] = fw[0];
+    }
+    if (cx || (fl & PF_MUT0) || !vw[0]) fl |= PF_INV0;
+    if (has1 && (cx || (fl & PF_MUT1) || !vw[1])) fl |= PF_INV1;
     PairPlan pl;
     pl.s0 = s[0];
     pl.s1 = s[1];
     pl.cuts = cuts;
     pl.flags = fl;
-    pl.f0 = a.pwv[(int64_t)s[0] * m];
-    pl.f1 = a.pwv[(int64_t)s[1] * m];
+    pl.f0 = fw[0];
+    pl.f1 = fw[1];
     plans[p] = pl;
     if (keys && tick) {
         // sort key: the fitter parent (tournament winners repeat with their
