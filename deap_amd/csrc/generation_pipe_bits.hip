@@ -85,8 +85,12 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #define DM_BITS_ABLATE 0
 #endif
 
+// Non-temporal parent-row loads (0 disables): the streamed rows no longer
+// evict the aspirants' 2 MiB key array from the L2 (A/B r04 c2ntl: kernel
+// 0.2255 -> 0.2227 ms, HBM bytes per launch 1.242e9 -> 1.101e9 = 0.99 x the
+// algorithmic 1.107e9).
 #ifndef DM_BITS_NTLOAD
-#define DM_BITS_NTLOAD 0  // non-temporal parent-row loads in the fused kernel (A/B)
+#define DM_BITS_NTLOAD 1
 #endif
 
 // Wave priority over the decision chain (0 disables; A/B r04 c2prio: 1 and
