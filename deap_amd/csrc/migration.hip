@@ -12,9 +12,10 @@
 //   2. a k x k pass compares emigrant and immigrant genomes;
 //   3. one workgroup resolves j = 0..k-1 in order: the first row that still
 //      holds an original match, or an already-placed emigrant equal to
-//      immigrant j, whichever index is smaller; it copies emigrant j there and
-//      clears that row from the later bitmaps.
+//      immigrant j, whichever index is smaller -- decisions first, in LDS,
+//      then every row copied in parallel by its last taker.
 #include "common.hpp"
+#include "sort.hpp"
 
 namespace dm {
 
@@ -190,114 +191,222 @@ __global__ void em_im_eq_kernel(const void* em_block, const void* im_block, int6
     }
 }
 
-// Sequential resolution; one workgroup of 256 threads.
+// Sequential resolution, decisions first: immigrant j's slot
+// depends only on which rows earlier immigrants took and which emigrants are
+// still where they were put, so the k decisions run in LDS -- (a) the first
+// original match not taken by an earlier placement (first[j], unless taken:
+// then the bitmap from there with the taken rows masked), (b) a smaller row
+// still holding an earlier emigrant equal to immigrant j -- and only then are
+// the rows copied, in parallel, each slot by its last writer.  Same result as
+// placing and copying one immigrant at a time (what round 3 did: 124 us per
+// deme at k = 15), without a global round trip and a row copy per immigrant.
+// Row copies of a placement, flattened over (row, 16-B piece) and eight
+// pieces per thread in flight: a wave copying one 8-KB row at a time with one
+// load outstanding took ~12 us per row.  dst_slot(j) < 0: row j not copied.
+template <typename SlotFn>
+__device__ __forceinline__ void copy_em_rows(char* genes, int64_t stride, const Block& em,
+                                             int64_t nrows, SlotFn dst_slot) {
+    const int64_t per = stride / 16, total = nrows * per;
+    const int64_t nt = blockDim.x;
+    constexpr int U = 8;
+    for (int64_t t0 = threadIdx.x; t0 < total; t0 += nt * U) {
+        uint4 v[U];
+        int64_t slot[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t = t0 + u * nt;
+            slot[u] = -1;
+            if (t < total) {
+                const int64_t j = t / per;
+                slot[u] = dst_slot(j);
+                if (slot[u] >= 0) v[u] = reinterpret_cast<const uint4*>(em.genes + j * stride)[t - j * per];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t t = t0 + u * nt;
+            if (slot[u] >= 0) {
+                const int64_t j = t / per;
+                reinterpret_cast<uint4*>(genes + slot[u] * stride)[t - j * per] = v[u];
+            }
+        }
+    }
+}
+
+constexpr int RES_MAX = 4096;  // placements tracked in LDS = the API's k limit (dm_mig_place)
+constexpr int MLIST = 64;      // leading matches of each immigrant listed before the resolution
+
+// mlist[j][0..mcount[j]): the first min(j + 1, MLIST) rows whose genome
+// equals immigrant j, ascending (at most j rows can be taken before
+// immigrant j is placed, so j + 1 leading matches always hold its answer when
+// the list is complete).  One workgroup per immigrant, from first[j]'s word.
+__global__ __launch_bounds__(256) void first_matches_kernel(const unsigned long long* bitmap,
+                                                            int64_t words, const int32_t* first,
+                                                            int64_t n, int32_t* mlist,
+                                                            int32_t* mcount) {
+    const int64_t j = blockIdx.x;
+    const int L = (int)std::min<int64_t>(MLIST, j + 1);
+    __shared__ int32_t sh[4];
+    if (first[j] >= n) {
+        if (threadIdx.x == 0) mcount[j] = 0;
+        return;
+    }
+    // 16 consecutive words per thread per pass (4,096 words = 262,144 rows):
+    // the loads of a pass are all in flight together
+    constexpr int WPT = 16;
+    const unsigned long long* row = bitmap + j * words;
+    int got = 0;
+    for (int64_t wb = first[j] >> 6; wb < words && got < L; wb += 256 * WPT) {
+        const int64_t w0 = wb + (int64_t)threadIdx.x * WPT;
+        unsigned long long x[WPT];
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+            x[i] = w0 + i < words ? row[w0 + i] : 0ull;
+            c += __popcll(x[i]);
+        }
+        int pos = got + block_incl_scan<256, false>(c, sh) - c;
+        const int total = sh[3];
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            for (unsigned long long y = x[i]; y && pos < L; y &= y - 1)
+                mlist[j * MLIST + pos++] = (int32_t)((w0 + i) * 64 + __ffsll((long long)y) - 1);
+        __syncthreads();  // sh is reused by the next pass's scan
+        got += total;
+    }
+    if (threadIdx.x == 0) mcount[j] = std::min(got, L);
+}
+
+__device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid, int64_t n,
+                                         int64_t stride, int nobj, const Block& em, int64_t k,
+                                         int64_t words, const unsigned long long* bitmap,
+                                         const uint8_t* E, const int32_t* mlist,
+                                         const int32_t* mcount, int32_t* slots,
+                                         unsigned long long* dirty, const int32_t* self_rows,
+                                         int32_t* err) {
+    __shared__ int32_t sl[RES_MAX];     // slot of placement j
+    __shared__ uint8_t stale[RES_MAX];  // placement j's row was taken by a later one
+    __shared__ int32_t smc[RES_MAX];
+    constexpr int SM = 64;              // E and the match lists staged in LDS up to k = 64 (C4: 15)
+    __shared__ uint8_t sE[SM * SM];
+    __shared__ int32_t sml[SM * MLIST];
+    __shared__ unsigned long long sbest;
+    __shared__ int nplaced;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const bool small = k <= SM;
+    for (int64_t j = tid; j < k; j += nt) smc[j] = mcount[j];
+    if (small) {
+        for (int64_t t = tid; t < k * k; t += nt) sE[t] = E[t];
+        for (int64_t t = tid; t < k * MLIST; t += nt) sml[t] = mlist[t];
+    }
+    if (tid == 0) nplaced = (int)k;
+    __syncthreads();
+    for (int64_t j = 0; j < k; ++j) {
+        if (tid == 0) sbest = ~0ull;
+        __syncthreads();
+        // (a) the first listed match no earlier placement took (rows ascend)
+        const int mc = smc[j];
+        if (tid < mc) {
+            const int32_t row = small ? sml[j * MLIST + tid] : mlist[j * MLIST + tid];
+            bool taken = false;
+            for (int64_t p = 0; p < j && !taken; ++p) taken = sl[p] == row;
+            if (!taken) atomicMin(&sbest, (unsigned long long)row);
+        }
+        __syncthreads();
+        if (sbest == ~0ull && mc == MLIST) {
+            // every listed match taken (j >= MLIST): scan on past the list,
+            // taken rows masked
+            const int64_t start = (int64_t)(small ? sml[j * MLIST + MLIST - 1]
+                                                  : mlist[j * MLIST + MLIST - 1]) + 1;
+            for (int64_t wb = start >> 6; wb < words; wb += nt) {
+                const int64_t w = wb + tid;
+                unsigned long long x = w < words ? bitmap[j * words + w] : 0ull;
+                if (w == (start >> 6) && (start & 63)) x &= ~0ull << (start & 63);
+                if (x)
+                    for (int64_t p = 0; p < j; ++p)
+                        if ((int64_t)(sl[p] >> 6) == w) x &= ~(1ull << (sl[p] & 63));
+                if (x) atomicMin(&sbest, (unsigned long long)(w * 64 + __ffsll((long long)x) - 1));
+                __syncthreads();
+                if (sbest != ~0ull) break;
+                __syncthreads();
+            }
+        }
+        // (b) an earlier emigrant equal to immigrant j, still in its row, at a smaller row
+        for (int64_t p = tid; p < j; p += nt)
+            if (!stale[p] && (small ? sE[p * k + j] : E[p * k + j]) &&
+                (unsigned long long)sl[p] < sbest)
+                atomicMin(&sbest, (unsigned long long)sl[p]);
+        __syncthreads();
+        const unsigned long long slot = sbest;
+        if (slot >= (unsigned long long)n) {  // list.index -> ValueError
+            if (tid == 0) {
+                *err = (int32_t)j + 1;
+                nplaced = (int)j;
+            }
+            __syncthreads();
+            break;
+        }
+        if (tid == 0) {
+            sl[j] = (int32_t)slot;
+            stale[j] = 0;
+        }
+        for (int64_t p = tid; p < j; p += nt)
+            if ((unsigned long long)sl[p] == slot) stale[p] = 1;
+        __syncthreads();
+    }
+    __syncthreads();
+    const int np = nplaced;
+    // copies: a row taken twice is written by its last taker
+    copy_em_rows(genes, stride, em, np, [&](int64_t j) { return stale[j] ? -1ll : (long long)sl[j]; });
+    for (int64_t j = tid; j < np; j += nt) {
+        const int64_t slot = sl[j];
+        if (!stale[j]) {
+            for (int o = 0; o < nobj; ++o) wv[slot * nobj + o] = em.wv[j * nobj + o];
+            valid[slot] = em.valid[j];
+        }
+        slots[j] = (int32_t)slot;
+        // a self hop that puts a row's own object back keeps its identity
+        if (dirty && !(self_rows && self_rows[j] == slot))
+            atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+    }
+}
+
+// Placement of one deme's k immigrants; one workgroup of 256 threads.
 __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, uint8_t* valid,
                                                       int64_t n, int64_t stride, int nobj,
                                                       const void* em_block, int64_t k,
                                                       int64_t words, unsigned long long* bitmap,
                                                       const uint8_t* E, const int32_t* first,
-                                                      int32_t* slots, int32_t* content,
-                                                      unsigned long long* dirty,
+                                                      const int32_t* mlist, const int32_t* mcount,
+                                                      int32_t* slots, unsigned long long* dirty,
                                                       const int32_t* self_rows, int32_t* err) {
     Block em = block_view((void*)em_block, stride, nobj, k);
-    __shared__ int64_t best;
-    __shared__ int32_t placed_slot[4096];
-    __shared__ int32_t placed_em[4096];
-    __shared__ int nplaced;
     __shared__ int fast;
-    if (threadIdx.x == 0) {
-        nplaced = 0;
-        fast = 1;
-    }
+    if (threadIdx.x == 0) fast = 1;
     __syncthreads();
     // Fast path: when every immigrant has a first match, the first matches
     // are pairwise distinct and no emigrant equals any immigrant, no
-    // placement can change another immigrant's match, so the sequential loop
-    // below would write emigrant j into first[j] for every j: do the k row
-    // copies in parallel (one wave per row).
+    // placement can change another immigrant's match, so the decisions
+    // below would put emigrant j into first[j] for every j: copy directly.
     for (int64_t t = threadIdx.x; t < k * k; t += blockDim.x) {
         const int64_t e = t / k, j = t % k;
         if (E[t] || first[j] >= n || (e < j && first[e] == first[j])) fast = 0;
     }
     __syncthreads();
     if (fast) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
-        for (int64_t j = wave; j < k; j += nwave) {
+        copy_em_rows(genes, stride, em, k, [&](int64_t j) { return (long long)first[j]; });
+        for (int64_t j = threadIdx.x; j < k; j += blockDim.x) {
             const int64_t slot = first[j];
-            const uint4* src = reinterpret_cast<const uint4*>(em.genes + j * stride);
-            uint4* dst = reinterpret_cast<uint4*>(genes + slot * stride);
-            for (int64_t i = lane; i < stride / 16; i += 64) dst[i] = src[i];
-            if (lane < nobj) wv[slot * nobj + lane] = em.wv[j * nobj + lane];
-            if (lane == 0) {
-                valid[slot] = em.valid[j];
-                slots[j] = (int32_t)slot;
-                if (dirty && !(self_rows && self_rows[j] == slot))
-                    atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
-            }
-        }
-        return;
-    }
-    for (int64_t j = 0; j < k; ++j) {
-        if (threadIdx.x == 0) best = INT64_MAX;
-        __syncthreads();
-        // (a) first original match still present: scan words in blocks of 256,
-        // from the first match the match kernel saw (bits are only ever cleared)
-        const int64_t w0 = first[j] < n ? (int64_t)(first[j] >> 6) : words;
-        for (int64_t wb = w0; wb < words; wb += blockDim.x) {
-            const int64_t w = wb + threadIdx.x;
-            if (w < words) {
-                const unsigned long long x = bitmap[j * words + w];
-                if (x) atomicMin((unsigned long long*)&best, (unsigned long long)(w * 64 + __ffsll(x) - 1));
-            }
-            __syncthreads();
-            if (best != INT64_MAX) break;
-            __syncthreads();
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t slot = best;
-            // (b) already-placed emigrants equal to immigrant j
-            for (int p = 0; p < nplaced; ++p) {
-                const int32_t s = placed_slot[p];
-                if (content[s] == placed_em[p] && E[(int64_t)placed_em[p] * k + j] && s < slot)
-                    slot = s;
-            }
-            if (slot == INT64_MAX || slot >= n) {
-                *err = (int32_t)j + 1;  // list.index -> ValueError
-                best = -1;
-            } else {
-                best = slot;
-                slots[j] = (int32_t)slot;
-                content[slot] = (int32_t)j;
-                if (nplaced < 4096) {
-                    placed_slot[nplaced] = (int32_t)slot;
-                    placed_em[nplaced] = (int32_t)j;
-                    ++nplaced;
-                }
-            }
-        }
-        __syncthreads();
-        const int64_t slot = best;
-        if (slot < 0) return;
-        // copy emigrant j into the slot
-        const uint4* src = reinterpret_cast<const uint4*>(em.genes + j * stride);
-        uint4* dst = reinterpret_cast<uint4*>(genes + slot * stride);
-        for (int64_t i = threadIdx.x; i < stride / 16; i += blockDim.x) dst[i] = src[i];
-        if (threadIdx.x < nobj) wv[slot * nobj + threadIdx.x] = em.wv[j * nobj + threadIdx.x];
-        if (threadIdx.x == 0) {
+            for (int o = 0; o < nobj; ++o) wv[slot * nobj + o] = em.wv[j * nobj + o];
             valid[slot] = em.valid[j];
-            // a self hop (migarray[d] == d) that puts a row's own object back
-            // in that row keeps its identity (list.index's `is` test of a later
-            // hop still matches it): not dirty
+            slots[j] = (int32_t)slot;
             if (dirty && !(self_rows && self_rows[j] == slot))
                 atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
         }
-        // the row no longer holds its original genome
-        for (int64_t jj = j + 1 + threadIdx.x; jj < k; jj += blockDim.x)
-            bitmap[jj * words + (slot >> 6)] &= ~(1ull << (slot & 63));
-        __threadfence_block();
-        __syncthreads();
+        return;
     }
+    resolve_decide_then_copy(genes, wv, valid, n, stride, nobj, em, k, words, bitmap, E, mlist,
+                             mcount, slots, dirty, self_rows, err);
 }
 
 }  // namespace dm
@@ -338,17 +447,18 @@ static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block
     const int64_t n = pop->n;
     const int64_t words = (n + 63) / 64;
     const size_t bm = align_up((size_t)k * words * 8, 256);
-    const size_t cb = align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);
-    char* base = (char*)scratch_slot(ctx, 3, bm + align_up((size_t)k * k, 256) + cb +
-                                                 align_up((size_t)k * 4, 256));
+    DM_CHECK_ARG(k <= RES_MAX, "k must be in [0, 4096]");
+    const size_t kb = align_up((size_t)k * 4, 256);
+    char* base = (char*)scratch_slot(ctx, 3, bm + align_up((size_t)k * k, 256) + 2 * kb +
+                                                 align_up((size_t)k * MLIST * 4, 256));
     if (!base) return DM_ERR_NOMEM;
     unsigned long long* bitmap = (unsigned long long*)base;
     uint8_t* E = (uint8_t*)(base + bm);
-    int32_t* content = (int32_t*)(base + bm + align_up((size_t)k * k, 256));
-    int32_t* first = (int32_t*)((char*)content + cb);
+    int32_t* first = (int32_t*)(base + bm + align_up((size_t)k * k, 256));
+    int32_t* mcount = (int32_t*)((char*)first + kb);
+    int32_t* mlist = (int32_t*)((char*)mcount + kb);
     hipStream_t s = ctx->stream;
     DM_HIP(hipMemsetAsync(bitmap, 0, (size_t)k * words * 8, s));
-    DM_HIP(hipMemsetAsync(content, 0xFF, (size_t)std::max<int64_t>(n, 1) * 4, s));
     DM_HIP(hipMemsetAsync(first, 0x7F, (size_t)k * 4, s));  // INT32 ~max: no match yet
     // one wave per 64 rows, at most 16 waves per CU slot pass
     const unsigned grid = (unsigned)std::max<int64_t>(
@@ -358,9 +468,10 @@ static int mig_place_async(dm_ctx* ctx, dm_pop* pop, const void* immigrant_block
                                       immigrant_block, k, words, dirty, bitmap, first);
     em_im_eq_kernel<<<(unsigned)std::max<int64_t>(1, (k * k + 255) / 256), 256, 0, s>>>(
         emigrant_block, immigrant_block, k, pop->stride, pop->dim, pop->gtype, pop->nobj, E);
+    first_matches_kernel<<<(unsigned)k, 256, 0, s>>>(bitmap, words, first, n, mlist, mcount);
     resolve_kernel<<<1, 256, 0, s>>>((char*)pop->genes, pop->wvalues, pop->valid, n, pop->stride,
                                      pop->nobj, emigrant_block, k, words, bitmap, E, first,
-                                     out_slots, content, dirty, self_rows, err);
+                                     mlist, mcount, out_slots, dirty, self_rows, err);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

@@ -226,3 +226,52 @@ def test_fp64_demes_stepwise_replay_in_oracle(gpu, dim, n, n_demes, replacement)
                 assert np.array_equal(state[d][1], before[d]["wvalues"]), (gen, d)
         prev = [(s[0], s[1], s[2].astype(bool)) for s in state]
     assert len(record) == ngen // 5
+
+
+@pytest.mark.parametrize("k,replacement", [(64, None), (3000, None), (3000, "sample"),
+                                            (4096, None)])
+def test_placement_with_heavy_duplicates_matches_list_index(gpu, k, replacement):
+    """migRing(k, selBest) over two demes of 6-bit genomes (64 distinct
+    values among 20,000 rows, so nearly every immigrant has earlier equal rows
+    and equal emigrants): the device placement against the reference loop
+    (migration.py:44-51) replayed on the host by value -- ``list.index`` is
+    the first row whose genome equals the immigrant, as the earlier
+    placements left the deme (no NaN genome, so identity adds nothing), up
+    to the library's k limit of 4,096; a taken first match (the masked bitmap
+    scan) and an equal earlier emigrant at a smaller row (rule b) occur in
+    every case."""
+    import random
+    import torch
+    from deap_amd import benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n, dim = 20000, 6
+    demes = []
+    for d in range(2):
+        p = tools.initPopulation(n=n, dim=dim, gtype="bits", weights=(1.0,),
+                                 stream=RandomStream(77, island=d))
+        benchmarks.onemax(p)
+        demes.append(p)
+    val = [np.packbits(p.rows_numpy(range(n))[0].astype(np.uint8), axis=1, bitorder="little")[:, 0]
+           .astype(np.int64) for p in demes]
+    fit = [p.wvalues[:n, 0].cpu().numpy().copy() for p in demes]
+    rec = []
+    tools.migRing(demes, k, tools.selBest,
+                  replacement=random.sample if replacement == "sample" else None, record=rec)
+    torch.cuda.synchronize()
+    em = rec[0]["emigrants"]
+    im = em if replacement is None else rec[0]["immigrants"]
+    cur = [(v.copy(), f.copy()) for v, f in zip(val, fit)]
+    for frm, to in enumerate([1, 0]):                      # migration.py:48-51
+        cv, cf = cur[to]
+        for i in range(k):
+            target = val[to][int(im[to][i])]
+            hit = np.flatnonzero(cv == target)
+            assert hit.size, "immigrant %d of deme %d not found" % (i, to)
+            s = int(hit[0])
+            cv[s] = val[frm][int(em[frm][i])]
+            cf[s] = fit[frm][int(em[frm][i])]
+    for d in range(2):
+        got = np.packbits(demes[d].rows_numpy(range(n))[0].astype(np.uint8), axis=1,
+                          bitorder="little")[:, 0].astype(np.int64)
+        assert np.array_equal(got, cur[d][0]), "deme %d genomes differ from the replay" % d
+        assert np.array_equal(demes[d].wvalues[:n, 0].cpu().numpy(), cur[d][1])
