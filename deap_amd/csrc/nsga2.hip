@@ -91,23 +91,30 @@ __global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, in
 // flagged run longer than LEX_RUN_CAP = 64 sets *overflow: the caller then
 // sorts in full.
 constexpr int LEX_RUN_CAP = 64;
-__device__ __forceinline__ bool lex_less_rest(const double* wv, int m, int32_t x, int32_t y) {
+// o0: the first objective compared (1 after the whole-key objective-0 sort; 0
+// after the 32-bit one, whose runs of equal top bits may differ in objective 0)
+__device__ __forceinline__ bool lex_less_rest(const double* wv, int m, int32_t x, int32_t y,
+                                              int o0) {
     const double* a = wv + (int64_t)x * m;
     const double* b = wv + (int64_t)y * m;
-    for (int o = 1; o < m; ++o) {
+    for (int o = o0; o < m; ++o) {
         const uint64_t ka = ordered_key(a[o]), kb = ordered_key(b[o]);
         if (ka != kb) return ka < kb;
     }
     return x < y;
 }
+// kshift: runs are rows whose objective-0 keys agree above bit kshift (0: the
+// whole key; 32: the top half, what a 4-pass radix sort orders)
 __global__ void lex_bad_kernel(const double* wv, int m, const uint64_t* keys0, const int32_t* perm,
-                               int64_t n, int32_t* runflag, int32_t* overflow) {
+                               int64_t n, int32_t* runflag, int32_t* overflow, int kshift) {
+    const int o0 = kshift ? 0 : 1;
     GRID_LOOP(j, n) {
-        if (j == 0 || keys0[j] != keys0[j - 1]) continue;
-        if (lex_less_rest(wv, m, perm[j - 1], perm[j])) continue;
+        const uint64_t kj = keys0[j] >> kshift;
+        if (j == 0 || kj != keys0[j - 1] >> kshift) continue;
+        if (lex_less_rest(wv, m, perm[j - 1], perm[j], o0)) continue;
         int64_t st = j - 1;
-        while (st > 0 && keys0[st - 1] == keys0[j] && j - st < LEX_RUN_CAP) --st;
-        if (st > 0 && keys0[st - 1] == keys0[j]) {
+        while (st > 0 && keys0[st - 1] >> kshift == kj && j - st < LEX_RUN_CAP) --st;
+        if (st > 0 && keys0[st - 1] >> kshift == kj) {
             *overflow = 1;
             continue;
         }
@@ -131,25 +138,26 @@ __device__ __forceinline__ uint64_t shfl_xor_u64l(uint64_t v, int mask) {
 __global__ __launch_bounds__(256) void lex_run_sort_kernel(const double* wv, int m,
                                                            const uint64_t* keys0, int32_t* perm,
                                                            int64_t n, const int32_t* runflag,
-                                                           int32_t* overflow) {
+                                                           int32_t* overflow, int kshift) {
     const int lane = threadIdx.x & 63;
+    const int o0 = kshift ? 0 : 1;  // the whole-key sort leaves objective 0 equal in a run
     const int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64;
     if (base >= n) return;
     uint64_t todo = __ballot(base + lane < n && runflag[base + lane] != 0);
     while (todo) {  // wave-uniform
         const int64_t st = base + __ffsll((long long)todo) - 1;
         todo &= todo - 1;
-        const uint64_t k0 = keys0[st];
-        if (st + LEX_RUN_CAP < n && keys0[st + LEX_RUN_CAP] == k0) {
+        const uint64_t k0 = keys0[st] >> kshift;
+        if (st + LEX_RUN_CAP < n && keys0[st + LEX_RUN_CAP] >> kshift == k0) {
             if (lane == 0) *overflow = 1;
             continue;
         }
         const int64_t i = st + lane;
-        const bool in = i < n && keys0[i] == k0;
+        const bool in = i < n && keys0[i] >> kshift == k0;
         LexRest r;
         r.x = in ? perm[i] : INT32_MAX;
         for (int o = 0; o < 3; ++o)
-            r.k[o] = in && o + 1 < m ? ordered_key(wv[(int64_t)r.x * m + o + 1]) : (in ? 0ull : ~0ull);
+            r.k[o] = in && o + o0 < m ? ordered_key(wv[(int64_t)r.x * m + o + o0]) : (in ? 0ull : ~0ull);
         for (int size = 2; size <= 64; size <<= 1) {
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
                 LexRest p;
@@ -569,31 +577,42 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     // in the others: the full redo cost 24 radix passes per selection.)
     int32_t* tieflag = small + 6;
     const bool full_lex = ctx->knobs.lex_full;
-    // the in-place run sort keys objectives 1..3 (LexRest): up to 4 objectives
+    // the in-place run sort keys objectives 1..3 (LexRest): up to 4 objectives;
+    // with at most 3 (LexRest then holds objectives 0..2) the objective-0 sort
+    // orders only the top 32 key bits (4 radix passes instead of 8) and the
+    // runs of equal top bits are fixed up the same way
     const bool quick = m > 1 && m <= 4 && !full_lex;
+    const bool q32 = quick && m <= 3 && !ctx->knobs.lex_no32;
     int rc;
-    DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
-    auto group = [&](int nlex) -> int {
-        int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex);
+    auto group = [&](int nlex, int kshift) -> int {
+        DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
+        int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex, kshift);
         if (r) return r;
         if (nlex < m) {
             zero_i32_kernel<<<g1(n), 256, 0, s>>>(vtmp, n);
-            lex_bad_kernel<<<g1(n), 256, 0, s>>>(wv, m, keys, perm, n, vtmp, tieflag);
-            lex_run_sort_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, s>>>(wv, m, keys, perm,
-                                                                             n, vtmp, tieflag);
+            lex_bad_kernel<<<g1(n), 256, 0, s>>>(wv, m, keys, perm, n, vtmp, tieflag, kshift);
+            lex_run_sort_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, s>>>(
+                wv, m, keys, perm, n, vtmp, tieflag, kshift);
         }
         zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
         seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
         if ((r = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return r;
         return exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp);
     };
-    if ((rc = group(quick ? 1 : m))) return rc;
+    if ((rc = group(quick ? 1 : m, q32 ? 32 : 0))) return rc;
     DM_HIP(hipMemsetAsync(nanflag, 0, 4, s));
     nan_any_kernel<<<g1(n * m), 256, 0, s>>>(wv, n * m, nanflag);
     DM_HIP(hipMemcpyAsync(hostv, utotal, 28, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
+    // a run longer than LEX_RUN_CAP: the whole-key objective-0 sort, then the
+    // full lexicographic sort
+    if (q32 && hostv[6]) {
+        if ((rc = group(1, 0))) return rc;
+        DM_HIP(hipMemcpyAsync(hostv, utotal, 28, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+    }
     if (quick && hostv[6]) {
-        if ((rc = group(m))) return rc;
+        if ((rc = group(m, 0))) return rc;
         DM_HIP(hipMemcpyAsync(hostv, utotal, 4, hipMemcpyDeviceToHost, s));
         DM_HIP(hipStreamSynchronize(s));
     }

@@ -338,13 +338,14 @@ int validate_pop(const dm_pop* p, const char* what);
 // Stable lexicographic sort of rows by wvalues (asc or desc) with caller
 // buffers; the permutation ends in vals.
 int lex_sort_rows(hipStream_t s, const double* wv, int nobj, int64_t n, bool desc, uint64_t* keys,
-                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp, int nlex) {
+                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp, int nlex,
+                  int begin_bit) {
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
     iota_kernel<<<g, 256, 0, s>>>(vals, n);
     if (nlex < 0 || nlex > nobj) nlex = nobj;
     for (int o = nlex - 1; o >= 0; --o) {  // LSD over objectives: last objective first
         key_obj_kernel<<<g, 256, 0, s>>>(wv, nobj, o, vals, keys, n, desc);
-        int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, n, 0, 64, rtemp);
+        int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, n, begin_bit, 64, rtemp);
         if (rc) return rc;
     }
     DM_LAUNCH_CHECK();

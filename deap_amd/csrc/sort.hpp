@@ -77,6 +77,7 @@ int inclusive_max_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64
 // Stable lexicographic sort of rows by wvalues with caller buffers; nlex
 // (default: all) sorts by the first nlex objectives only.
 int lex_sort_rows(hipStream_t s, const double* wv, int nobj, int64_t n, bool desc, uint64_t* keys,
-                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp, int nlex = -1);
+                  uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp, int nlex = -1,
+                  int begin_bit = 0);
 
 }  // namespace dm

@@ -360,32 +360,40 @@ def test_sort_nondominated_large_random(gpu):
         assert chosen == want_c
 
 
-def _near_clone_fitness(rng, m, nbase, long_mixed):
+def _near_clone_fitness(rng, m, nbase, long_mixed, ulp0=False):
     """Rows in runs of equal objective 0: exact clones, and near-clones a few
     ulps apart in the other objectives (what cxBlend of two clones leaves in
     C5's populations), in shuffled order; a run of 100 exact clones; with
     long_mixed a run of 90 rows equal in objective 0 and all different in the
-    others (longer than the 64-row in-place run sort: the full sort)."""
+    others (longer than the 64-row in-place run sort: the full sort).  ulp0:
+    the near-clones and the 90-row run also a few ulps apart in objective 0
+    (equal in the top 32 key bits the 4-pass objective-0 sort orders, so its
+    fix-up sorts them; the 90-row run overflows it into the whole-key sort)."""
     base = rng.uniform(0, 1, size=(nbase, m))
     rows = []
     for b in base:
         for _ in range(int(rng.integers(1, 9))):
             r = b.copy()
             if rng.random() < 0.6:
-                for o in range(1, m):
+                for o in range(0 if ulp0 else 1, m):
                     for _ in range(int(rng.integers(0, 3))):
                         r[o] = np.nextafter(r[o], 2.0 if rng.random() < 0.5 else -1.0)
             rows.append(r)
     rows += [base[0]] * 100
     if long_mixed:
-        rows += [np.concatenate([[0.25], rng.uniform(0, 1, m - 1)]) for _ in range(90)]
+        x0 = 0.25
+        for _ in range(90):
+            rows.append(np.concatenate([[x0], rng.uniform(0, 1, m - 1)]))
+            if ulp0:
+                x0 = np.nextafter(x0, 1.0)
     wv = np.array(rows)
     return wv[rng.permutation(len(wv))]
 
 
 @pytest.mark.parametrize("m", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("long_mixed", [False, True])
-def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed):
+@pytest.mark.parametrize("ulp0", [False, True])
+def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed, ulp0):
     """The grouping sorts by objective 0 and then sorts, in place, only the
     runs of equal objective 0 that are out of order in the other objectives
     (nsga2.hip lex_bad_kernel / lex_run_sort_kernel), falling back to the full
@@ -395,8 +403,8 @@ def test_near_clone_runs_lexicographic_order(gpu, m, long_mixed):
     only in the later ones (the run sort keys objectives 1-3 only, so those
     objective counts take the full lexicographic sort)."""
     from deap_amd import tools
-    rng = np.random.default_rng(70 + 10 * m + long_mixed)
-    wv = _near_clone_fitness(rng, m, 500, long_mixed)
+    rng = np.random.default_rng(70 + 10 * m + long_mixed + 100 * ulp0)
+    wv = _near_clone_fitness(rng, m, 500, long_mixed, ulp0)
     if m > 4:  # near-clones that differ only in objectives 4..m-1
         tail = rng.choice(len(wv), len(wv) // 3, replace=False)
         wv[tail, 1:4] = wv[tail, 0:1]
