@@ -1160,12 +1160,14 @@ __device__ __forceinline__ bool dominates_wv(const double* a, const double* b, i
     return not_equal;
 }
 
-__global__ void dcd_keys_kernel(Rng rng, int64_t n, uint32_t which, uint64_t* keys,
-                                int32_t* vals) {
-    GRID_LOOP(i, n) {
-        const u32x4 w = rng(ST_DCD, (uint32_t)i, which);
-        keys[i] = ((uint64_t)w.x << 32) | w.y;
-        vals[i] = (int32_t)i;
+// keys of both permutations: segment q (0, 1) = the Philox keys of call q
+__global__ void dcd_keys_kernel(Rng rng, int64_t n, uint64_t* keys, int32_t* vals) {
+    GRID_LOOP(t, 2 * n) {
+        const uint32_t q = t >= n ? 1u : 0u;
+        const int64_t i = t - (int64_t)q * n;
+        const u32x4 w = rng(ST_DCD, (uint32_t)i, q);
+        keys[t] = ((uint64_t)w.x << 32) | w.y;
+        vals[t] = (int32_t)i;
     }
 }
 
@@ -1239,23 +1241,31 @@ extern "C" int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const doubl
     if (k == 0) return DM_OK;
     hipStream_t s = ctx->stream;
     if (mode != DM_RNG_INJECT) {
-        // random.sample(individuals, len(individuals)): permutations from
-        // sorting Philox keys (stable radix sort, ties by index)
-        const size_t kb = align_up((size_t)n * 8, 256), vb = align_up((size_t)n * 4, 256);
-        char* w = (char*)scratch(ctx, 2 * kb + 3 * vb + radix_sort_temp_bytes(n));
+        // random.sample(individuals, len(individuals)) twice: permutations from
+        // sorting Philox keys (stable radix sort, ties by index), both in ONE
+        // batched sort (two segments of n: 8 radix passes, not 16)
+        const size_t kb = align_up((size_t)n * 16, 256), vb = align_up((size_t)n * 8, 256);
+        char* w = (char*)scratch(ctx, 2 * kb + 2 * vb + radix_sort_batched_temp_bytes(2, n));
         if (!w) return DM_ERR_NOMEM;
         uint64_t* keys = (uint64_t*)w;
         uint64_t* ktmp = (uint64_t*)(w + kb);
-        int32_t* vtmp = (int32_t*)(w + 2 * kb);
-        int32_t* own1 = (int32_t*)(w + 2 * kb + vb);
-        int32_t* own2 = (int32_t*)(w + 2 * kb + 2 * vb);
-        void* rtemp = w + 2 * kb + 3 * vb;
-        if (!perm1) perm1 = own1;
-        if (!perm2) perm2 = own2;
-        int32_t* perms[2] = {perm1, perm2};
-        for (uint32_t q = 0; q < 2; ++q) {
-            dcd_keys_kernel<<<g1(n), 256, 0, s>>>(Rng(rng), n, q, keys, perms[q]);
-            if ((rc = radix_sort_pairs(s, keys, perms[q], ktmp, vtmp, n, 0, 64, rtemp))) return rc;
+        int32_t* vals = (int32_t*)(w + 2 * kb);
+        int32_t* vtmp = (int32_t*)(w + 2 * kb + vb);
+        void* rtemp = w + 2 * kb + 2 * vb;
+        dcd_keys_kernel<<<g1(2 * n), 256, 0, s>>>(Rng(rng), n, keys, vals);
+        bool in_tmp = false;
+        if ((rc = radix_sort_pairs_batched(s, keys, vals, ktmp, vtmp, 2, n, 0, 64, rtemp, &in_tmp)))
+            return rc;
+        int32_t* sorted = in_tmp ? vtmp : vals;
+        if (perm1) {  // the caller's dump buffers
+            DM_HIP(hipMemcpyAsync(perm1, sorted, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        } else {
+            perm1 = sorted;
+        }
+        if (perm2) {
+            DM_HIP(hipMemcpyAsync(perm2, sorted + n, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        } else {
+            perm2 = sorted + n;
         }
     }
     dcd_kernel<<<g1(k4), 256, 0, s>>>(pop->wvalues, pop->nobj, crowd, perm1, perm2, k4, Rng(rng),
