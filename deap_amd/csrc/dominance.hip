@@ -863,8 +863,8 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
 // ranks in LDS and one 64-byte prefix-set read from the global table per
 // objective; a workgroup reads only the sets its members need, mostly from
 // L2) instead of read from a stored D, so the dominance matrix is never
-// written.  Member rows, their ranks and tie spans
-// are loaded two 64-member steps ahead (a row's ranks wait on its row index).
+// written.  Each member's (reach, tie-group end, ranks) record is read from
+// the front-ordered table (MemberTab), a window of 2,048 at a time.
 #ifndef DM_PEEL_TAB_MINW
 #define DM_PEEL_TAB_MINW 4  // min waves per SIMD (4: two 512-thread workgroups per CU)
 #endif
@@ -928,7 +928,8 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_ke
     const int64_t j0s = blockIdx.y * slen;
     const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
     // (reach, last q of the objective-0 tie group, ranks 1 and 2) per member,
-    // front order: gathered once per front by the ordering (member_tab)
+    // front order: built per q once per selection (member_rec_kernel), carried by the
+    // released candidates and written in front order by the ordering (MemberTab)
     const int4* members = mtab + sust;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int STEP = PEEL_WAVES * 64;
