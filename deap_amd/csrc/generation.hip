@@ -144,10 +144,16 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
             DM_HIP(hipMemsetAsync(hist, 0, (size_t)a.np * 4, ctx->stream));
             if (!ctx->knobs.pipe_key_fitter) {
                 int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
+                // bins: labels of the parent graph's neighbourhoods (round 1
+                // inside the plan kernel, further rounds after it), or with
+                // DM_PIPE_LABEL_ROUNDS=0 the degree keys
+                const int rounds = ctx->knobs.pipe_label_rounds;
+                int32_t* lab = rounds > 0 ? deg : nullptr;  // zeroed: labels unset
                 DM_HIP(hipMemsetAsync(deg, 0, (size_t)a.np * 4, ctx->stream));
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
-                                  nullptr, deg, nullptr);
-                launch_plan_degree_keys(plans, deg, keys, tick, hist, npairs, ctx->stream);
+                                  nullptr, lab ? nullptr : deg, nullptr, lab);
+                if (rounds > 1) launch_plan_labels(plans, lab, npairs, rounds - 1, ctx->stream);
+                launch_plan_degree_keys(plans, deg, lab, keys, tick, hist, npairs, ctx->stream);
             } else {
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
                                   hist, tick);

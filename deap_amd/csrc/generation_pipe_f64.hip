@@ -14,7 +14,8 @@ namespace dm {
 __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
                                              int64_t p, int32_t* __restrict__ keys,
                                              int32_t* __restrict__ hist,
-                                             int32_t* __restrict__ tick) {
+                                             int32_t* __restrict__ tick,
+                                             int32_t* __restrict__ lab) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
     const int m = a.nobj;
@@ -142,6 +143,13 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         const int32_t key = pl.f1 > pl.f0 ? s[1] : s[0];
         keys[p] = key;
         tick[p] = atomicAdd(hist + key, 1);
+    } else if (lab) {
+        // neighbourhood bins: the first label-propagation round (plan_label_kernel)
+        if (has1) {
+            const int32_t m = min(s[0], s[1]);
+            atomicMax(lab + s[0], INT32_MAX - m);
+            atomicMax(lab + s[1], INT32_MAX - m);
+        }
     } else if (hist) {
         // degree keys (plan_degree_key_kernel): count both parents' slots
         atomicAdd(hist + s[0], 1);
@@ -158,13 +166,14 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                                                         long long* __restrict__ count_evals,
                                                         int32_t* __restrict__ keys,
                                                         int32_t* __restrict__ hist,
-                                                        int32_t* __restrict__ tick) {
+                                                        int32_t* __restrict__ tick,
+                                                        int32_t* __restrict__ lab) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick);
+        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -174,14 +183,14 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p, keys, hist, tick);
+    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab);
 }
 
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
-                       int32_t* keys, int32_t* hist, int32_t* tick) {
+                       int32_t* keys, int32_t* hist, int32_t* tick, int32_t* lab) {
     const int64_t npairs = (a.nc + 1) / 2;
     pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals,
-                                                                           keys, hist, tick);
+                                                                           keys, hist, tick, lab);
 }
 
 // Counting-sort placement of the plans by key: slot start[key] + tick of pair
@@ -206,8 +215,13 @@ __global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restr
 // Degree keys: the parent that appears in more pair slots of this generation
 // (a greedy vertex cover of the pairs: fewer distinct key rows than the fitter
 // parent gives), ticketed into the zeroed hist2.
+// With lab (label propagation below) the bin is the pair's label -- the
+// smaller of its parents' labels -- instead of a degree key: the pairs of one
+// neighbourhood of the parent graph land together, so more of their rows
+// (not only one shared parent's) are re-read from the L2.
 __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __restrict__ plans,
                                                               const int32_t* __restrict__ deg,
+                                                              const int32_t* __restrict__ lab,
                                                               int32_t* __restrict__ keys,
                                                               int32_t* __restrict__ tick,
                                                               int32_t* __restrict__ hist2,
@@ -215,14 +229,39 @@ __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npairs) return;
     const int32_t s0 = plans[p].s0, s1 = plans[p].s1;
-    const int32_t key = deg[s1] > deg[s0] ? s1 : s0;
-    keys[p] = key;
-    tick[p] = atomicAdd(hist2 + key, 1);
+    const int32_t bin = lab ? min(min(INT32_MAX - lab[s0], s0), min(INT32_MAX - lab[s1], s1))
+                            : (deg[s1] > deg[s0] ? s1 : s0);
+    keys[p] = bin;
+    tick[p] = atomicAdd(hist2 + bin, 1);
 }
-void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, int32_t* keys,
-                             int32_t* tick, int32_t* hist2, int64_t npairs, hipStream_t s) {
+void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, const int32_t* lab,
+                             int32_t* keys, int32_t* tick, int32_t* hist2, int64_t npairs,
+                             hipStream_t s) {
     plan_degree_key_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        plans, deg, keys, tick, hist2, npairs);
+        plans, deg, lab, keys, tick, hist2, npairs);
+}
+
+// One round of label propagation over the parent graph (rows = vertices, a
+// pair's two parents = an edge): every parent takes the smallest label among
+// itself and its pair partner.  lab holds INT32_MAX - label, zeroed = unset
+// (one memset with the degree counts): a row's label is
+// min(INT32_MAX - lab[row], row).  In place -- the rounds are a heuristic for
+// locality, any interleaving of the atomics is a valid labelling and the
+// order never changes a child.  The first round runs inside the plan kernel.
+__global__ __launch_bounds__(256) void plan_label_kernel(const PairPlan* __restrict__ plans,
+                                                         int32_t* __restrict__ lab, int64_t npairs) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npairs) return;
+    const int32_t s0 = plans[p].s0, s1 = plans[p].s1;
+    const int32_t l0 = min(INT32_MAX - lab[s0], s0), l1 = min(INT32_MAX - lab[s1], s1);
+    const int32_t m = min(l0, l1);
+    if (m < l0) atomicMax(lab + s0, INT32_MAX - m);
+    if (m < l1) atomicMax(lab + s1, INT32_MAX - m);
+}
+void launch_plan_labels(const PairPlan* plans, int32_t* lab, int64_t npairs, int rounds,
+                        hipStream_t s) {
+    for (int r = 0; r < rounds; ++r)
+        plan_label_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(plans, lab, npairs);
 }
 
 void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
