@@ -412,3 +412,50 @@ def test_c4_migration_at_full_size(gpu):
             final[s_] = src  # a slot placed twice keeps the later emigrant
         for i, s_ in enumerate(slots):
             assert np.array_equal(g[i], final[s_][0]) and w[i, 0] == final[s_][1] and ok[i]
+
+
+@pytest.mark.parametrize("knob", ["DM_PIPE_NOORDER", "DM_PIPE_LABEL_ROUNDS=0",
+                                  "DM_PIPE_LABEL_ROUNDS=3", "DM_PIPE_KEY_FITTER"])
+def test_plan_orders_give_identical_children(gpu, knob):
+    """The C3 hot kernel's plan order -- label-propagation bins (default),
+    degree keys, fitter-parent keys, pair order -- only changes which pairs
+    a workgroup varies together: every child is a function of its own plan
+    and Philox counters, so one generation at 2^19 must be bit-identical under
+    every order (genomes, fitness, nevals)."""
+    import ctypes
+    import os
+    import torch
+    from deap_amd import _lib, algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    n = 1 << 19
+    stream = RandomStream(99)
+    pop = tools.initPopulation(n=n, dim=1000, low=-5.12, high=5.12, gtype="f64", weights=(-1.0,),
+                               stream=stream)
+    benchmarks.rastrigin(pop)
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.rastrigin)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("mutate", tools.mutGaussian, mu=0, sigma=1.0, indpb=0.05)
+    step = algorithms.GenerationStep(pop, tb, 0.5, 0.2)
+    nev = torch.zeros(2, dtype=torch.int64, device=pop.device)
+    state = stream.getstate()
+    ref = pop.like(n, capacity=n)
+    step.step(pop, ref, stream, ctypes.c_void_p(nev.data_ptr()))
+    name, _, val = knob.partition("=")
+    ctx = pop.ctx.bind()
+    os.environ[name] = val or "1"
+    try:
+        _lib.call("dm_ctx_reload_knobs", ctx)
+        stream.setstate(state)
+        other = pop.like(n, capacity=n)
+        step.step(pop, other, stream, ctypes.c_void_p(nev.data_ptr() + 8))
+        torch.cuda.synchronize()
+    finally:
+        del os.environ[name]
+        _lib.call("dm_ctx_reload_knobs", ctx)
+    assert torch.equal(ref.genes[:n], other.genes[:n])
+    assert torch.equal(ref.wvalues[:n], other.wvalues[:n])
+    assert torch.equal(ref.valid[:n], other.valid[:n])
+    a, b = nev.cpu().tolist()
+    assert a == b > 0
