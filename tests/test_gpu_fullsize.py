@@ -454,7 +454,7 @@ def test_plan_orders_give_identical_children(gpu, knob):
     finally:
         del os.environ[name]
         _lib.call("dm_ctx_reload_knobs", ctx)
-    assert torch.equal(ref.genes[:n], other.genes[:n])
+    assert torch.equal(ref.genes[:n, :8000], other.genes[:n, :8000])  # 1,000 fp64 genes
     assert torch.equal(ref.wvalues[:n], other.wvalues[:n])
     assert torch.equal(ref.valid[:n], other.valid[:n])
     a, b = nev.cpu().tolist()
