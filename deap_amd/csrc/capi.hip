@@ -439,7 +439,7 @@ static void read_knobs(dm_knobs& kn) {
     kn.bits_pp4 = std::getenv("DM_BITS_PP4") != nullptr;
     kn.lex_full = std::getenv("DM_LEX_FULL") != nullptr;
     kn.lex_no32 = std::getenv("DM_LEX_NO32") != nullptr;
-    kn.pipe_label_rounds = std::max(0, std::min(8, env_int("DM_PIPE_LABEL_ROUNDS", 1)));
+    kn.pipe_label_rounds = std::max(0, std::min(8, env_int("DM_PIPE_LABEL_ROUNDS", 2)));
     kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
     kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);

@@ -57,7 +57,7 @@ struct dm_knobs {
     bool bits_pp4 = false;          // DM_BITS_PP4: 4 pairs per wave in the fused C2 kernel
     bool lex_full = false;          // DM_LEX_FULL: full lexicographic sort in the grouping
     bool lex_no32 = false;          // DM_LEX_NO32: whole-key objective-0 sort in the grouping
-    int32_t pipe_label_rounds = 1;  // DM_PIPE_LABEL_ROUNDS: label propagation rounds of the plan order
+    int32_t pipe_label_rounds = 2;  // DM_PIPE_LABEL_ROUNDS: label propagation rounds of the plan order
     bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
     int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
     int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)

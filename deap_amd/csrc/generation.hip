@@ -127,7 +127,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         const size_t pb = align_up((size_t)npairs * sizeof(PairPlan), 256);
         const size_t hb = align_up((size_t)(a.np + 1) * 4, 256);
         const size_t kb = align_up((size_t)npairs * 4, 256);
-        char* w = (char*)scratch(ctx, ordered ? 2 * pb + 3 * hb + 2 * kb +
+        char* w = (char*)scratch(ctx, ordered ? 2 * pb + 3 * hb + 4 * kb +
                                                     align_up(scan_temp_bytes(a.np), 256) : pb);
         if (!w) return DM_ERR_NOMEM;
         PairPlan* plans = (PairPlan*)w;
@@ -150,10 +150,12 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 const int rounds = ctx->knobs.pipe_label_rounds;
                 int32_t* lab = rounds > 0 ? deg : nullptr;  // zeroed: labels unset
                 DM_HIP(hipMemsetAsync(deg, 0, (size_t)a.np * 4, ctx->stream));
+                int2* pairs2 = lab ? (int2*)((char*)deg + hb) : nullptr;  // 2 kb
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
-                                  nullptr, lab ? nullptr : deg, nullptr, lab);
-                if (rounds > 1) launch_plan_labels(plans, lab, npairs, rounds - 1, ctx->stream);
-                launch_plan_degree_keys(plans, deg, lab, keys, tick, hist, npairs, ctx->stream);
+                                  nullptr, lab ? nullptr : deg, nullptr, lab, pairs2);
+                if (rounds > 1) launch_plan_labels(pairs2, lab, npairs, rounds - 1, ctx->stream);
+                launch_plan_degree_keys(plans, pairs2, deg, lab, keys, tick, hist, npairs,
+                                        ctx->stream);
             } else {
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
                                   hist, tick);

@@ -566,7 +566,8 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 // lab (with hist): the first label-propagation round of the parent order
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
                        int32_t* keys = nullptr, int32_t* hist = nullptr,
-                       int32_t* tick = nullptr, int32_t* lab = nullptr);
+                       int32_t* tick = nullptr, int32_t* lab = nullptr,
+                       int2* pairs2 = nullptr);
 // Parent order: ordered[start[key[p]] + tick[p]] = plans[p] with p in its
 // flags (start = the exclusive scan of hist).
 void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
@@ -574,10 +575,10 @@ void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t
 // Degree keys (the default; DM_PIPE_KEY_FITTER keys by the fitter parent in
 // the plan kernel instead): after launch_pair_plans(..., hist = deg) counted
 // every parent slot, key[p] = the parent of more slots, ticketed into hist2.
-void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, const int32_t* lab,
-                             int32_t* keys, int32_t* tick, int32_t* hist2, int64_t npairs,
-                             hipStream_t s);
-void launch_plan_labels(const PairPlan* plans, int32_t* lab, int64_t npairs, int rounds,
+void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
+                             const int32_t* lab, int32_t* keys, int32_t* tick, int32_t* hist2,
+                             int64_t npairs, hipStream_t s);
+void launch_plan_labels(const int2* pairs2, int32_t* lab, int64_t npairs, int rounds,
                         hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);

@@ -15,7 +15,8 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
                                              int64_t p, int32_t* __restrict__ keys,
                                              int32_t* __restrict__ hist,
                                              int32_t* __restrict__ tick,
-                                             int32_t* __restrict__ lab) {
+                                             int32_t* __restrict__ lab,
+                                             int2* __restrict__ pairs2) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
     const int m = a.nobj;
@@ -144,7 +145,10 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         keys[p] = key;
         tick[p] = atomicAdd(hist + key, 1);
     } else if (lab) {
-        // neighbourhood bins: the first label-propagation round (plan_label_kernel)
+        // neighbourhood bins: the first label-propagation round (plan_label_kernel);
+        // the pair's parents also go to a compact array the label rounds and
+        // the bin kernel read (8 B per pair instead of 32-B plans)
+        if (pairs2) pairs2[p] = make_int2(s[0], s[1]);
         if (has1) {
             const int32_t m = min(s[0], s[1]);
             atomicMax(lab + s[0], INT32_MAX - m);
@@ -167,13 +171,14 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                                                         int32_t* __restrict__ keys,
                                                         int32_t* __restrict__ hist,
                                                         int32_t* __restrict__ tick,
-                                                        int32_t* __restrict__ lab) {
+                                                        int32_t* __restrict__ lab,
+                                                        int2* __restrict__ pairs2) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab);
+        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab, pairs2);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -183,14 +188,14 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab);
+    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab, pairs2);
 }
 
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
-                       int32_t* keys, int32_t* hist, int32_t* tick, int32_t* lab) {
+                       int32_t* keys, int32_t* hist, int32_t* tick, int32_t* lab, int2* pairs2) {
     const int64_t npairs = (a.nc + 1) / 2;
-    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(a, plans, count_evals,
-                                                                           keys, hist, tick, lab);
+    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
+        a, plans, count_evals, keys, hist, tick, lab, pairs2);
 }
 
 // Counting-sort placement of the plans by key: slot start[key] + tick of pair
@@ -220,6 +225,7 @@ __global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restr
 // neighbourhood of the parent graph land together, so more of their rows
 // (not only one shared parent's) are re-read from the L2.
 __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __restrict__ plans,
+                                                              const int2* __restrict__ pairs2,
                                                               const int32_t* __restrict__ deg,
                                                               const int32_t* __restrict__ lab,
                                                               int32_t* __restrict__ keys,
@@ -228,17 +234,18 @@ __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __
                                                               int64_t npairs) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npairs) return;
-    const int32_t s0 = plans[p].s0, s1 = plans[p].s1;
+    const int2 pr = pairs2 ? pairs2[p] : make_int2(plans[p].s0, plans[p].s1);
+    const int32_t s0 = pr.x, s1 = pr.y;
     const int32_t bin = lab ? min(min(INT32_MAX - lab[s0], s0), min(INT32_MAX - lab[s1], s1))
                             : (deg[s1] > deg[s0] ? s1 : s0);
     keys[p] = bin;
     tick[p] = atomicAdd(hist2 + bin, 1);
 }
-void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, const int32_t* lab,
-                             int32_t* keys, int32_t* tick, int32_t* hist2, int64_t npairs,
-                             hipStream_t s) {
+void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
+                             const int32_t* lab, int32_t* keys, int32_t* tick, int32_t* hist2,
+                             int64_t npairs, hipStream_t s) {
     plan_degree_key_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        plans, deg, lab, keys, tick, hist2, npairs);
+        plans, pairs2, deg, lab, keys, tick, hist2, npairs);
 }
 
 // One round of label propagation over the parent graph (rows = vertices, a
@@ -248,20 +255,21 @@ void launch_plan_degree_keys(const PairPlan* plans, const int32_t* deg, const in
 // min(INT32_MAX - lab[row], row).  In place -- the rounds are a heuristic for
 // locality, any interleaving of the atomics is a valid labelling and the
 // order never changes a child.  The first round runs inside the plan kernel.
-__global__ __launch_bounds__(256) void plan_label_kernel(const PairPlan* __restrict__ plans,
+__global__ __launch_bounds__(256) void plan_label_kernel(const int2* __restrict__ pairs2,
                                                          int32_t* __restrict__ lab, int64_t npairs) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npairs) return;
-    const int32_t s0 = plans[p].s0, s1 = plans[p].s1;
+    const int2 pr = pairs2[p];
+    const int32_t s0 = pr.x, s1 = pr.y;
     const int32_t l0 = min(INT32_MAX - lab[s0], s0), l1 = min(INT32_MAX - lab[s1], s1);
     const int32_t m = min(l0, l1);
     if (m < l0) atomicMax(lab + s0, INT32_MAX - m);
     if (m < l1) atomicMax(lab + s1, INT32_MAX - m);
 }
-void launch_plan_labels(const PairPlan* plans, int32_t* lab, int64_t npairs, int rounds,
+void launch_plan_labels(const int2* pairs2, int32_t* lab, int64_t npairs, int rounds,
                         hipStream_t s) {
     for (int r = 0; r < rounds; ++r)
-        plan_label_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(plans, lab, npairs);
+        plan_label_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(pairs2, lab, npairs);
 }
 
 void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
