@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--nobj", type=int, default=3,
+                    help="C5: DTLZ2 objectives (3 = the benched config; 4 takes the compare "
+                         "kernel + D-matrix peel)")
     return ap.parse_args(argv)
 
 
@@ -493,7 +496,7 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
 VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9  # wave64 VALU instructions/s: SIMD-32, 2 clk each
 
 
-def peel_report(peel_us, usz):
+def peel_report(peel_us, usz, m=3):
     """C5's dominant kernel, the table-fed front peel (dominance.hip
     peel_tab_kernel): one launch per front; launch i peels front i (usz[i]
     unique fitnesses) and releases front i + 1, the launches after the last
@@ -516,10 +519,11 @@ def peel_report(peel_us, usz):
               "by_front": [[int(a), round(b, 1)] for a, b in work]}
     pmc = None
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "c5_peel_pmc.json")
-    if os.path.exists(path):
+    if os.path.exists(path) and m <= 3:
         with open(path) as f:
             pmc = json.load(f)
-    roof = {"bound": "valu-issue", "kernel": "peel_tab_kernel<2>", "unit": "Ginstr/s",
+    roof = {"bound": "valu-issue", "unit": "Ginstr/s",
+            "kernel": "peel_tab_kernel<%d>" % (m - 1) if m <= 3 else "peel_owned_kernel",
             "peak": round(VALU_PEAK_GINSTR, 1), "kernel_ms": round(tot_ms, 4),
             "peak_basis": "wave64 VALU instructions: 256 CU x 4 SIMD-32 x 2.4 GHz / 2 clk",
             "traffic": None, "achieved": None, "frac": None}
@@ -595,7 +599,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     from deap_amd.ops import RandomStream
     device = replica_setup(args, world, local)
     n = args.pop if args.pop != 1 << 20 else 1 << 17
-    m, dim = 3, 12
+    m, dim = args.nobj, 12
     stream = RandomStream(args.seed, island=rank)
     pop = tools.initPopulation(n=n, dim=dim, low=0.0, high=1.0, gtype="f64",
                                weights=(-1.0,) * m, device=device, stream=stream)
@@ -661,7 +665,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     sel_fronts = tools.sortNondominated(two, n)
     wvh = two.wvalues[:2 * n].cpu().numpy()
     usz = [int(len(np.unique(wvh[f.cpu().numpy()], axis=0))) for f in sel_fronts]
-    peel = peel_report(peel_us, usz)
+    peel = peel_report(peel_us, usz, m)
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
     ufit = torch.unique(wv, dim=0).cpu().numpy()
@@ -677,28 +681,37 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     valu_peak = 256 * 4 * 32 * 2.4e9 / 1e9  # Gop/s of 32-bit integer VALU lane ops
     achieved = lds_bytes / (dom_ms * 1e-3) / 1e9
     cmp_rate = cmp_per_sel / (dom_ms * 1e-3) / 1e9
+    if m <= 3:
+        count_pass = {"bound": "lds", "achieved": round(achieved, 1), "peak": lds_peak,
+                      "unit": "GB/s", "frac": round(achieved / lds_peak, 4),
+                      "kernel": "bd_count_kernel<%d>" % m,
+                      "kernel_ms": round(dom_ms, 4), "lds_bytes_per_launch": lds_bytes,
+                      "count": "sum_c reach_c x (M-1) x (11 probes x 4 B + 64-B prefix set)",
+                      "peak_basis": "LDS reads: 256 CU x 256 B/clk x 2.4 GHz"}
+    else:
+        # M = 4: the integer compare kernel (M-1 rank compares per pair below
+        # the objective-0 diagonal) writing the D matrix the peel reads
+        count_pass = {"bound": "valu", "achieved": round(cmp_rate, 1), "peak": valu_peak,
+                      "unit": "G pair-compares/s", "frac": round(cmp_rate / valu_peak, 4),
+                      "kernel": "tri_dom_kernel<%d>" % m, "kernel_ms": round(dom_ms, 4),
+                      "count": "M U (U-1) / 2 pair compares (SURVEY.md §8d)",
+                      "peak_basis": "32-bit VALU lane ops: 256 CU x 4 SIMD x 32 x 2.4 GHz"}
+    count_pass.update({"compares_per_launch": cmp_per_sel, "compare_rate_G": round(cmp_rate, 1),
+                       "unique_fits": uniq, "fronts": len(fronts)})
     out = {"metric": "individual-generations/sec @pop=2^17 DTLZ2 NSGA-II (C5)",
            "value": round(n * args.steps * world / elapsed, 1),
            "unit": "individual-generations/sec",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": "C5 NSGA-II DTLZ2 M=3 D=12 eaMuPlusLambda(mu=lambda=N) + "
-                                  "selNSGA2(2N->N)", "pop": n, "genes": dim, "objectives": m,
+           "config": {"workload": "C5 NSGA-II DTLZ2 M=%d D=12 eaMuPlusLambda(mu=lambda=N) + "
+                                  "selNSGA2(2N->N)" % m, "pop": n, "genes": dim, "objectives": m,
                       "operators": "varOr cxBlend(0.5) mutGaussian(0,0.1,1/D) cxpb=0.6 mutpb=0.3",
                       "parallelism": "replicas%d" % world},
            "gen_ms_events": round(gen_ms, 4),
            "roofline": peel["roofline"],
            "peel": peel["fronts"],
-           "count_pass": {"bound": "lds", "achieved": round(achieved, 1), "peak": lds_peak,
-                          "unit": "GB/s", "frac": round(achieved / lds_peak, 4),
-                          "kernel": "bd_count_kernel<3>",
-                          "kernel_ms": round(dom_ms, 4), "lds_bytes_per_launch": lds_bytes,
-                          "count": "sum_c reach_c x (M-1) x (11 probes x 4 B + 64-B prefix set)",
-                          "peak_basis": "LDS reads: 256 CU x 256 B/clk x 2.4 GHz",
-                          "compares_per_launch": cmp_per_sel,
-                          "compare_rate_G": round(cmp_rate, 1),
-                          "unique_fits": uniq, "fronts": len(fronts)},
+           "count_pass": count_pass,
            "selection": {"ms": round(sel_ms, 4),
                          "what": "whole selNSGA2(2N -> N): ranks, bitset tables, counts, peel, "
                                  "crowding, last-front selection"},

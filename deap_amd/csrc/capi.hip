@@ -434,15 +434,12 @@ static int env_int(const char* name, int dflt) {
 static void read_knobs(dm_knobs& kn) {
     kn.disable_pipe = std::getenv("DM_DISABLE_PIPE") != nullptr;
     kn.bits_plan = std::getenv("DM_BITS_PLAN") != nullptr;
-    kn.bits_nocount = std::getenv("DM_BITS_NOCOUNT") != nullptr;
     kn.bits_nokeys = std::getenv("DM_BITS_NOKEYS") != nullptr;
-    kn.bits_pp4 = std::getenv("DM_BITS_PP4") != nullptr;
     kn.lex_full = std::getenv("DM_LEX_FULL") != nullptr;
     kn.lex_no32 = std::getenv("DM_LEX_NO32") != nullptr;
     kn.pipe_label_rounds = std::max(0, std::min(8, env_int("DM_PIPE_LABEL_ROUNDS", 2)));
     kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));
-    kn.pipe_depth = env_int("DM_PIPE_DEPTH", 0);
     kn.pipe_noorder = std::getenv("DM_PIPE_NOORDER") != nullptr;
     kn.pipe_key_fitter = std::getenv("DM_PIPE_KEY_FITTER") != nullptr;
 }

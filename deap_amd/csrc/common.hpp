@@ -48,19 +48,20 @@ constexpr int kEvalSpread = 64, kEvalSpreadStride = 16;  // counters, int64 stri
 constexpr int kEvalSpreadWords = (2 * kEvalSpread + 2) * kEvalSpreadStride;
 // Tuning switches for A/B measurements (tools_gpu/), read ONCE from the
 // environment at dm_ctx_create; all off by default.  None of them changes a
-// result: every one selects between bit-identical kernels.
+// result: every one selects between bit-identical kernels (one exception:
+// DM_DISABLE_PIPE's general kernel evaluates Rastrigin's cosine with the
+// fdlibm form, the hot kernel with its LDS table -- fitness within 1e-12
+// relative), and every one is run against the default by a GPU test
+// (tests/test_gpu_knobs.py, test_gpu_fullsize.py).
 struct dm_knobs {
     bool disable_pipe = false;      // DM_DISABLE_PIPE: general kernels instead of the hot ones
     bool bits_plan = false;         // DM_BITS_PLAN: C2 through the plan + burst kernels
-    bool bits_nocount = false;      // DM_BITS_NOCOUNT: C2 without the nevals count (ablation)
     bool bits_nokeys = false;       // DM_BITS_NOKEYS: C2 tournaments read wvalues, no int16 keys
-    bool bits_pp4 = false;          // DM_BITS_PP4: 4 pairs per wave in the fused C2 kernel
     bool lex_full = false;          // DM_LEX_FULL: full lexicographic sort in the grouping
     bool lex_no32 = false;          // DM_LEX_NO32: whole-key objective-0 sort in the grouping
     int32_t pipe_label_rounds = 2;  // DM_PIPE_LABEL_ROUNDS: label propagation rounds of the plan order
     bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
-    int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 64)
-    int pipe_depth = 0;             // DM_PIPE_DEPTH: C3 ring depth (0 = 2)
+    int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 32 ordered / 64)
     bool pipe_noorder = false;      // DM_PIPE_NOORDER: C3 plans in pair order (no parent order)
     bool pipe_key_fitter = false;   // DM_PIPE_KEY_FITTER: parent order keyed by the fitter parent
 };

@@ -1600,8 +1600,10 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                                                                      st, countq, lastq, ckey, cq, rankU, cr);
                 timing_end(ctx, DM_TIME_PEEL);
             } else {
+                timing_begin(ctx, DM_TIME_PEEL);
                 peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
                     D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
+                timing_end(ctx, DM_TIME_PEEL);
             }
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0, mt);
         }

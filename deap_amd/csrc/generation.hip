@@ -192,7 +192,6 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         q.w0 = a.w0;
         q.ev = a.ev;
         q.bpc = ctx->knobs.pipe_bpc;
-        q.depth = ctx->knobs.pipe_depth;
         q.ordered = ordered ? 1 : 0;
         timing_begin(ctx);
         if (parents->gtype == DM_F64)
@@ -212,7 +211,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
         if ((sel == DM_SEL_RANDOM || tournsize <= 8) && !ctx->knobs.bits_plan) {
             // one launch: decisions drawn inside the burst kernel (+ the
             // nevals reduction of its per-workgroup partials)
-            const bool count = ec != EC_NONE && a.nevals && !ctx->knobs.bits_nocount;
+            const bool count = ec != EC_NONE && a.nevals;
             // tournaments read the parents' fitness through int16 keys (one
             // coalesced pass, timed with the generation kernel)
             const bool keys = sel == DM_SEL_TOURNAMENT && a.w0 != 0.0 && !ctx->knobs.bits_nokeys;
@@ -221,7 +220,6 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 if (!kb) return DM_ERR_NOMEM;
                 a.pkeys = kb;
             }
-            a.pp4 = ctx->knobs.bits_pp4 ? 1 : 0;
             timing_begin(ctx);
             if (keys) launch_fit_keys(a, (int16_t*)a.pkeys, ctx->stream);
             launch_gen_bits_fused(a, ec != EC_NONE, count ? ctx->evals_spread : nullptr,

@@ -40,7 +40,6 @@ struct GenArgs {
     // C2 fitness keys (fit_key_kernel, generation_pipe_bits.hip): the parents'
     // wvalues as exact int16 multiples of |w0| (or FIT_KEY_NONE), nullable
     const int16_t* pkeys;
-    int32_t pp4;  // dm_knobs.bits_pp4: 4 pairs per wave in the fused kernel (A/B)
     dm_eval ev;
     Rng rng;
     const double* zig;

@@ -260,7 +260,7 @@ struct PipeArgs {
     int64_t* nevals;
     int64_t nc, pstride, cstride;
     int32_t dim, nobj;
-    int32_t bpc, depth;  // dm_knobs: workgroups per CU, ring depth (0 = defaults)
+    int32_t bpc;  // dm_knobs.pipe_bpc: workgroups per CU (0 = default)
     // 1: the plans are in parent order (plan_order_kernel), each carries its
     // pair index (flags >> PF_PAIR_SHIFT); a workgroup takes a contiguous run
     // of them, its waves interleaved, so the pairs that share a parent row are
@@ -497,38 +497,25 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     }
 }
 
-// Persistent grid: as many 256-thread workgroups as stay resident on every CU
-// (occupancy API, capped at 6: the admission limit for ~106 SGPRs on gfx950,
-// MI355X_MICROARCH.md §Residency), never more than one wave per pair.
-// bpc > 0 (dm_knobs, DM_PIPE_BPC) overrides the per-CU count (A/B experiments).
-template <typename K>
-dim3 pipe_grid(K kern, int num_cus, int64_t npairs, int bpc, bool ordered) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1)
-        occ = 1;
-    // 64 workgroups per CU in pair order (>= 16x the resident ones): the grid
-    // drains in many waves of blocks, so late blocks fill CUs whose first
-    // blocks finished early (A/B on C3, profiles/r01m: 2 resident/CU 3.47 ms;
-    // 8/CU 3.33-3.40; 32/CU 3.10; 48-64/CU 2.88; 128/CU 2.95; one pair per
-    // wave 4.84; r01s on a slower box: 32/CU 3.31 ms, 64/CU 3.25).  With the
-    // plans in label order 32 per CU (runs of 64 pairs per workgroup: more of
-    // a bin in one L2): 3.102-3.104 ms per step against 3.118-3.123 at 64, 16 /
-    // 24 / 48 in between, 96 3.15 (profiles/r04_labels/ab_bpc.txt)
-    occ = ordered ? 32 : 64;
-    if (bpc > 0) occ = bpc;
+// Persistent grid of 256-thread workgroups, never more than one wave per
+// pair: 64 workgroups per CU in pair order (>= 16x the resident ones): the
+// grid drains in many waves of blocks, so late blocks fill CUs whose first
+// blocks finished early (A/B on C3, profiles/r01m: 2 resident/CU 3.47 ms;
+// 8/CU 3.33-3.40; 32/CU 3.10; 48-64/CU 2.88; 128/CU 2.95; one pair per wave
+// 4.84; r01s on a slower box: 32/CU 3.31 ms, 64/CU 3.25).  With the plans in
+// label order 32 per CU (runs of 64 pairs per workgroup: more of a bin in one
+// L2): 3.102-3.104 ms per step against 3.118-3.123 at 64, 16 / 24 / 48 in
+// between, 96 3.15 (profiles/r04_labels/ab_bpc.txt).  bpc > 0 (dm_knobs,
+// DM_PIPE_BPC) overrides the per-CU count (A/B experiments).
+inline dim3 pipe_grid(int num_cus, int64_t npairs, int bpc, bool ordered) {
+    const int occ = bpc > 0 ? bpc : ordered ? 32 : 64;
     const int64_t blocks = std::min<int64_t>((npairs + 3) / 4, (int64_t)num_cus * occ);
     return dim3((unsigned)std::max<int64_t>(blocks, 1));
 }
 template <typename T, int NCH, int CX, int MUT, int EC>
 void launch_pipe_k(const PipeArgs& a, int num_cus, hipStream_t s) {
-    // depth 4 (dm_knobs, DM_PIPE_DEPTH=4, A/B): whole 1000-gene rows in flight
-    if (NCH == 4 && a.depth == 4) {
-        auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC, 4>;
-        kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2, a.bpc, a.ordered != 0), 256, 0, s>>>(a);
-        return;
-    }
     auto kern = gen_pipe_kernel<T, NCH, CX, MUT, EC>;
-    kern<<<pipe_grid(kern, num_cus, (a.nc + 1) / 2, a.bpc, a.ordered != 0), 256, 0, s>>>(a);
+    kern<<<pipe_grid(num_cus, (a.nc + 1) / 2, a.bpc, a.ordered != 0), 256, 0, s>>>(a);
 }
 template <typename T, int NCH, int CX, int MUT>
 void launch_pipe_e(const PipeArgs& a, int ec, int num_cus, hipStream_t s) {

@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenAr
 // wave: 16 children x 2 selection calls, 8 x 2 crossover calls, 16 mutation
 // flags) when t <= 4; 4 pairs per wave for 4 < t <= 8.
 static int fused_pp(const GenArgs& a) {
-    return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) && !a.pp4 ? 8 : 4;
+    return (a.sel != DM_SEL_TOURNAMENT || a.tournsize <= 4) ? 8 : 4;
 }
 
 // One-shot grid: one wave per group.

@@ -224,9 +224,10 @@ def _check_standard_order(pop, wv, weights, k, ref_fronts):
 
 
 @pytest.mark.parametrize("n,m,kind", [(1 << 18, 3, "sphere"), (1 << 18, 2, "sphere"),
+                                      (1 << 18, 4, "sphere"),
                                       (40000, 3, "shells"), (40000, 2, "shells"),
                                       (60000, 3, "dupshells"), (60000, 2, "dupshells"),
-                                      (60000, 3, "grid")])
+                                      (60000, 4, "dupshells"), (60000, 3, "grid")])
 def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
     """C5 at its benched size against reference-pinned restatements (VERDICT
     r2 item 2, r3 item 1): ``oracle/deap_port.py``'s Fortin log sort and
@@ -242,7 +243,12 @@ def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
       the benched path) == the closed form IN ORDER, with the ranks of the
       port's sort;
     * the standard ``selNSGA2`` chosen order == emo.py:40-48 on those fronts,
-      ties at the cut included, crowding distances bitwise."""
+      ties at the cut included, crowding distances bitwise.
+
+    M = 4 (DTLZ's free objective count, deap/benchmarks/__init__.py:495-521)
+    takes the integer compare kernel + D-matrix peel: the
+    same checks at 2^18 (34 fronts of up to ~22,000 members) and on the
+    duplicated shells."""
     from deap_amd import tools
     from oracle import deap_port
     k = n // 2
@@ -272,7 +278,7 @@ def test_nsga2_at_full_size_against_reference_port(gpu, n, m, kind):
     # port's (log-order) distances agree on rows without an equal twin
     if kind == "shells":  # fronts of ~3,500 unique fits: one slice per chunk
         assert max(usizes) > 1024, usizes
-    if kind == "dupshells":  # >= 2 x 2,048: the table peel's member slices
+    if kind == "dupshells" and m <= 3:  # >= 2 x 2,048: the table peel's member slices
         assert max(usizes) >= 8192, usizes
     if kind == "grid":
         last = want[-1]

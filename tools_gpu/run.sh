@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 GPU-box runner.  STEPS (space separated) picks the steps, e.g.
-#   STEPS="pytest smoke bench_c3" TAG=r04k tools_gpu/r04.sh
+# GPU-box runner.  STEPS (space separated) picks the steps, e.g.
+#   STEPS="pytest smoke bench_c3" TAG=r05k tools_gpu/run.sh
 # Every GPU step runs under its own timeout; the script stops at the first
 # failing step (fault / abort / timeout / test failure) and starts nothing
 # more on the GPU.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${TAG:-r04}
+OUT=gpurun_out/${TAG:-r05}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 step() {  # step NAME SECONDS CMD...
@@ -28,6 +28,10 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
     bench_c5) step bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
     bench_c5q) step bench_c5q 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     bench_c5x) step bench_c5x 600 python bench.py --config c5x --steps 5 --warmup 2 ;;
+    bench_c5m4) step bench_c5m4 400 python bench.py --config c5 --nobj 4 --steps 3 --warmup 2 --no-cpu-baseline ;;
+    kt_c5m4) step kt_c5m4 400 $KT -d $OUT/kt_c5m4 -- python3 bench.py --config c5 --nobj 4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    gap1) step gap1 200 python tools_gpu/deme_gap_probe.py 1 20 ;;
+    gap8) step gap8 400 python tools_gpu/deme_gap_probe.py 8 20 ;;
     kt_c3) step kt_c3 300 $KT -d $OUT/kt_c3 -- python3 bench.py --steps 12 --warmup 2 --no-cpu-baseline ;;
     kt_c2) step kt_c2 300 $KT -d $OUT/kt_c2 -- python3 bench.py --config c2 --steps 20 --warmup 2 --no-cpu-baseline ;;
     kt_c4) step kt_c4 400 $KT -d $OUT/kt_c4 -- python3 bench.py --islands 8 --steps 10 --warmup 0 --no-cpu-baseline ;;
