@@ -56,6 +56,16 @@ def parse(argv=None):
                          "the migRing hop plan of every rank, no kernels")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup-secs", type=float, default=1.0,
+                    help="after the --warmup steps, keep warming up (untimed) until this much "
+                         "wall time has passed: the GPU's clocks reach steady state (C2 ran "
+                         "0.24 ms per step after 5 steps, 0.214 after 200).  The extra "
+                         "generations recompute the next generation from the same state and "
+                         "discard it, so the populations (and deme_digests) do not depend on "
+                         "how many there were")
+    ap.add_argument("--digests-out", default=None,
+                    help="append this run's deme digests to a JSON reference file "
+                         "(profiles/deme_digests.json is the committed one)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c5", "c5x"])
     ap.add_argument("--pop", type=int, default=1 << 20)
     ap.add_argument("--islands-per-gpu", type=int, default=1,
@@ -270,13 +280,11 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
 
+    device = rank_device(args, local)
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.backend, device_id=torch.device("cuda", local)
-                                if args.backend == "nccl" else None)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        dist.init_process_group(args.backend, device_id=device if args.backend == "nccl" else None)
 
     from deap_amd import _lib, algorithms, base, benchmarks, tools
     from deap_amd.ops import RandomStream
@@ -305,7 +313,7 @@ def main(argv=None):
         getattr(benchmarks, problem)(p)  # generation 0: evaluate everyone
     steps = [algorithms.GenerationStep(p, tb, cxpb, mutpb) for p in pops]
     offs = [p.like(n, capacity=n) for p in pops]
-    total_gens = args.warmup + args.steps + 1
+    total_gens = args.warmup + args.steps + 2  # + a scratch slot for the warm-up top-up
     nevals = torch.zeros((per, total_gens), dtype=torch.int64, device=device)
     mig_events = []
 
@@ -333,6 +341,17 @@ def main(argv=None):
 
     for g in range(args.warmup):
         one_gen(g, False)
+
+    def rerun_next():
+        # generation `warmup` computed from the current parents and stream
+        # state and discarded (the state restored): the populations after
+        # the timed steps do not depend on how many of these ran
+        for i in range(per):
+            state = streams[i].getstate()
+            steps[i].step(pops[i], offs[i], streams[i],
+                          ctypes.c_void_p(nevals[i].data_ptr() + 8 * (total_gens - 1)))
+            streams[i].setstate(state)
+    extra_warm = warm_until(args, rerun_next)
     if n_demes > 1:
         # one untimed migration: the RCCL communicator (ncclCommInitRank), the
         # peers' point-to-point connections and the migration scratch are set
@@ -357,9 +376,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks([elapsed], device)[0]
     times = (ctypes.c_float * launches)()
     cnt = ctypes.c_int32(0)
     _lib.call("dm_ctx_kernel_times", ctx, times, launches, ctypes.byref(cnt))
@@ -369,9 +386,7 @@ def main(argv=None):
     mig_ms = (sum(a.elapsed_time(b) for a, b in mig_events) / len(mig_events)
               if mig_events else 0.0)
     if world > 1:
-        t = torch.tensor([kern_ms, mig_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        kern_ms, mig_ms = (float(x) for x in t.tolist())
+        kern_ms, mig_ms = max_over_ranks([kern_ms, mig_ms], device)
     nev = nevals.cpu().tolist()
     # sanity: the populations stay valid and finite
     for p in pops:
@@ -406,6 +421,7 @@ def main(argv=None):
     out = {"metric": METRICS[args.config],
            "value": round(value, 1), "unit": "individual-generations/sec", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
+           "warmup_topup": {"secs": args.warmup_secs, "generations": extra_warm},
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": scaling, "vs_baseline": None,
            "dtype": {"f64": "f64", "f32": "f32", "bits": "u64"}[gtype], "data": "synthetic",
@@ -424,6 +440,11 @@ def main(argv=None):
     out["deme_digests"] = {"after_generation": args.warmup + args.steps, "seed": args.seed,
                            "islands": n_demes,
                            "digest": {str(d): digests[d] for d in sorted(digests)}}
+    key = digest_key(args, n, n_demes)
+    check = check_digests(key, out["deme_digests"]["digest"])
+    out["deme_digests"].update(key=key, check=check)
+    if rank == 0 and args.digests_out:
+        save_digests(args.digests_out, key, out["deme_digests"]["digest"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(problem, args.cpu_sample)
     else:
@@ -434,6 +455,48 @@ def main(argv=None):
         from deap_amd import islands
         islands.close_comms()
         dist.destroy_process_group()
+    if check == "mismatch":
+        sys.stderr.write("bench.py: deme digests differ from the one-GPU reference %s (%s)\n"
+                         % (DIGESTS, key))
+        return 3
+
+
+DIGESTS = os.path.join(ROOT, "profiles", "deme_digests.json")
+
+
+def digest_key(args, n, n_demes):
+    """Everything a deme's digest depends on: the config, the
+    deme size and count, the seed, the generations and the migration
+    schedule -- not the GPU count or the deme split."""
+    return ("config=%s pop=%d islands=%d seed=%d warmup=%d steps=%d mig_every=%d mig_k=%d"
+            % (args.config, n, n_demes, args.seed, args.warmup, args.steps, args.mig_every,
+               args.mig_k))
+
+
+def check_digests(key, digest):
+    """'match' / 'mismatch' against the committed one-GPU reference
+    (profiles/deme_digests.json, written by --digests-out runs on one GPU),
+    or 'no reference' for a configuration it does not hold."""
+    try:
+        with open(DIGESTS) as f:
+            ref = json.load(f).get(key)
+    except (OSError, ValueError):
+        ref = None
+    if ref is None:
+        return "no reference"
+    return "match" if ref == digest else "mismatch"
+
+
+def save_digests(path, key, digest):
+    try:
+        with open(path) as f:
+            table = json.load(f)
+    except (OSError, ValueError):
+        table = {}
+    table[key] = digest
+    with open(path, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+        f.write("\n")
 
 
 def deme_digest(pop, n):
@@ -536,13 +599,24 @@ def peel_report(peel_us, usz, m=3):
     return {"roofline": roof, "fronts": fronts}
 
 
+def rank_device(args, local):
+    """One GPU per rank; with the gloo backend (CPU collectives, host-staged
+    migration) ranks may share GPUs, local rank r on GPU r mod count -- how
+    the one-GPU test boxes run the multi-rank path (RCCL refuses two ranks on
+    one device)."""
+    import torch
+    if args.backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
+    return torch.device("cuda", local)
+
+
 def replica_setup(args, world, local):
     """C5 / C5x at N > 1: replicas only (no exchange step), one
     process per GPU; the process group is used for the barrier and the
     max-over-ranks time only."""
     import torch
     import torch.distributed as dist
-    device = torch.device("cuda", local)
+    device = rank_device(args, local)
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group(args.backend, device_id=device if args.backend == "nccl" else None)
@@ -563,9 +637,32 @@ def replica_max(x, world, device):
     import torch.distributed as dist
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    return max_over_ranks([x], device)[0]
+
+
+def max_over_ranks(values, device):
+    """Element-wise max of a list of floats over the ranks (a device tensor
+    for RCCL, a host one for gloo)."""
+    import torch
+    import torch.distributed as dist
+    on = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(values, dtype=torch.float64, device=on)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return [float(x) for x in t.tolist()]
+
+
+def warm_until(args, fn):
+    """The untimed --warmup-secs top-up: call fn() until that much wall time
+    has passed (at least once when --warmup-secs > 0); returns the count."""
+    import torch
+    count, t0 = 0, time.perf_counter()
+    while args.warmup_secs > 0 and (count == 0 or time.perf_counter() - t0 < args.warmup_secs):
+        fn()
+        count += 1
+        if count % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return count
 
 
 def replica_finish(world):
@@ -612,6 +709,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     step = algorithms.MuPlusLambdaStep(pop, tb, n, n, 0.6, 0.3)
     for _ in range(args.warmup):
         step.step(stream)
+    extra_warm = warm_until(args, lambda: step.step(stream))
     replica_barrier(world)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
     t0 = time.perf_counter()
@@ -702,6 +800,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
            "value": round(n * args.steps * world / elapsed, 1),
            "unit": "individual-generations/sec",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "warmup_topup": {"secs": args.warmup_secs, "generations": extra_warm},
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": "C5 NSGA-II DTLZ2 M=%d D=12 eaMuPlusLambda(mu=lambda=N) + "
@@ -780,6 +879,7 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
 
     for _ in range(args.warmup):
         one_gen(False)
+    extra_warm = warm_until(args, lambda: one_gen(False))
     replica_barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -794,6 +894,7 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
            "value": round(n * args.steps * world / elapsed, 1),
            "unit": "individual-generations/sec",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "warmup_topup": {"secs": args.warmup_secs, "generations": extra_warm},
            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": "C5x examples/ga/nsga2.py loop: selTournamentDCD + "

@@ -124,3 +124,40 @@ def test_driver_torchrun_form():
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["owner"] == [0, 1]
+
+
+def test_digest_reference_check(tmp_path, monkeypatch):
+    """bench.py's self-check of a scaling run: the per-deme digests are looked
+    up in the committed one-GPU reference by everything they depend on
+    (config, deme size and count, seed, generations, migration schedule) --
+    'match', 'mismatch' (the run then exits non-zero) or 'no reference'."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ref = tmp_path / "digests.json"
+    monkeypatch.setattr(bench, "DIGESTS", str(ref))
+    args = bench.parse(["--islands", "8", "--steps", "20", "--warmup", "5"])
+    key = bench.digest_key(args, 1 << 20, 8)
+    assert "islands=8" in key and "steps=20" in key and "warmup=5" in key
+    digest = {str(d): "%016x" % (d * 7919) for d in range(8)}
+    assert bench.check_digests(key, digest) == "no reference"
+    bench.save_digests(str(ref), key, digest)
+    assert bench.check_digests(key, digest) == "match"
+    bad = dict(digest, **{"3": "0" * 16})
+    assert bench.check_digests(key, bad) == "mismatch"
+    other = bench.digest_key(bench.parse(["--islands", "8", "--steps", "21"]), 1 << 20, 8)
+    assert bench.check_digests(other, digest) == "no reference"
+
+
+def test_committed_digest_reference_is_well_formed():
+    """profiles/deme_digests.json (one-GPU runs of bench.py --digests-out):
+    every entry maps deme ids 0..islands-1 to 64-bit hex digests."""
+    path = os.path.join(ROOT, "profiles", "deme_digests.json")
+    if not os.path.exists(path):
+        pytest.skip("no committed reference yet")
+    with open(path) as f:
+        table = json.load(f)
+    assert table
+    for key, digest in table.items():
+        islands = int(key.split("islands=")[1].split()[0])
+        assert sorted(digest, key=int) == [str(d) for d in range(islands)]
+        assert all(len(h) == 16 and int(h, 16) >= 0 for h in digest.values())

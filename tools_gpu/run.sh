@@ -31,6 +31,18 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
     bench_c5m4) step bench_c5m4 400 python bench.py --config c5 --nobj 4 --steps 3 --warmup 2 --no-cpu-baseline ;;
     kt_c5m4) step kt_c5m4 400 $KT -d $OUT/kt_c5m4 -- python3 bench.py --config c5 --nobj 4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     gap1) step gap1 200 python tools_gpu/deme_gap_probe.py 1 20 ;;
+    digests)  # the one-GPU reference of the scaling runs' deme digests (profiles/deme_digests.json)
+      for sw in "20 5" "50 3"; do
+        set -- $sw
+        for per in 1 2 4 8; do
+          step digests_${per}_$1 300 python bench.py --gpus 1 --islands-per-gpu $per --steps $1 --warmup $2 --no-cpu-baseline --digests-out $OUT/deme_digests.json
+        done
+      done ;;
+    alloc)
+      for m in base mid:8 mid:16 mid:24 mid:32 mid:16 post:16 base; do
+        step alloc_${m/:/_} 120 python tools_gpu/alloc_order_probe.py $m 20
+        cat $OUT/alloc_${m/:/_}.out >> $OUT/alloc.jsonl
+      done ;;
     gap8) step gap8 400 python tools_gpu/deme_gap_probe.py 8 20 ;;
     kt_c3) step kt_c3 300 $KT -d $OUT/kt_c3 -- python3 bench.py --steps 12 --warmup 2 --no-cpu-baseline ;;
     kt_c2) step kt_c2 300 $KT -d $OUT/kt_c2 -- python3 bench.py --config c2 --steps 20 --warmup 2 --no-cpu-baseline ;;
