@@ -559,6 +559,36 @@ def cpu_baseline_nsga2(wv2, weights, pop, with_log=True):
 VALU_PEAK_GINSTR = 256 * 4 * 2.4e9 / 2 / 1e9  # wave64 VALU instructions/s: SIMD-32, 2 clk each
 
 
+def peel_work(wv, fronts, peel_us):
+    """The peel's algorithmic work per front: a member u
+    of front r is compared with every v of each 512-v chunk of the q order
+    (unique fits, ascending objective 0) up to the chunk holding the last fit
+    tied with u in objective 0 -- the only v it can dominate -- so front r
+    costs sum_u reach(u) member-chunk pairs (512 dominance bits each).
+    Reported as pairs per microsecond of the front's peel launch, next to the
+    VALU-issue fraction (which counts instructions, not work)."""
+    import numpy as np
+    ufit, inv = np.unique(wv + 0.0, axis=0, return_inverse=True)
+    inv = np.asarray(inv).ravel()
+    w0 = np.sort(ufit[:, 0])
+    # last position (ascending objective 0) tied with each unique fit
+    tie_end = np.searchsorted(w0, ufit[:, 0], side="right") - 1
+    reach = tie_end // 512 + 1
+    rows = []
+    for i, f in enumerate(fronts):
+        if i >= len(peel_us):
+            break
+        members = np.unique(inv[f.cpu().numpy()])
+        pairs = int(reach[members].sum())
+        rows.append((len(members), pairs, peel_us[i]))
+    tot_pairs = sum(r[1] for r in rows)
+    tot_us = sum(r[2] for r in rows)
+    return {"unit": "member-chunk pairs per us (512 dominance bits each)",
+            "pairs_per_selection": tot_pairs,
+            "pairs_per_us": round(tot_pairs / tot_us, 1) if tot_us else None,
+            "by_front": [[a, b, round(b / c, 1) if c else None] for a, b, c in rows]}
+
+
 def peel_report(peel_us, usz, m=3):
     """C5's dominant kernel, the table-fed front peel (dominance.hip
     peel_tab_kernel): one launch per front; launch i peels front i (usz[i]
@@ -764,6 +794,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     wvh = two.wvalues[:2 * n].cpu().numpy()
     usz = [int(len(np.unique(wvh[f.cpu().numpy()], axis=0))) for f in sel_fronts]
     peel = peel_report(peel_us, usz, m)
+    peel["fronts"]["work"] = peel_work(wvh, sel_fronts, peel_us)
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
     ufit = torch.unique(wv, dim=0).cpu().numpy()
@@ -848,6 +879,18 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
     benchmarks.dtlz2(pop, obj=m)
     two = pop.like(2 * n, capacity=2 * n)
     ctx = pop.ctx.bind()
+    from deap_amd.device import zeros
+    crowd_tmp = zeros((n,), torch.float64, device)
+
+    def carry_crowding(dst, src, idx):
+        # the chosen rows' crowding distances travel with them (dm_gather_f64,
+        # no PyTorch index kernel); src may be dst's own buffer (staged)
+        _lib.call("dm_gather_f64", ctx, ctypes.c_void_p(src.data_ptr()),
+                  ctypes.c_void_p(idx.data_ptr()), n, ctypes.c_void_p(crowd_tmp.data_ptr()))
+        if dst.crowding_dist is None or len(dst.crowding_dist) < n:
+            dst.crowding_dist = zeros((dst.capacity,), torch.float64, device)
+        _lib.call("dm_gather_f64", ctx, ctypes.c_void_p(crowd_tmp.data_ptr()), None, n,
+                  ctypes.c_void_p(dst.crowding_dist.data_ptr()))
 
     def select_into(pop, off):
         # pop[:] = toolbox.select(pop + offspring, MU)                 (nsga2.py:114)
@@ -856,11 +899,11 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
         idx = tools.selNSGA2(two, n)
         _lib.call("dm_gather", ctx, ctypes.byref(two.c_pop()), ctypes.c_void_p(idx.data_ptr()),
                   ctypes.byref(pop.c_pop()))
-        pop.crowding_dist = two.crowding_dist[idx.long()].contiguous()
+        carry_crowding(pop, two.crowding_dist, idx)
 
     # pop = toolbox.select(pop, len(pop)): assigns the crowding distances (nsga2.py:92)
     idx0 = tools.selNSGA2(pop, n)
-    pop.crowding_dist = pop.crowding_dist[idx0.long()].contiguous()
+    carry_crowding(pop, pop.crowding_dist, idx0)
     _lib.call("dm_gather", ctx, ctypes.byref(pop.c_pop()), ctypes.c_void_p(idx0.data_ptr()),
               ctypes.byref(two.c_pop(0, n)))
     _lib.call("dm_gather", ctx, ctypes.byref(two.c_pop(0, n)), None, ctypes.byref(pop.c_pop()))

@@ -84,6 +84,8 @@ SIGNATURES = {
     "dm_ctx_destroy": (ctypes.c_int, [_p]),
     "dm_ctx_set_stream": (ctypes.c_int, [_p, _p]),
     "dm_ctx_sync": (ctypes.c_int, [_p]),
+    "dm_zero": (ctypes.c_int, [_p, _p, _i64]),
+    "dm_set_fitness": (ctypes.c_int, [_p, _p, _p, _i64, _p]),
     "dm_ctx_set_timing": (ctypes.c_int, [_p, _i32]),
     "dm_ctx_kernel_times": (ctypes.c_int, [_p, _p, _i32, _PP(_i32)]),
     "dm_ctx_set_timing_target": (ctypes.c_int, [_p, _i32]),

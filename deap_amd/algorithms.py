@@ -1,9 +1,15 @@
 """Generational drivers on device-resident populations (``deap/algorithms.py``).
 
 Signatures and return values follow the reference; the population argument is
-a :class:`~deap_amd.device.DevicePopulation` and every registered operator must
-be a ``deap_amd`` device operator (there is no host fallback: a plain Python
-function in the toolbox raises ``TypeError``).  Each generation is one fused
+a :class:`~deap_amd.device.DevicePopulation` and every variation / selection
+operator must be a ``deap_amd`` device operator (a plain Python function
+there raises ``TypeError``).  ``evaluate`` may be a device objective
+(``deap_amd.benchmarks``, fused into the generation kernel) or any Python
+callable on one individual, such as the reference README's ``evalOneMax``:
+the :class:`HostEvaluator` bridge gathers the invalid rows, runs
+``toolbox.map(toolbox.evaluate, invalid_ind)`` on host individuals and
+writes the fitness back (``dm_set_fitness``), exactly the reference's
+``algorithms.py:171-174``.  Each generation is one fused
 kernel launch (select -> clone -> varAnd -> evaluate, ``dm_generation``) for
 ``eaSimple``; ``eaMuPlusLambda`` runs ``varOr`` (``dm_var_or``) then the
 selection over ``population + offspring``.  Per-generation bookkeeping
@@ -17,12 +23,14 @@ Extra keyword-only arguments (not in DEAP) control the random decisions:
 appended to in dump mode).
 """
 import ctypes
+import functools
 
 from . import _lib
 from .decisions import Decisions
 from .device import DevicePopulation
 from .ops import default_stream, mode_code, resolve
 from .tools.support import Logbook
+from .device import zeros as _zeros
 
 
 def _torch():
@@ -49,6 +57,75 @@ def _variation(population, mate, mutate, cxpb, mutpb):
         op, a, kw = mutate
         op.fill(var, a, kw, population)
     return var
+
+
+class HostEvaluator:
+    """``toolbox.evaluate`` that is a plain Python callable (not a device
+    objective): evaluates the invalid individuals of a device population on
+    the host, as the reference's loop does (``deap/algorithms.py:149-152,
+    171-174``)::
+
+        invalid_ind = [ind for ind in offspring if not ind.fitness.valid]
+        fitnesses = toolbox.map(toolbox.evaluate, invalid_ind)
+        for ind, fit in zip(invalid_ind, fitnesses):
+            ind.fitness.values = fit
+
+    The invalid rows (read from the device ``valid`` array, in population
+    order) are gathered on the device (``dm_gather``), copied once to the
+    host and materialised as individuals of the population's creator class;
+    ``values * weights`` (``Fitness.wvalues``, base.py:184-198) goes back in
+    one copy and one scatter (``dm_set_fitness``).  Returns the number of
+    evaluations (``nevals``)."""
+
+    def __init__(self, toolbox):
+        self.evaluate = toolbox.evaluate
+        self.map = getattr(toolbox, "map", map)
+
+    def __call__(self, population):
+        import numpy as np
+        torch = _torch()
+        n = len(population)
+        if n == 0:
+            return 0
+        ok = population.valid[:n].cpu().numpy()
+        inv = np.flatnonzero(ok == 0).astype(np.int32)
+        k = int(inv.size)
+        if k == 0:
+            return 0
+        ctx = population.ctx.bind()
+        idx = torch.from_numpy(inv).to(population.device)
+        batch = population.like(k, capacity=k)
+        _lib.call("dm_gather", ctx, ctypes.byref(population.c_pop()),
+                  ctypes.c_void_p(idx.data_ptr()), ctypes.byref(batch.c_pop()))
+        inds = batch.to_individuals()
+        fits = list(self.map(self.evaluate, inds))
+        if len(fits) != k:
+            raise ValueError("evaluate returned %d fitnesses for %d individuals" % (len(fits), k))
+        w = np.asarray(population.weights, dtype=np.float64)
+        vals = np.empty((k, population.nobj), dtype=np.float64)
+        for i, fit in enumerate(fits):
+            if len(fit) != population.nobj:
+                raise ValueError("evaluate returned %d values, the fitness has %d weights"
+                                 % (len(fit), population.nobj))
+            vals[i] = [float(x) for x in fit]
+        wv = torch.from_numpy(vals * w).to(population.device)  # Fitness.values setter
+        _lib.call("dm_set_fitness", ctx, ctypes.byref(population.c_pop()),
+                  ctypes.c_void_p(idx.data_ptr()), k, ctypes.c_void_p(wv.data_ptr()))
+        return k
+
+
+def _evaluator(toolbox):
+    """(device objective spec, None) or (None, HostEvaluator) for
+    ``toolbox.evaluate``."""
+    from .ops import DeviceOperator
+    f = toolbox.evaluate
+    while isinstance(f, functools.partial):
+        f = f.func
+    if isinstance(f, DeviceOperator):
+        return resolve(toolbox.evaluate), None
+    if callable(f):
+        return None, HostEvaluator(toolbox)
+    raise TypeError("toolbox.evaluate is not callable: %r" % (toolbox.evaluate,))
 
 
 def _eval(population, evaluate):
@@ -158,11 +235,12 @@ class _Bookkeeping:
 
     def __init__(self, population, ngen, stats, halloffame, verbose):
         torch = _torch()
-        self.nevals = torch.zeros((ngen + 1,), dtype=torch.int64, device=population.device)
+        self.nevals = _zeros((ngen + 1,), torch.int64, population.device)
         self.stats = stats
         self.hof = halloffame
         self.verbose = verbose
         self.records = []
+        self.host_nevals = {}  # generations evaluated by a HostEvaluator
         self.logbook = Logbook()
         self.logbook.header = ["gen", "nevals"] + (stats.fields if stats else [])
 
@@ -191,13 +269,15 @@ class _Bookkeeping:
             self._flush_one(gen, rec)
 
     def _flush_one(self, gen, rec):
-        nev = int(self.nevals[gen].item())
+        nev = self.host_nevals[gen] if gen in self.host_nevals else int(self.nevals[gen].item())
         self.logbook.record(gen=gen, nevals=nev, **_materialise(rec))
         print(self.logbook.stream)
 
     def finish(self):
         if not self.verbose:
             nev = self.nevals.cpu().tolist()
+            for gen, v in self.host_nevals.items():
+                nev[gen] = v
             for gen, rec in self.records:
                 self.logbook.record(gen=gen, nevals=nev[gen], **_materialise(rec))
         return self.logbook
@@ -221,7 +301,9 @@ class GenerationStep:
         self._selTournament, self._selRandom = selTournament, selRandom
         self.mate = resolve(toolbox.mate)
         self.mutate = resolve(toolbox.mutate)
-        self.evaluate = resolve(toolbox.evaluate) if evaluate else None
+        # a host `evaluate` (HostEvaluator): the kernel varies only, the
+        # driver evaluates the invalid children afterwards
+        self.evaluate, self.host_eval = _evaluator(toolbox) if evaluate else (None, None)
         self.sel = _selection_spec(toolbox)
         self.var = _variation(population, self.mate, self.mutate, cxpb, mutpb)
         self.ev = _eval(population, self.evaluate)
@@ -259,18 +341,24 @@ def eaSimple(population, toolbox, cxpb, mutpb, ngen, stats=None, halloffame=None
     step = GenerationStep(population, toolbox, cxpb, mutpb)
     book = _Bookkeeping(population, ngen, stats, halloffame, verbose)
     ctx = population.ctx.bind()
+    host = step.host_eval
 
     # generation 0: evaluate the invalid individuals                      :149-160
-    _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(step.ev), 1,
-              book.nevals_ptr(0))
+    if host is None:
+        _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(step.ev), 1,
+                  book.nevals_ptr(0))
+    else:
+        book.host_nevals[0] = host(population)
     book.record(0, population)
 
     offspring = population.like(len(population), capacity=population.capacity)
     # the HallOfFame's host loop for generation g runs while generation g + 1
     # is on the GPU (g's rows are rewritten only by generation g + 2)
-    defer = not verbose
+    defer = not verbose and host is None
     for gen in range(1, ngen + 1):
         step.step(population, offspring, stream, book.nevals_ptr(gen), mode, decisions, gen - 1)
+        if host is not None:
+            book.host_nevals[gen] = host(offspring)                        # :171-174
         book.complete_hof()
         population.swap_storage(offspring)                                 # :181
         book.record(gen, population, defer_hof=defer)
@@ -310,7 +398,8 @@ def varOr(population, toolbox, lambda_, cxpb, mutpb, *, decisions=None, mode=Non
     mate = resolve(toolbox.mate)
     mutate = resolve(toolbox.mutate)
     var = _variation(population, mate, mutate, cxpb, mutpb)
-    ev = _eval(population, resolve(toolbox.evaluate) if evaluate else None)
+    spec, host = _evaluator(toolbox) if evaluate else (None, None)
+    ev = _eval(population, spec)
     offspring = out if out is not None else population.like(lambda_, capacity=lambda_)
     code, d = _mode_and_decisions(mode, decisions, 0, lambda_, population, 0, var, varor=True)
     dec = d.c_struct() if d is not None else None
@@ -318,6 +407,8 @@ def varOr(population, toolbox, lambda_, cxpb, mutpb, *, decisions=None, mode=Non
     _lib.call("dm_var_or", ctx, ctypes.byref(population.c_pop()),
               ctypes.byref(offspring.c_pop(0, lambda_)), ctypes.byref(var), ctypes.byref(ev),
               stream.next(), code, ctypes.byref(dec) if dec is not None else None, None)
+    if host is not None:
+        host(offspring)
     return offspring
 
 
@@ -339,7 +430,9 @@ class MuPlusLambdaStep:
         self.sel = _selection_spec(toolbox)
         self.var = _variation(population, resolve(toolbox.mate), resolve(toolbox.mutate), cxpb,
                               mutpb)
-        self.ev = _eval(population, resolve(toolbox.evaluate))
+        spec, self.host_eval = _evaluator(toolbox)
+        self.ev = _eval(population, spec)
+        self.last_nevals = None  # set by a host evaluation
         n0 = len(population)
         cap = max(n0, mu) + lambda_
         self.combined = population.like(n0 + lambda_, capacity=cap)
@@ -360,6 +453,8 @@ class MuPlusLambdaStep:
                   ctypes.byref(comb.c_pop(n, lam)), ctypes.byref(self.var), ctypes.byref(self.ev),
                   stream.next(), code, ctypes.byref(dec) if dec is not None else None, nevals_ptr)
         comb.resize(n + lam)
+        if self.host_eval is not None:
+            self.last_nevals = self.host_eval(_View(comb, n, lam))       # :319-322
         if halloffame is not None:
             halloffame.update(_View(comb, n, lam))
         sel_op, sel_args, sel_kw = self.sel
@@ -403,17 +498,23 @@ def _mu_lambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen, stats, hallo
     stream = stream or default_stream()
     assert (cxpb + mutpb) <= 1.0, (
         "The sum of the crossover and mutation probabilities must be smaller or equal to 1.0.")
-    ev = _eval(population, resolve(toolbox.evaluate))
+    spec, host = _evaluator(toolbox)
+    ev = _eval(population, spec)
     book = _Bookkeeping(population, ngen, stats, halloffame, verbose)
     ctx = population.ctx.bind()
 
-    _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(ev), 1,
-              book.nevals_ptr(0))
+    if host is None:
+        _lib.call("dm_evaluate", ctx, ctypes.byref(population.c_pop()), ctypes.byref(ev), 1,
+                  book.nevals_ptr(0))
+    else:
+        book.host_nevals[0] = host(population)
     book.record(0, population)
 
     step = MuPlusLambdaStep(population, toolbox, mu, lambda_, cxpb, mutpb, comma=comma)
     for gen in range(1, ngen + 1):
         combined = step.step(stream, book.nevals_ptr(gen), mode, decisions, gen - 1, halloffame)
+        if step.host_eval is not None:
+            book.host_nevals[gen] = step.last_nevals
         rec = stats.compile(combined) if stats else {}
         book.records.append((gen, rec))
         if verbose:

@@ -17,6 +17,7 @@ test_checkpoint_resume_is_bit_exact).
 import json
 
 import numpy as np
+from .device import zeros as _zeros
 
 FORMAT = "deap_amd.checkpoint/1"
 
@@ -122,8 +123,7 @@ def load(path, device=None, individual_class=None, capacity=None):
             pop.wvalues[:n].copy_(torch.from_numpy(z["wvalues"]))
             pop.valid[:n].copy_(torch.from_numpy(z["valid"]))
         if "crowding_dist" in z.files:
-            pop.crowding_dist = torch.zeros((pop.capacity,), dtype=torch.float64,
-                                            device=pop.device)
+            pop.crowding_dist = _zeros((pop.capacity,), torch.float64, pop.device)
             pop.crowding_dist[:n].copy_(torch.from_numpy(z["crowding_dist"]))
     out = {"population": pop, "generation": h.get("generation"), "extra": h.get("extra"),
            "stream": None, "halloffame": None, "logbook": None}

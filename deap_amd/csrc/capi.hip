@@ -320,6 +320,25 @@ __global__ void gather_kernel(const char* sg, const double* swv, const uint8_t* 
     }
 }
 
+// Host-evaluated fitness written back (the scatter half of the host-evaluate
+// bridge): row idx[i] takes wvalues src[i][0..nobj) and becomes valid; a row
+// index outside [0, n) is skipped and counted in *bad.
+__global__ void set_fitness_kernel(double* wv, uint8_t* valid, int nobj, int64_t nrows,
+                                   const int32_t* idx, int64_t k, const double* src, int32_t* bad) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k * nobj;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / nobj;
+        const int o = (int)(t % nobj);
+        const int64_t r = idx[i];
+        if (r < 0 || r >= nrows) {
+            if (o == 0) atomicAdd(bad, 1);
+            continue;
+        }
+        wv[r * nobj + o] = src[i * nobj + o];
+        if (o == 0) valid[r] = 1;
+    }
+}
+
 // Fitness statistics (tools.Statistics over fitness.values, support.py:199-210):
 // per objective the min / max with first-occurrence argmin / argmax (numpy
 // semantics), the count, mean and M2 = sum of squared deviations combined with
@@ -561,6 +580,12 @@ int dm_ctx_sync(dm_ctx* ctx) {
     return DM_OK;
 }
 
+int dm_zero(dm_ctx* ctx, void* ptr, int64_t bytes) {
+    DM_CHECK_ARG(ctx != nullptr && bytes >= 0 && (ptr != nullptr || bytes == 0), "bad argument");
+    if (bytes) DM_HIP(hipMemsetAsync(ptr, 0, (size_t)bytes, ctx->stream));
+    return DM_OK;
+}
+
 int dm_philox_blocks(dm_ctx* ctx, const uint32_t ctr0[4], const uint32_t key[2], int64_t nblocks,
                      uint32_t* out) {
     DM_CHECK_ARG(ctx && ctr0 && key && out && nblocks >= 0, "bad argument");
@@ -691,6 +716,28 @@ int dm_gather(dm_ctx* ctx, const dm_pop* src, const int32_t* idx, dm_pop* dst) {
         (const char*)src->genes, src->wvalues, src->valid, src->stride, (char*)dst->genes,
         dst->wvalues, dst->valid, dst->stride, idx, dst->n, row_bytes, src->nobj);
     DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int dm_set_fitness(dm_ctx* ctx, dm_pop* pop, const int32_t* idx, int64_t k, const double* wv) {
+    DM_CHECK_ARG(ctx && pop && (k == 0 || (idx && wv)), "null argument");
+    DM_CHECK_ARG(k >= 0, "negative count");
+    int rc = validate_pop(pop, "pop");
+    if (rc) return rc;
+    if (k == 0) return DM_OK;
+    int32_t* bad = (int32_t*)scratch(ctx, 16);
+    if (!bad) return DM_ERR_NOMEM;
+    DM_HIP(hipMemsetAsync(bad, 0, 4, ctx->stream));
+    set_fitness_kernel<<<grid_for(ctx, k * pop->nobj, 256), 256, 0, ctx->stream>>>(
+        pop->wvalues, pop->valid, pop->nobj, pop->n, idx, k, wv, bad);
+    DM_LAUNCH_CHECK();
+    int32_t hbad = 0;
+    DM_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    if (hbad) {
+        set_error("dm_set_fitness: %d row indices outside [0, %lld)", hbad, (long long)pop->n);
+        return DM_ERR_INDEX;
+    }
     return DM_OK;
 }
 

@@ -184,9 +184,11 @@ __global__ void em_im_eq_kernel(const void* em_block, const void* im_block, int6
                                 int64_t stride, int dim, int gtype, int nobj, uint8_t* E) {
     Block em = block_view((void*)em_block, stride, nobj, k);
     Block im = block_view((void*)im_block, stride, nobj, k);
+    // stored by immigrant: E[j * k + e] = emigrant e equals immigrant j (the
+    // placement of immigrant j reads row j of it)
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k * k;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = t / k, j = t % k;
+        const int64_t j = t / k, e = t % k;
         E[t] = genome_eq(em.genes + e * stride, im.genes + j * stride, gtype, dim) ? 1 : 0;
     }
 }
@@ -277,6 +279,22 @@ __global__ __launch_bounds__(256) void first_matches_kernel(const unsigned long 
     if (threadIdx.x == 0) mcount[j] = std::min(got, L);
 }
 
+// The identity bitmap of a receiving deme (rows whose original object is no
+// longer in the list, so list.index may not match them by identity), set
+// from each row's FINAL occupant of a hop: a row whose last taker is its own
+// object (a self hop's emigrant from that row, self_rows[j] == slot) has its
+// identity back -- even if an earlier placement of this hop or an earlier hop
+// took it -- every other final occupant is foreign.  Stale placements (a
+// later one took the row) leave the bit alone.
+__device__ __forceinline__ void mark_identity(unsigned long long* dirty, const int32_t* self_rows,
+                                              int64_t j, int64_t slot) {
+    const unsigned long long bit = 1ull << (slot & 63);
+    if (self_rows && self_rows[j] == slot)
+        atomicAnd(&dirty[slot >> 6], ~bit);
+    else
+        atomicOr(&dirty[slot >> 6], bit);
+}
+
 __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid, int64_t n,
                                          int64_t stride, int nobj, const Block& em, int64_t k,
                                          int64_t words, const unsigned long long* bitmap,
@@ -287,6 +305,19 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
     __shared__ int32_t sl[RES_MAX];     // slot of placement j
     __shared__ uint8_t stale[RES_MAX];  // placement j's row was taken by a later one
     __shared__ int32_t smc[RES_MAX];
+    // the rows taken so far, an open-addressing set (load <= 1/2): rule (a)'s
+    // "taken?" is one or two LDS probes instead of a scan over every earlier
+    // placement (O(k^2) per lane at k = 4,096)
+    constexpr int TH = 2 * RES_MAX;
+    __shared__ int32_t taken_set[TH];
+    auto slot_of = [](int32_t row) { return (int)(((uint32_t)row * 2654435761u) >> 19) & (TH - 1); };
+    auto is_taken = [&](int32_t row) {
+        for (int h = slot_of(row);; h = (h + 1) & (TH - 1)) {
+            const int32_t v = taken_set[h];
+            if (v == row) return true;
+            if (v < 0) return false;
+        }
+    };
     constexpr int SM = 64;              // E and the match lists staged in LDS up to k = 64 (C4: 15)
     __shared__ uint8_t sE[SM * SM];
     __shared__ int32_t sml[SM * MLIST];
@@ -295,6 +326,7 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
     const int tid = threadIdx.x, nt = blockDim.x;
     const bool small = k <= SM;
     for (int64_t j = tid; j < k; j += nt) smc[j] = mcount[j];
+    for (int t = tid; t < TH; t += nt) taken_set[t] = -1;
     if (small) {
         for (int64_t t = tid; t < k * k; t += nt) sE[t] = E[t];
         for (int64_t t = tid; t < k * MLIST; t += nt) sml[t] = mlist[t];
@@ -308,9 +340,7 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
         const int mc = smc[j];
         if (tid < mc) {
             const int32_t row = small ? sml[j * MLIST + tid] : mlist[j * MLIST + tid];
-            bool taken = false;
-            for (int64_t p = 0; p < j && !taken; ++p) taken = sl[p] == row;
-            if (!taken) atomicMin(&sbest, (unsigned long long)row);
+            if (!is_taken(row)) atomicMin(&sbest, (unsigned long long)row);
         }
         __syncthreads();
         if (sbest == ~0ull && mc == MLIST) {
@@ -322,9 +352,11 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
                 const int64_t w = wb + tid;
                 unsigned long long x = w < words ? bitmap[j * words + w] : 0ull;
                 if (w == (start >> 6) && (start & 63)) x &= ~0ull << (start & 63);
-                if (x)
-                    for (int64_t p = 0; p < j; ++p)
-                        if ((int64_t)(sl[p] >> 6) == w) x &= ~(1ull << (sl[p] & 63));
+                for (unsigned long long y = x; y; y &= y - 1) {
+                    const int b = __ffsll((long long)y) - 1;
+                    if (is_taken((int32_t)(w * 64 + b))) x &= ~(1ull << b);
+                    else break;  // the lowest untaken row of the word is all rule (a) needs
+                }
                 if (x) atomicMin(&sbest, (unsigned long long)(w * 64 + __ffsll((long long)x) - 1));
                 __syncthreads();
                 if (sbest != ~0ull) break;
@@ -333,7 +365,7 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
         }
         // (b) an earlier emigrant equal to immigrant j, still in its row, at a smaller row
         for (int64_t p = tid; p < j; p += nt)
-            if (!stale[p] && (small ? sE[p * k + j] : E[p * k + j]) &&
+            if (!stale[p] && (small ? sE[j * k + p] : E[j * k + p]) &&
                 (unsigned long long)sl[p] < sbest)
                 atomicMin(&sbest, (unsigned long long)sl[p]);
         __syncthreads();
@@ -349,6 +381,11 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
         if (tid == 0) {
             sl[j] = (int32_t)slot;
             stale[j] = 0;
+            if (!is_taken((int32_t)slot)) {
+                int h = slot_of((int32_t)slot);
+                while (taken_set[h] >= 0) h = (h + 1) & (TH - 1);
+                taken_set[h] = (int32_t)slot;
+            }
         }
         for (int64_t p = tid; p < j; p += nt)
             if ((unsigned long long)sl[p] == slot) stale[p] = 1;
@@ -365,9 +402,7 @@ __device__ void resolve_decide_then_copy(char* genes, double* wv, uint8_t* valid
             valid[slot] = em.valid[j];
         }
         slots[j] = (int32_t)slot;
-        // a self hop that puts a row's own object back keeps its identity
-        if (dirty && !(self_rows && self_rows[j] == slot))
-            atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+        if (dirty && !stale[j]) mark_identity(dirty, self_rows, j, slot);
     }
 }
 
@@ -400,8 +435,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(char* genes, double* wv, u
             for (int o = 0; o < nobj; ++o) wv[slot * nobj + o] = em.wv[j * nobj + o];
             valid[slot] = em.valid[j];
             slots[j] = (int32_t)slot;
-            if (dirty && !(self_rows && self_rows[j] == slot))
-                atomicOr(&dirty[slot >> 6], 1ull << (slot & 63));
+            if (dirty) mark_identity(dirty, self_rows, j, slot);
         }
         return;
     }

@@ -1029,7 +1029,7 @@ static int log_sort_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, bool first_o
 }
 
 __global__ void gather_f64_kernel(const double* src, const int32_t* idx, int64_t n, double* dst) {
-    GRID_LOOP(i, n) dst[i] = src[idx[i]];
+    GRID_LOOP(i, n) dst[i] = src[idx ? idx[i] : i];
 }
 
 }  // namespace dm
@@ -1134,7 +1134,7 @@ extern "C" int dm_sel_nsga2_log(dm_ctx* ctx, const dm_pop* pop, const double* we
 
 extern "C" int dm_gather_f64(dm_ctx* ctx, const double* src, const int32_t* idx, int64_t n,
                              double* dst) {
-    DM_CHECK_ARG(ctx && (n == 0 || (src && idx && dst)), "null argument");
+    DM_CHECK_ARG(ctx && (n == 0 || (src && dst)), "null argument");
     DM_CHECK_ARG(n >= 0, "negative n");
     if (n == 0) return DM_OK;
     gather_f64_kernel<<<g1(n), 256, 0, ctx->stream>>>(src, idx, n, dst);

@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
+from .device import zeros as _zeros
 
 FIELDS = ("aspirants", "cx_flag", "cx_raw", "blend_u", "mut_flag", "mut_mask", "gauss",
           "varor_op", "varor_idx")
@@ -37,20 +38,20 @@ class Decisions:
         words = (dim + 63) // 64
         npairs = k if varor else k // 2
         if tournsize:
-            kw["aspirants"] = torch.zeros((k, tournsize), dtype=torch.int32, device=device)
+            kw["aspirants"] = _zeros((k, tournsize), torch.int32, device)
         if cx:
-            kw["cx_flag"] = torch.zeros((max(npairs, 1),), dtype=torch.uint8, device=device)
-            kw["cx_raw"] = torch.zeros((max(npairs, 1), 2), dtype=torch.int32, device=device)
+            kw["cx_flag"] = _zeros((max(npairs, 1),), torch.uint8, device)
+            kw["cx_raw"] = _zeros((max(npairs, 1), 2), torch.int32, device)
         if blend:
-            kw["blend_u"] = torch.zeros((max(npairs, 1), dim), dtype=torch.float64, device=device)
+            kw["blend_u"] = _zeros((max(npairs, 1), dim), torch.float64, device)
         if mut:
-            kw["mut_flag"] = torch.zeros((k,), dtype=torch.uint8, device=device)
-            kw["mut_mask"] = torch.zeros((k, words), dtype=torch.int64, device=device)
+            kw["mut_flag"] = _zeros((k,), torch.uint8, device)
+            kw["mut_mask"] = _zeros((k, words), torch.int64, device)
         if gauss:
-            kw["gauss"] = torch.zeros((k, dim), dtype=torch.float64, device=device)
+            kw["gauss"] = _zeros((k, dim), torch.float64, device)
         if varor:
-            kw["varor_op"] = torch.zeros((k,), dtype=torch.int32, device=device)
-            kw["varor_idx"] = torch.zeros((k, 2), dtype=torch.int32, device=device)
+            kw["varor_op"] = _zeros((k,), torch.int32, device)
+            kw["varor_idx"] = _zeros((k, 2), torch.int32, device)
         return cls(**kw)
 
     @classmethod

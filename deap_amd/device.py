@@ -98,6 +98,19 @@ class Context:
         _lib.check(_lib.load().dm_ctx_sync(self.handle), "dm_ctx_sync")
 
 
+def zeros(shape, dtype, device):
+    """A zero-filled device tensor: ``torch.empty`` (buffer ownership) zeroed
+    by the library on the current stream (``dm_zero``: hipMemsetAsync), so
+    buffer set-up launches no PyTorch fill kernel."""
+    torch = _torch()
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if t.numel():
+        ctx = Context.get(t.device)
+        _lib.call("dm_zero", ctx.handle, ctypes.c_void_p(t.data_ptr()),
+                  t.numel() * t.element_size())
+    return t
+
+
 @contextlib.contextmanager
 def dominance_path(name, device=None):
     """Run sortNondominated / selNSGA2 on one of the library's cross-check
@@ -126,6 +139,36 @@ def gtype_of(individual_class=None, typecode=None, gtype=None):
     return _lib.DM_F64
 
 
+class FitnessValues:
+    """The unweighted fitness values of a device population (``Fitness.values
+    = wvalues / weights``, deap/base.py:184-185) as returned by a device
+    objective: held as the device's weighted values and turned into numpy on
+    the host when read (``numpy()``, ``np.asarray``, or ``cpu()`` for a
+    torch CPU tensor), so an evaluation call launches no division kernel and
+    copies nothing until the values are used."""
+
+    def __init__(self, wvalues, weights):
+        self._wv = wvalues
+        self._w = np.asarray(weights, dtype=np.float64)
+
+    def numpy(self):
+        return self._wv.cpu().numpy() / self._w
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.numpy()
+        return a if dtype is None else a.astype(dtype)
+
+    def cpu(self):
+        return _torch().from_numpy(self.numpy())
+
+    @property
+    def shape(self):
+        return tuple(self._wv.shape)
+
+    def __len__(self):
+        return int(self._wv.shape[0])
+
+
 class DevicePopulation:
     """A population resident on one GPU (SoA).  ``len(pop)`` is the number of
     individuals; rows ``[0, len)`` are live.  Drivers swap storage in place so
@@ -148,10 +191,9 @@ class DevicePopulation:
             raise ValueError("n > capacity")
         self.n = int(n)
         self.individual_class = individual_class
-        self.genes = torch.zeros((self.capacity, self.stride), dtype=torch.uint8, device=self.device)
-        self.wvalues = torch.zeros((self.capacity, self.nobj), dtype=torch.float64,
-                                   device=self.device)
-        self.valid = torch.zeros((self.capacity,), dtype=torch.uint8, device=self.device)
+        self.genes = zeros((self.capacity, self.stride), torch.uint8, self.device)
+        self.wvalues = zeros((self.capacity, self.nobj), torch.float64, self.device)
+        self.valid = zeros((self.capacity,), torch.uint8, self.device)
         self.crowding_dist = None  # set by selNSGA2 / assignCrowdingDist
 
     # -- C view -------------------------------------------------------------
@@ -209,10 +251,10 @@ class DevicePopulation:
         return rows.view(torch.float64)[:, : self.dim]
 
     def fitness_values(self):
-        """Unweighted values ``wvalues / weights`` (``deap/base.py:184-185``) as a tensor."""
-        torch = _torch()
-        w = torch.tensor(self.weights, dtype=torch.float64, device=self.device)
-        return self.wvalues[: self.n] / w
+        """Unweighted values ``wvalues / weights`` (``deap/base.py:184-185``),
+        read lazily: :class:`FitnessValues` copies the weighted values to the
+        host and divides there when asked (no device kernel)."""
+        return FitnessValues(self.wvalues[: self.n], self.weights)
 
     # -- host transfer ---------------------------------------------------------
     def genes_numpy(self):

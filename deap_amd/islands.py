@@ -30,6 +30,7 @@ import torch.distributed as dist
 from . import _lib
 from .ops import resolve
 from .tools.migration import pack, place, replacement_indices
+from .device import zeros as _zeros
 
 
 def migRingDistributed(demes, deme_ids, n_demes, k, selection, replacement=None,
@@ -284,7 +285,7 @@ def eaSimpleDemes(demes, toolbox, cxpb, mutpb, ngen, mig_every=5, *, deme_ids=No
     # a rank may hold no deme (any split, owner_map): it still joins every
     # migration, which is collective
     dev = demes[0].device if demes else torch.device("cuda", torch.cuda.current_device())
-    nev = torch.zeros((len(demes), ngen + 1), dtype=torch.int64, device=dev)
+    nev = _zeros((len(demes), ngen + 1), torch.int64, dev)
     logbook = Logbook()
     logbook.header = ["gen", "deme", "evals"] + (stats.fields if stats else [])
     recs = []

@@ -15,6 +15,7 @@ from collections.abc import Sequence
 import numpy as np
 
 from .. import _lib
+from ..device import zeros as _zeros
 
 
 def _arg(args, kwargs, pos, name, op):
@@ -114,12 +115,10 @@ def vary_bounded(population, index, sbx, poly, cxpb, decisions=None, mode=None, 
             raise ValueError("mode %r needs a decisions dict" % mode)
         if code == _lib.DM_RNG_DUMP:
             if sbx is not None:
-                decisions["cx_u"] = torch.zeros((max(pairs, 1),), dtype=torch.float64, device=dev)
-                decisions["sbx_u"] = torch.zeros((max(pairs, 1), dim, 3), dtype=torch.float64,
-                                                 device=dev)
+                decisions["cx_u"] = _zeros((max(pairs, 1),), torch.float64, dev)
+                decisions["sbx_u"] = _zeros((max(pairs, 1), dim, 3), torch.float64, dev)
             if poly is not None:
-                decisions["mut_u"] = torch.zeros((max(nmut, 1), dim, 2), dtype=torch.float64,
-                                                 device=dev)
+                decisions["mut_u"] = _zeros((max(nmut, 1), dim, 2), torch.float64, dev)
         if sbx is not None:
             cx_u = decisions["cx_u"].to(device=dev, dtype=torch.float64).contiguous()
             sbx_u = decisions["sbx_u"].to(device=dev, dtype=torch.float64).contiguous()

@@ -13,13 +13,28 @@ Results are device ``int32`` index tensors in the reference's order:
 """
 import ctypes
 
+import numpy as np
+
 from .. import _lib
 from ..ops import DeviceOperator
+from ..device import zeros as _zeros
 
 
 def _torch():
     import torch
     return torch
+
+
+def _host_array(x):
+    """A host numpy view of an index / decision array (device tensors are
+    copied, never computed on)."""
+    if hasattr(x, "detach"):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _host_index(front):
+    return np.ascontiguousarray(_host_array(front), dtype=np.int32).ravel()
 
 
 def _check(individuals):
@@ -78,18 +93,21 @@ class _CrowdingDist(DeviceOperator):
             return
         dev = individuals.device
         if fronts is None:
-            order = torch.arange(n, dtype=torch.int32, device=dev)
-            fstart = torch.tensor([0, n], dtype=torch.int32, device=dev)
+            order = torch.from_numpy(np.arange(n, dtype=np.int32)).to(dev)
+            fstart = torch.from_numpy(np.array([0, n], dtype=np.int32)).to(dev)
             nf = 1
         else:
-            order = torch.cat([f.to(torch.int32) for f in fronts]) if fronts else \
-                torch.empty((0,), dtype=torch.int32, device=dev)
-            sizes = [0] + [len(f) for f in fronts]
-            fstart = torch.tensor(sizes, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+            # user-supplied fronts: concatenated on the host (one copy each
+            # way, no device kernel); the library's own selNSGA2 never takes
+            # this path
+            parts = [_host_index(f) for f in fronts]
+            order = torch.from_numpy(np.concatenate(parts) if parts else
+                                     np.zeros(0, np.int32)).to(dev)
+            sizes = np.cumsum([0] + [len(f) for f in parts]).astype(np.int32)
+            fstart = torch.from_numpy(sizes).to(dev)
             nf = len(fronts)
         if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
-            individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
-                                                    device=dev)
+            individuals.crowding_dist = _zeros((individuals.capacity,), torch.float64, dev)
         ctx = individuals.ctx.bind()
         _lib.call("dm_crowding_dist", ctx, ctypes.byref(individuals.c_pop()), _weights(individuals),
                   ctypes.c_void_p(order.data_ptr()), ctypes.c_void_p(fstart.data_ptr()), nf,
@@ -112,8 +130,8 @@ class _SelNSGA2(DeviceOperator):
         k = int(k)
         out = torch.empty((max(k, 1),), dtype=torch.int32, device=individuals.device)
         if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
-            individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
-                                                    device=individuals.device)
+            individuals.crowding_dist = _zeros((individuals.capacity,), torch.float64,
+                                                individuals.device)
         if k == 0 or n == 0:
             return out[:0]
         ctx = individuals.ctx.bind()
@@ -168,8 +186,8 @@ def _sel_nsga2_log(individuals, k):
     n = len(individuals)
     out = torch.empty((max(k, 1),), dtype=torch.int32, device=individuals.device)
     if individuals.crowding_dist is None or len(individuals.crowding_dist) < n:
-        individuals.crowding_dist = torch.zeros((individuals.capacity,), dtype=torch.float64,
-                                                device=individuals.device)
+        individuals.crowding_dist = _zeros((individuals.capacity,), torch.float64,
+                                           individuals.device)
     if k == 0 or n == 0:
         return out[:0]
     ctx = individuals.ctx.bind()
@@ -208,25 +226,24 @@ class _SelTournamentDCD(DeviceOperator):
             if code == _lib.DM_RNG_DUMP:
                 decisions["perm1"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
                 decisions["perm2"] = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
-                decisions["coin"] = torch.zeros((max(k4, 1),), dtype=torch.uint8, device=dev)
+                decisions["coin"] = _zeros((max(k4, 1),), torch.uint8, dev)
             else:
                 # injected decisions: device tensors of the kernel's dtypes, long
                 # enough, and permutations of range(n) (the kernel dereferences
                 # fitness rows through them)
+                # (checked on the host: no device kernel)
                 decisions = dict(decisions)
-                for name, dt, need in (("perm1", torch.int32, n), ("perm2", torch.int32, n),
-                                       ("coin", torch.uint8, k4)):
-                    t = torch.as_tensor(decisions[name]).to(device=dev, dtype=dt).contiguous()
-                    if t.numel() < need:
+                for name, dt, need in (("perm1", np.int32, n), ("perm2", np.int32, n),
+                                       ("coin", np.uint8, k4)):
+                    h = np.ascontiguousarray(_host_array(decisions[name]), dtype=dt).ravel()
+                    if h.size < need:
                         raise ValueError("decisions[%r] holds %d values, %d needed"
-                                         % (name, t.numel(), need))
-                    decisions[name] = t
-                for name in ("perm1", "perm2"):
-                    p = decisions[name][:n]
-                    if n and not bool(torch.equal(torch.sort(p).values,
-                                                  torch.arange(n, dtype=torch.int32, device=dev))):
+                                         % (name, h.size, need))
+                    if name != "coin" and n and not np.array_equal(np.sort(h[:n]),
+                                                                   np.arange(n, dtype=np.int32)):
                         raise ValueError("decisions[%r] is not a permutation of range(%d)"
                                          % (name, n))
+                    decisions[name] = torch.from_numpy(h).to(dev)
             p1, p2, coin = decisions["perm1"], decisions["perm2"], decisions["coin"]
         ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
         ctx = individuals.ctx.bind()

@@ -44,24 +44,6 @@ def _is_values_key(key):
         return False
 
 
-_DEVICE_REDUCERS = {}
-
-
-def _device_reducer(func):
-    try:
-        _DEVICE_REDUCERS[np.mean] = lambda t, axis: t.mean() if axis is None else t.mean(dim=axis)
-        _DEVICE_REDUCERS[np.std] = (lambda t, axis: t.std(unbiased=False) if axis is None
-                                    else t.std(dim=axis, unbiased=False))
-        _DEVICE_REDUCERS[np.min] = lambda t, axis: t.min() if axis is None else t.min(dim=axis).values
-        _DEVICE_REDUCERS[np.max] = lambda t, axis: t.max() if axis is None else t.max(dim=axis).values
-        _DEVICE_REDUCERS[np.sum] = lambda t, axis: t.sum() if axis is None else t.sum(dim=axis)
-        _DEVICE_REDUCERS[np.amin] = _DEVICE_REDUCERS[np.min]
-        _DEVICE_REDUCERS[np.amax] = _DEVICE_REDUCERS[np.max]
-    except AttributeError:
-        pass
-    return _DEVICE_REDUCERS.get(func)
-
-
 def _identity(obj):
     return obj
 
@@ -93,28 +75,24 @@ class Statistics:
             return {name: fn(values) for name, fn in self.functions.items()}
         out = {}
         host = None
-        vals = None
         kstats = None
         for name, fn in self.functions.items():
             kw = dict(fn.keywords or {})
             axis = kw.pop("axis", None)
             pick = _KERNEL_STATS.get(fn.func)
-            if pick is not None and not fn.args and not kw and \
-                    (axis == 0 or (axis is None and pop.nobj == 1)):
-                # one dm_fitness_stats pass serves every such reducer
+            if pick is not None and not fn.args and not kw and axis in (None, 0):
+                # one dm_fitness_stats pass serves every such reducer: per
+                # objective (axis=0), or over all values (axis=None: the
+                # objectives' rows combined on the host)
                 if kstats is None:
                     kstats = _KernelStats(pop)
-                out[name] = functools.partial(kstats.value, pick, axis)
+                out[name] = functools.partial(kstats.value, fn.func, axis)
                 continue
-            red = _device_reducer(fn.func)
-            if red is not None and not fn.args and not kw:
-                if vals is None:
-                    vals = pop.fitness_values()
-                out[name] = functools.partial(_to_numpy, red(vals, axis))
-            else:
-                if host is None:
-                    host = tuple(tuple(r) for r in pop.fitness_values().cpu().numpy().tolist())
-                out[name] = fn(host)
+            # any other reducer: the reference's call on host values (one copy
+            # of the weighted fitness, divided by the weights on the host)
+            if host is None:
+                host = tuple(tuple(r) for r in pop.fitness_values().numpy().tolist())
+            out[name] = fn(host)
         return out
 
 
@@ -148,19 +126,58 @@ class _KernelStats:
             self._host = self.out.cpu().numpy().reshape(self.nobj, 8)
         return self._host
 
-    def value(self, pick, axis):
+    def value(self, func, axis):
         rows = self.rows()
-        if axis is None:
+        pick = _KERNEL_STATS[func]
+        if axis == 0:
+            return np.array([pick(r) for r in rows])
+        if self.nobj == 1:
             return np.float64(pick(rows[0])) if pick not in _INT_PICKS else pick(rows[0])
-        return np.array([pick(r) for r in rows])
+        return _combined(func, rows, self.nobj)
+
+
+def _combined(func, rows, nobj):
+    """``func(values)`` over every objective value of the population (axis
+    None on ``nobj`` > 1 objectives: numpy flattens the [n][nobj] tuple)
+    from the per-objective rows {min, max, mean, m2, sum, argmin, argmax,
+    count}: extrema of the extrema, sums of the sums, the Welford parts
+    combined (Chan et al.) for mean / var / std, and for argmin / argmax the
+    first flattened position (row * nobj + objective) holding the extremum."""
+    mn, mx, mean, m2, sm, amn, amx, cnt = (np.array([r[i] for r in rows]) for i in range(8))
+    if func in (np.min, np.amin):
+        return np.float64(np.min(mn))
+    if func in (np.max, np.amax):
+        return np.float64(np.max(mx))
+    if func is np.sum:
+        return np.float64(np.sum(sm))
+    total = np.sum(cnt)
+    if func in (np.argmin, np.argmax):
+        ext, arg = (mn, amn) if func is np.argmin else (mx, amx)
+        best = np.min(ext) if func is np.argmin else np.max(ext)
+        flat = [int(arg[o]) * nobj + o for o in range(nobj) if ext[o] == best]
+        return np.int64(min(flat)) if flat else np.int64(0)
+    if not total:
+        return np.float64("nan")
+    mu = np.sum(cnt * mean) / total
+    if func is np.mean:
+        return np.float64(mu)
+    var = (np.sum(m2) + np.sum(cnt * (mean - mu) ** 2)) / total
+    return np.float64(var if func is np.var else np.sqrt(var))
 
 
 _INT_PICKS = (_KERNEL_STATS[np.argmin], _KERNEL_STATS[np.argmax])
 
 
-def _to_numpy(t):
-    a = t.detach().cpu().numpy()
-    return a[()] if a.ndim == 0 else a
+def _typed_rows(pop, raw):
+    """Host rows of raw genome bytes ([rows][stride] uint8) as the typed
+    genome words genes_view() gives: int64 words for packed bits, else the
+    float genes."""
+    from .. import _lib
+    if pop.gtype == _lib.DM_BITS:
+        return raw.view(np.int64)[:, : (pop.dim + 63) // 64]
+    if pop.gtype == _lib.DM_F32:
+        return raw.view(np.float32)[:, : pop.dim]
+    return raw.view(np.float64)[:, : pop.dim]
 
 
 class MultiStatistics(dict):
@@ -363,10 +380,18 @@ class HallOfFame:
         on the stream after this call is not waited for) and yields
         (order, rows, genes, wvalues, valid) for _try_candidates."""
         import torch
+        from .. import _lib
         from .selection import selBest
-        order = selBest(pop, K).to(torch.int64)
-        idx = torch.cat([order, torch.zeros(1, dtype=torch.int64, device=order.device)])
-        dev = (idx, pop.genes_view()[idx], pop.wvalues[: len(pop)][idx], pop.valid[: len(pop)][idx])
+        order = selBest(pop, K)  # int32 rows, fitness descending (device)
+        # the K rows and row 0 gathered by the library (dm_gather) into a
+        # candidate population of the same layout: no PyTorch index kernels
+        cand = self._candidates_buffer(pop, K + 1)
+        ctx = pop.ctx.bind()
+        _lib.call("dm_gather", ctx, ctypes.byref(pop.c_pop()), ctypes.c_void_p(order.data_ptr()),
+                  ctypes.byref(cand.c_pop(0, K)))
+        _lib.call("dm_gather", ctx, ctypes.byref(pop.c_pop(0, 1)), None,
+                  ctypes.byref(cand.c_pop(K, 1)))
+        dev = (order, cand.genes[: K + 1], cand.wvalues[: K + 1], cand.valid[: K + 1])
         host = self._staging(dev)
         for h, t in zip(host, dev):
             h.copy_(t, non_blocking=True)
@@ -376,8 +401,19 @@ class HallOfFame:
         def wait():
             done.synchronize()
             o, g, w, v = (h.numpy() for h in host)
-            return o, g, w, v
+            idx = np.append(o.astype(np.int64), 0)
+            return idx, _typed_rows(pop, g), w, v
         return wait
+
+    def _candidates_buffer(self, pop, rows):
+        """A DevicePopulation of ``pop``'s layout with room for ``rows`` rows,
+        kept between updates (grown when a larger K is asked for)."""
+        buf = self.__dict__.get("_cand")
+        if (buf is None or buf.capacity < rows or buf.stride != pop.stride or
+                buf.gtype != pop.gtype or buf.nobj != pop.nobj or buf.device != pop.device):
+            buf = self.__dict__["_cand"] = pop.like(rows, capacity=max(rows, 256))
+        buf.resize(rows)
+        return buf
 
     def _staging(self, dev):
         """Pinned host buffers for one candidate gather, two sets used in
@@ -471,7 +507,7 @@ class HallOfFame:
 
     def __getstate__(self):
         state = dict(self.__dict__)
-        for k in ("_garr", "_pinned", "_pinned_turn"):
+        for k in ("_garr", "_pinned", "_pinned_turn", "_cand"):  # transient device buffers
             state.pop(k, None)
         return state
 

@@ -146,6 +146,10 @@ int dm_ctx_create(int device, void* hip_stream, dm_ctx** out);
 int dm_ctx_destroy(dm_ctx* ctx);
 int dm_ctx_set_stream(dm_ctx* ctx, void* hip_stream);
 int dm_ctx_sync(dm_ctx* ctx);  /* hipStreamSynchronize on the ctx stream */
+/* Zero `bytes` bytes of device memory at `ptr` on the ctx stream
+ * (hipMemsetAsync): buffer set-up (population rows, counters, crowding
+ * distances) without a host-framework fill kernel. */
+int dm_zero(dm_ctx* ctx, void* ptr, int64_t bytes);
 /* Measurement hook (no reference counterpart; used by bench.py): record a HIP
  * event pair on the ctx stream around each of the next `max_launches`
  * generation-kernel launches of dm_generation (0 = off).  dm_ctx_kernel_times
@@ -220,6 +224,13 @@ int dm_sel_worst(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx);
  * dst row r <- src row idx[r] (genome, wvalues, valid). */
 int dm_gather(dm_ctx* ctx, const dm_pop* src, const int32_t* idx, dm_pop* dst);
 
+/* The scatter half of the host-evaluate bridge (a plain Python `evaluate`
+ * such as the reference README's evalOneMax, algorithms.py:171-174
+ * `ind.fitness.values = fit`): wvalues[idx[i]] = wv[i][0..nobj) and
+ * valid[idx[i]] = 1 for i < k (wv: device, k x nobj weighted values).
+ * DM_ERR_INDEX if an index is outside [0, pop->n).  Host-synchronising. */
+int dm_set_fitness(dm_ctx* ctx, dm_pop* pop, const int32_t* idx, int64_t k, const double* wv);
+
 /* ---- variation / fused generation ----------------------------------------- */
 /* One eaSimple generation body (algorithms.py:163-181), fused:
  *   select (per `sel`) -> clone -> varAnd (algorithms.py:33-82) -> evaluate
@@ -275,7 +286,8 @@ int dm_sort_log_nondominated(dm_ctx* ctx, const dm_pop* pop, int64_t k,
 int dm_sel_nsga2_log(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                      int64_t k, int32_t* out_idx, double* crowd);
 /* dst[i] = src[idx[i]] for i < n (fitness.crowding_dist carried with a
- * selection's clones, algorithms.py:329 select + base.py:252-261). */
+ * selection's clones, algorithms.py:329 select + base.py:252-261); idx NULL:
+ * dst[i] = src[i]. */
 int dm_gather_f64(dm_ctx* ctx, const double* src, const int32_t* idx, int64_t n,
                   double* dst);
 

@@ -203,3 +203,33 @@ def test_self_hop_keeps_identity_for_a_later_hop(gpu):
     g0, _, _ = demes[0].to_numpy()
     assert np.array_equal(g0, np.array(host[0]), equal_nan=True)
     assert np.array_equal(g0[2], genes[1][2])
+
+
+def test_row_taken_and_restored_in_a_self_hop_keeps_identity(gpu):
+    """within one self hop a row is first taken by another emigrant
+    and then gets its own object back; the row's identity must follow its
+    FINAL occupant.  Deme 0 = [x (NaN genome, list.index finds it only by
+    identity), e0]; selBest(2) = [e0, x] emigrate, selWorst(2) = [x, e0] are
+    replaced; migarray [0, 0]: the self hop puts e0 into x's row and then x
+    back into it, so the second hop (deme 1 -> deme 0) still finds x there by
+    identity (deap/tools/migration.py:39-51, restated below with Python lists
+    of the same objects)."""
+    from deap_amd import tools
+    from deap_amd.device import DevicePopulation
+
+    genes = [np.arange(8, dtype=np.float64).reshape(2, 4) + 100 * d for d in range(2)]
+    genes[0][0, 1] = np.nan
+    fits = [np.array([[1.0], [5.0]]), np.array([[3.0], [4.0]])]
+    demes = [DevicePopulation.from_numpy(g, (1.0,), wvalues=f, valid=np.ones(2))
+             for g, f in zip(genes, fits)]
+    host = [[list(r) for r in g] for g in genes]
+    em = [[host[d][1], host[d][0]] for d in range(2)]   # selBest(2): fitness descending
+    imm = [[host[d][0], host[d][1]] for d in range(2)]  # selWorst(2): ascending
+    for frm, to in enumerate([0, 0]):
+        for i, x in enumerate(imm[to]):
+            host[to][host[to].index(x)] = em[frm][i]
+    assert host[0][0] is em[1][0] and host[0][1] is em[1][1]
+    tools.migRing(demes, 2, tools.selBest, replacement=tools.selWorst, migarray=[0, 0])
+    g0, _, _ = demes[0].to_numpy()
+    assert np.array_equal(g0, np.array(host[0]), equal_nan=True)
+    assert np.array_equal(g0, genes[1][[1, 0]])

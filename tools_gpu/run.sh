@@ -38,6 +38,18 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
           step digests_${per}_$1 300 python bench.py --gpus 1 --islands-per-gpu $per --steps $1 --warmup $2 --no-cpu-baseline --digests-out $OUT/deme_digests.json
         done
       done ;;
+    native)  # the product loops launch library kernels only (no at::native after the marker)
+      for ph in easimple c5 c5x; do
+        step native_$ph 300 $KT -d $OUT/native_$ph -- python3 tools_gpu/native_free_probe.py $ph
+        step native_${ph}_names 60 python3 tools_gpu/trace_names.py $OUT/native_$ph/run_kernel_trace.csv $OUT/native_$ph.json
+      done ;;
+    migab)  # placement cost at k = 4,096 with heavy duplicates: this library vs libdeapmi_migold.so
+      for v in new old; do
+        lib=$PWD/deap_amd/libdeapmi.so; [ $v = old ] && lib=$PWD/deap_amd/libdeapmi_migold.so
+        export DEAPMI_LIB=$lib
+        step migab_$v 300 $KT -d $OUT/migab_$v -- python3 -m pytest tests/test_gpu_islands.py -q -x -k "heavy_duplicates"
+        unset DEAPMI_LIB
+      done ;;
     alloc)
       for m in base mid:8 mid:16 mid:24 mid:32 mid:16 post:16 base; do
         step alloc_${m/:/_} 120 python tools_gpu/alloc_order_probe.py $m 20
