@@ -146,3 +146,4 @@ def test_selbest_fullsort_knob(gpu, k):
         worst = tools.selWorst(pop, k).cpu().numpy().tolist()
     assert best == ops.sel_best(wv, k).tolist()
     assert worst == ops.sel_worst(wv, k).tolist()
+
