@@ -22,23 +22,33 @@ fn = lib.dm_debug_peel_prof
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 buf = np.zeros((1 << 17, 8), np.uint64)
+ctx = pop.ctx.bind()
+cap = 1024
 for rep in range(3):
+    if rep == 2:  # the last selection also timed per peel launch by library events
+        _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_PEEL)
+        _lib.call("dm_ctx_set_timing", ctx, cap)
     tools.selNSGA2(pop, n // 2)
     torch.cuda.synchronize()
     k = fn(buf.ctypes.data, 1 << 17)
+times = (ctypes.c_float * cap)()
+cnt = ctypes.c_int32(0)
+_lib.call("dm_ctx_kernel_times", ctx, times, cap, ctypes.byref(cnt))
+_lib.call("dm_ctx_set_timing", ctx, 0)
+ev_us = [t * 1e3 for t in times[:cnt.value]]
 a = buf[:k].astype(np.int64)
 # launches: a new launch starts when F changes or the start clock jumps
 order = np.argsort(a[:, 3], kind="stable")
 a = a[order]
 cut = np.flatnonzero(np.diff(a[:, 3]) > 300) + 1  # > 3 us gap between workgroup starts
 tot = 0.0
-print("launch  F  wgs  span_us  max(pro) max(mem) max(rel)  mean(mem) mean(rel)  [us]")
+print("launch  F  wgs  span_us  max(pro) max(mem) max(rel)  mean(mem) mean(rel)  event_us  [us]")
 for i, g in enumerate(np.split(a, cut)):
     span = (g[:, 6].max() - g[:, 3].min()) / 100.0
     pro = (g[:, 4] - g[:, 3]) / 100.0
     mem = (g[:, 5] - g[:, 4]) / 100.0
     rel = (g[:, 6] - g[:, 5]) / 100.0
     tot += span
-    print("%3d %6d %5d %7.1f %7.1f %7.1f %7.1f %7.1f %7.1f" % (i, g[0, 2], len(g), span, pro.max(),
-          mem.max(), rel.max(), mem.mean(), rel.mean()))
+    print("%3d %6d %5d %7.1f %7.1f %7.1f %7.1f %7.1f %7.1f %7.1f" % (i, g[0, 2], len(g), span, pro.max(),
+          mem.max(), rel.max(), mem.mean(), rel.mean(), ev_us[i] if i < len(ev_us) else -1))
 print("sum of spans %.1f us over %d launches" % (tot, len(cut) + 1))
