@@ -48,7 +48,7 @@ def _lib_built():
     return os.path.exists(_lib.LIB_PATH)
 
 
-@pytest.mark.parametrize("gpus,per", [(2, 1), (2, 2), (4, 1)])
+@pytest.mark.parametrize("gpus,per", [(2, 1), (2, 2), (4, 1), (8, 1)])
 def test_gpus_n_launches_n_ranks(gpus, per):
     if not _lib_built():
         pytest.skip("libdeapmi.so not built")
