@@ -23,7 +23,7 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_c3) step bench_c3 400 python bench.py --steps 20 --warmup 5 ;;
     bench_c3q) step bench_c3q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-    bench_c2) step bench_c2 200 python bench.py --config c2 --steps 200 --warmup 200 --no-cpu-baseline ;;
+    bench_c2) step bench_c2 200 python bench.py --config c2 --steps 100 --warmup 5 ;;
     bench_c4) step bench_c4 400 python bench.py --islands 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench_c5) step bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
     bench_c5q) step bench_c5q 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline ;;
