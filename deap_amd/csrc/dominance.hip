@@ -1364,7 +1364,7 @@ static size_t ranks_work_bytes(int64_t n, int64_t U) {
 }
 static size_t fronts_work_bytes(int64_t U) {
     return align_up(sizeof(FrontState), 256) + 3 * align_up((size_t)U * 8, 256) +
-           2 * align_up((size_t)U * 4, 256) + 256 + radix_sort_temp_bytes(U);
+           2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
 }
 static FastLayout fast_layout(int64_t n, int64_t U) {
     FastLayout L;
@@ -1547,10 +1547,6 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     // sliced peels: per v the max (front + 1, last releasing position)
     unsigned long long* lastq = (unsigned long long*)p;
     p += align_up((size_t)U * 8, 256);
-    // persistent peel: barrier counter and error flag
-    unsigned* bar = (unsigned*)p;
-    int32_t* perr = (int32_t*)(p + 192);  // bar[0]: arrivals, bar[16]: ordered front
-    p += 256;
     void* rtemp = p;
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
