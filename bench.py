@@ -681,6 +681,39 @@ def max_over_ranks(values, device):
     return [float(x) for x in t.tolist()]
 
 
+def save_state(pops, stream, step=None):
+    """Device copies of populations (rows, fitness, validity, crowding) and
+    the stream / step counters, for restore_state after an untimed top-up
+    that advances them (C5, C5x)."""
+    import torch
+    copies = []
+    for p in pops:
+        cd = p.crowding_dist
+        copies.append((p, p.n, p.genes.clone(), p.wvalues.clone(), p.valid.clone(),
+                       None if cd is None else cd.clone()))
+    torch.cuda.synchronize()
+    return copies, (stream, stream.getstate()), step, (step.n if step is not None else None)
+
+
+def restore_state(saved):
+    import torch
+    copies, (stream, st), step, n = saved
+    stream.setstate(st)
+    for p, pn, g, w, v, cd in copies:
+        p.resize(pn)
+        p.genes.copy_(g)
+        p.wvalues.copy_(w)
+        p.valid.copy_(v)
+        if cd is not None:
+            if p.crowding_dist is None or p.crowding_dist.shape != cd.shape:
+                p.crowding_dist = cd
+            else:
+                p.crowding_dist.copy_(cd)
+    if step is not None:
+        step.n = n
+    torch.cuda.synchronize()
+
+
 def warm_until(args, fn):
     """The untimed --warmup-secs top-up: call fn() until that much wall time
     has passed (at least once when --warmup-secs > 0); returns the count."""
@@ -739,7 +772,11 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     step = algorithms.MuPlusLambdaStep(pop, tb, n, n, 0.6, 0.3)
     for _ in range(args.warmup):
         step.step(stream)
+    # the top-up evolves a copy of the state: the timed steps start from the
+    # population --warmup steps leave, whatever the top-up's length
+    saved = save_state([step.combined], stream, step)
     extra_warm = warm_until(args, lambda: step.step(stream))
+    restore_state(saved)
     replica_barrier(world)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
     t0 = time.perf_counter()
@@ -922,7 +959,9 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
 
     for _ in range(args.warmup):
         one_gen(False)
+    saved = save_state([pop], stream)
     extra_warm = warm_until(args, lambda: one_gen(False))
+    restore_state(saved)
     replica_barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
