@@ -522,6 +522,55 @@ struct FrontState {
     int64_t U;
 };
 
+// Released candidates go to eight slot buckets (bucket = the releasing
+// workgroup's chunk or segment index mod 8) instead of one shared counter:
+// every workgroup of a peel launch that releases something took a returning
+// atomic on st->ncand and st->pending, and ~400 of them serialised on those
+// two addresses (the release phase's slowest workgroup took 7-19 us on the
+// fronts of a few hundred members, profiles/r05_peelphase).  Bucket b's
+// counters live in their own 4-KB page after the state (st + 4096 (b + 1):
+// slot count, and the released individuals at +64), its candidates in slots
+// [b cap, b cap + count) of ckey / cq / crec, cap = cand_cap(U) (room for
+// every v of the chunks of 512 or segments of 1,024 that map to it).  The
+// ordering reads the eight ranges as one list (CandMap) and resets the
+// counters.
+constexpr int CAND_BUCKETS = 8;
+constexpr size_t CAND_PAGE = 4096;
+__host__ __device__ __forceinline__ int64_t cand_cap(int64_t U) { return (U + 8191) / 8192 * 1024; }
+__device__ __forceinline__ int32_t* cand_count(FrontState* st, int b) {
+    return reinterpret_cast<int32_t*>(reinterpret_cast<char*>(st) + CAND_PAGE * (b + 1));
+}
+__device__ __forceinline__ unsigned long long* cand_pending(FrontState* st, int b) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(st) + CAND_PAGE * (b + 1) + 64);
+}
+// candidate i of the ordering's list -> its slot
+struct CandMap {
+    int32_t pre[CAND_BUCKETS + 1];  // bucket starts in the list (pre[8] = n)
+    int64_t cap;                    // 0: the list is contiguous (presorted, overflow path)
+    // static indices only (a dynamic pre[b] put the map in scratch memory)
+    __device__ __forceinline__ int64_t slot(int32_t i) const {
+        if (!cap) return i;
+        int32_t base = 0;
+        int64_t off = 0;
+#pragma unroll
+        for (int k = 1; k < CAND_BUCKETS; ++k)
+            if (i >= pre[k]) {
+                base = pre[k];
+                off = k * cap;
+            }
+        return off + (i - base);
+    }
+    // the workgroup-uniform map in scalar registers
+    __device__ __forceinline__ CandMap uniform() const {
+        CandMap m;
+#pragma unroll
+        for (int k = 0; k <= CAND_BUCKETS; ++k) m.pre[k] = __builtin_amdgcn_readfirstlane(pre[k]);
+        m.cap = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)cap) |
+                ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(cap >> 32)) << 32);
+        return m;
+    }
+};
+
 #ifndef DM_PEEL_WAVES
 #define DM_PEEL_WAVES 8
 #endif
@@ -808,8 +857,9 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
                 tot += c;
                 gtot += S.wgs[it][wv];
             }
-        S.sbase = tot ? atomicAdd(&st->ncand, tot) : 0;
-        if (gtot) atomicAdd((unsigned long long*)&st->pending, (unsigned long long)gtot);
+        const int b = (int)((vbase / (PW * 64)) & (CAND_BUCKETS - 1));
+        S.sbase = tot ? (int32_t)(b * cand_cap(U)) + atomicAdd(cand_count(st, b), tot) : 0;
+        if (gtot) atomicAdd(cand_pending(st, b), (unsigned long long)gtot);
     }
     __syncthreads();
 #pragma unroll
@@ -817,7 +867,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         if (!fresh[it]) continue;
         const int64_t v = vbase + threadIdx.x + it * PEEL_WAVES * 64;
         const int32_t slot = S.sbase + S.wcnt[it][wave] + __popcll(fm[it] & ((1ull << lane) - 1));
-        if (!BD_OK(slot, U, "release slot") || !BD_OK(vu[it], U, "release vu")) continue;
+        if (!BD_OK(slot, CAND_BUCKETS * cand_cap(U), "release slot") || !BD_OK(vu[it], U, "release vu")) continue;
         cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
         cst<COH>(cq + slot, (int32_t)v);
         if (cr.crec) cr.crec[slot] = rq[it];
@@ -1074,12 +1124,12 @@ __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t
 template <int NT, int E, bool COH>
 __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2* mout,
                              const int32_t* pos, const int32_t* nseg, uint64_t* lds,
-                             const MemberTab& mt, int4* tout) {
+                             const MemberTab& mt, int4* tout, const CandMap& cm) {
     uint64_t k[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = threadIdx.x * E + e;
-        k[e] = i < n ? cld<COH>(ckey + i) : ~0ull;
+        k[e] = i < n ? cld<COH>(ckey + cm.slot(i)) : ~0ull;
     }
     block_bitonic<NT, E>(k, lds);
 #pragma unroll
@@ -1107,6 +1157,8 @@ union OrderLds {
 };
 struct OrderScalars {
     int32_t sn, sgo, snstart, sF, smax;
+    int64_t spending;  // individuals of the candidates (the buckets' sums)
+    CandMap cm;
 };
 
 // Orders the released candidates by (last releasing position l, U index) and
@@ -1146,6 +1198,98 @@ __device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* sh) {
     return x - v + (wave ? sh[wave - 1] : 0);
 }
 
+// The counting-sort ordering with E candidate slots per thread (E x NT >= n):
+// the candidates binned by their last releasing position l < Fr, ranked in
+// their bin by U index.  Returns false when a bin is too large for the
+// in-bin scan (the caller's bitonic fallback orders them).  Templated on E so
+// that the common fronts of a few thousand candidates do not carry the
+// registers (and scratch spills) of the 16-slot form.
+template <int NT, int E, int CAP, bool COH>
+__device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* out, int2* mout,
+                            int4* tout, const int32_t* nseg, const MemberTab& mt,
+                            const CandMap& cm, int32_t n, int32_t Fr, OrderLds<CAP>& lds,
+                            int32_t* part, OrderScalars& sc) {
+    const int tid = threadIdx.x;
+    bool sorted_here = false;
+    for (int i = tid; i <= Fr; i += NT) lds.cs.base[i] = 0;
+    __syncthreads();
+    uint64_t key[E];
+    int32_t qv[E], slot[E];
+    // the first PF candidates' records (slot order, beside the keys) are
+    // fetched here, in flight across the binning's barriers (they wait
+    // on LDS only)
+    constexpr int PF = E < 4 ? E : 4;
+    int4 rec[PF];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        if (i < n) {
+            const int64_t sl = cm.slot(i);
+            key[e] = cld<COH>(ckey + sl);
+            qv[e] = cld<COH>(cq + sl);
+            if (e < PF && tout) rec[e] = mt.crec[sl];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        if (i < n) slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
+    }
+    __syncthreads();
+    // exclusive prefix of the bin counts: thread t owns C consecutive bins
+    const int C = (Fr + NT - 1) / NT;
+    const int b0 = tid * C, b1 = min(Fr, b0 + C);
+    int32_t sum = 0, mx = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = lds.cs.base[b];
+        sum += c;
+        mx = max(mx, c);
+    }
+    if (mx > ORDER_BIN_MAX) atomicMax(&sc.smax, mx);
+    int32_t run = block_excl_scan<NT>(sum, part);
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = lds.cs.base[b];
+        lds.cs.base[b] = run;
+        run += c;
+    }
+    if (tid == 0) lds.cs.base[Fr] = n;
+    __syncthreads();
+    if (sc.smax == 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = tid + e * NT;
+            if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
+        }
+        __syncthreads();
+        // ranks first, then the record copies as one batch of loads
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = tid + e * NT;
+            if (i < n) {
+                const int32_t l = (int32_t)(key[e] >> 32), vu = (int32_t)(uint32_t)key[e];
+                const int32_t beg = lds.cs.base[l], end = lds.cs.base[l + 1];
+                int32_t r = beg;
+                for (int32_t j = beg; j < end; ++j) r += lds.cs.tmp[j] < vu ? 1 : 0;
+                cst<COH>(out + r, vu);
+                slot[e] = r;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = tid + e * NT;
+            if (i < n) {
+                if (tout)
+                    tout[slot[e]] = e < PF ? rec[e] : mt.crec[cm.slot(i)];
+                else
+                    cst2<COH>(mout + slot[e], make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
+            }
+        }
+        sorted_here = true;
+    }
+    __syncthreads();  // the bitonic fallback reuses the LDS
+    return sorted_here;
+}
+
 template <int NT, int CAP, bool COH>
 __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t* cq,
                             int32_t* ulist, int2* mrow, const int32_t* pos, const int32_t* nseg,
@@ -1155,7 +1299,19 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     if (tid == 0) {
         const int32_t done = cld<COH>(&st->done), ovf = cld<COH>(&st->overflow);
         sc.sgo = !(done || (ovf && !presorted));
-        sc.sn = cld<COH>(&st->ncand);
+        // the candidate list: the eight slot buckets in order, or (presorted,
+        // after the host's compaction and radix sort) ckey[0, ncand)
+        int32_t run = 0;
+        int64_t pend = 0;
+        for (int b = 0; b < CAND_BUCKETS; ++b) {
+            sc.cm.pre[b] = run;
+            run += cld<COH>(cand_count(st, b));
+            pend += (int64_t)cld<COH>(cand_pending(st, b));
+        }
+        sc.cm.pre[CAND_BUCKETS] = run;
+        sc.cm.cap = presorted ? 0 : cand_cap(st->U);
+        sc.sn = presorted ? cld<COH>(&st->ncand) : run;
+        sc.spending = pend;
         sc.snstart = cld<COH>(&st->ustart) + cld<COH>(&st->F);
         sc.sF = cld<COH>(&st->F);
         sc.smax = 0;
@@ -1163,13 +1319,17 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     __syncthreads();
     if (!sc.sgo) return;
     const int32_t n = sc.sn;
+    const CandMap cm = sc.cm.uniform();
     if (!BD_OK(sc.snstart + (int64_t)n - 1, st->U, "order front end")) return;
     if (n == 0) {  // nothing released: the reference's `if F2 == 0: break`
         if (tid == 0) cst<COH>(&st->done, 1);
         return;
     }
     if (!presorted && n > CAP) {
-        if (tid == 0) cst<COH>(&st->overflow, 1);
+        if (tid == 0) {
+            cst<COH>(&st->ncand, n);  // the host compacts the buckets and sorts them
+            cst<COH>(&st->overflow, 1);
+        }
         return;
     }
     int32_t* out = ulist + sc.snstart;
@@ -1188,113 +1348,47 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
         }
         sorted_here = true;
     } else if (sc.sF <= CAP) {
-        constexpr int E = CAP / NT;
-        const int32_t Fr = sc.sF;
-        for (int i = tid; i <= Fr; i += NT) lds.cs.base[i] = 0;
-        __syncthreads();
-        uint64_t key[E];
-        int32_t qv[E], slot[E];
-        // the first PF candidates' records (slot order, beside the keys) are
-        // fetched here, in flight across the binning's barriers (they wait
-        // on LDS only)
-        constexpr int PF = E < 4 ? E : 4;
-        int4 rec[PF];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int i = tid + e * NT;
-            if (i < n) {
-                key[e] = cld<COH>(ckey + i);
-                qv[e] = cld<COH>(cq + i);
-                if (e < PF && tout) rec[e] = mt.crec[i];
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int i = tid + e * NT;
-            if (i < n) slot[e] = atomicAdd(&lds.cs.base[(int32_t)(key[e] >> 32)], 1);
-        }
-        __syncthreads();
-        // exclusive prefix of the bin counts: thread t owns C consecutive bins
-        const int C = (Fr + NT - 1) / NT;
-        const int b0 = tid * C, b1 = min(Fr, b0 + C);
-        int32_t sum = 0, mx = 0;
-        for (int b = b0; b < b1; ++b) {
-            const int32_t c = lds.cs.base[b];
-            sum += c;
-            mx = max(mx, c);
-        }
-        if (mx > ORDER_BIN_MAX) atomicMax(&sc.smax, mx);
-        int32_t run = block_excl_scan<NT>(sum, part);
-        for (int b = b0; b < b1; ++b) {
-            const int32_t c = lds.cs.base[b];
-            lds.cs.base[b] = run;
-            run += c;
-        }
-        if (tid == 0) lds.cs.base[Fr] = n;
-        __syncthreads();
-        if (sc.smax == 0) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int i = tid + e * NT;
-                if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
-            }
-            __syncthreads();
-            // ranks first, then the record copies as one batch of loads
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int i = tid + e * NT;
-                if (i < n) {
-                    const int32_t l = (int32_t)(key[e] >> 32), vu = (int32_t)(uint32_t)key[e];
-                    const int32_t beg = lds.cs.base[l], end = lds.cs.base[l + 1];
-                    int32_t r = beg;
-                    for (int32_t j = beg; j < end; ++j) r += lds.cs.tmp[j] < vu ? 1 : 0;
-                    cst<COH>(out + r, vu);
-                    slot[e] = r;
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int i = tid + e * NT;
-                if (i < n) {
-                    if (tout)
-                        tout[slot[e]] = e < PF ? rec[e] : mt.crec[i];
-                    else
-                        cst2<COH>(mout + slot[e], make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
-                }
-            }
-            sorted_here = true;
-        }
-        __syncthreads();  // the bitonic fallback reuses the LDS
+        // slots per thread for this front: 4 covers the C5 fronts (< 4,096)
+        if (n <= 4 * NT)
+            sorted_here = order_count<NT, 4, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt, cm, n,
+                                                       sc.sF, lds, part, sc);
+        else if (n <= 8 * NT)
+            sorted_here = order_count<NT, 8, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt, cm, n,
+                                                       sc.sF, lds, part, sc);
+        else
+            sorted_here = order_count<NT, CAP / NT, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt,
+                                                              cm, n, sc.sF, lds, part, sc);
     }
     if (!sorted_here) {
         uint64_t* keys = lds.keys;
         if (n <= NT) {
-            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
+            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
         } else if (n <= 2 * NT) {
-            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
+            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
         } else if (n <= 4 * NT) {
-            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
+            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
         } else if (n <= 8 * NT) {
-            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
+            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
         } else {
             static_assert(CAP <= 16 * NT, "order capacity exceeds the bitonic sizes");
-            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout);
+            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
         }
     }
     if (tid == 0) {
         const int32_t nstart = sc.snstart, r = cld<COH>(&st->nfronts);
-        const int64_t pending = (int64_t)__hip_atomic_load(
-            reinterpret_cast<unsigned long long*>(&st->pending), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t pending = sc.spending;
         const int64_t sorted = cld<COH>(&st->sorted) + pending;
         cst<COH>(&st->sorted, sorted);
         cst<COH>(&st->lastinds, pending);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&st->pending), 0ull,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
         cst<COH>(&st->ustart, nstart);
         cst<COH>(&st->F, n);
         cst<COH>(&st->nfronts, r + 1);
         __hip_atomic_store(&st->ncand, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int b = 0; b < CAND_BUCKETS; ++b) {  // empty buckets for the next peel
+            __hip_atomic_store(cand_count(st, b), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cand_pending(st, b), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         cst<COH>(&st->overflow, 0);
         cst<COH>(fstarts + r + 2, nstart + n);
         // emo.py:109: continue while pareto_sorted < N (and fronts remain)
@@ -1312,6 +1406,19 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
     __shared__ OrderScalars sc;
     order_front<1024, ORDER_CAP, false>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, presorted,
                                         lds, part, sc, mt);
+}
+
+// The overflow path's compaction: bucket blockIdx.y's candidates to
+// out[pre_b + j] (pre_b: the earlier buckets' counts).
+__global__ void cand_compact_kernel(FrontState* st, const uint64_t* ckey, int64_t cap,
+                                    uint64_t* out) {
+    const int b = blockIdx.y;
+    int32_t pre = 0;
+    for (int k = 0; k < b; ++k) pre += *cand_count(st, k);
+    const int32_t cnt = *cand_count(st, b);
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < cnt;
+         j += (int64_t)gridDim.x * blockDim.x)
+        out[pre + j] = ckey[b * cap + j];
 }
 
 __global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, const int32_t* pos,
@@ -1363,7 +1470,8 @@ static size_t ranks_work_bytes(int64_t n, int64_t U) {
            scan_temp_bytes(e);
 }
 static size_t fronts_work_bytes(int64_t U) {
-    return align_up(sizeof(FrontState), 256) + 3 * align_up((size_t)U * 8, 256) +
+    return CAND_PAGE * (CAND_BUCKETS + 1) +
+           align_up((size_t)CAND_BUCKETS * cand_cap(U) * 8, 256) + 2 * align_up((size_t)U * 8, 256) +
            2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
 }
 static FastLayout fast_layout(int64_t n, int64_t U) {
@@ -1390,9 +1498,9 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
     L.mrow = take((size_t)U * 8);
     L.mtab = take((size_t)U * 16);
     L.qrec = take((size_t)U * 16);
-    L.crec = take((size_t)U * 16);
+    L.crec = take((size_t)CAND_BUCKETS * cand_cap(U) * 16);
     L.countq = take((size_t)U * 4);
-    L.cq = take((size_t)U * 4);
+    L.cq = take((size_t)CAND_BUCKETS * cand_cap(U) * 4);
     L.work = take(std::max(ranks_work_bytes(n, U), fronts_work_bytes(U)));
     L.total = off;
     return L;
@@ -1534,10 +1642,10 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     int32_t* countq = (int32_t*)(ws + L.countq);
     int32_t* cq = (int32_t*)(ws + L.cq);
     char* p = ws + L.work;
-    FrontState* st = (FrontState*)p;
-    p += align_up(sizeof(FrontState), 256);
+    FrontState* st = (FrontState*)p;  // + the eight candidate-bucket pages
+    p += CAND_PAGE * (CAND_BUCKETS + 1);
     uint64_t* ckey = (uint64_t*)p;
-    p += align_up((size_t)U * 8, 256);
+    p += align_up((size_t)CAND_BUCKETS * cand_cap(U) * 8, 256);
     uint64_t* ktmp = (uint64_t*)p;
     p += align_up((size_t)U * 8, 256);
     int32_t* vals = (int32_t*)p;
@@ -1549,6 +1657,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     p += align_up((size_t)U * 8, 256);
     void* rtemp = p;
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
+    DM_HIP(hipMemsetAsync(st, 0, CAND_PAGE * (CAND_BUCKETS + 1), s));
     front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     // table-fed peel: the bitset pass's tables in the part region
     const bool tab = fast_table_peel(ctx, m);
@@ -1611,9 +1720,14 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
         if (hst->overflow) {
             // a front too large for the LDS sort: the radix sort orders its keys
             const int32_t nc = hst->ncand;
+            // the buckets' candidates gathered into one list (ktmp), sorted,
+            // and back into ckey[0, nc) for the presorted ordering
+            cand_compact_kernel<<<dim3((unsigned)((cand_cap(U) + 255) / 256), CAND_BUCKETS), 256, 0,
+                                  s>>>(st, ckey, cand_cap(U), ktmp);
             DM_HIP(hipMemsetAsync(vals, 0, (size_t)nc * 4, s));
-            int rc = radix_sort_pairs(s, ckey, vals, ktmp, vtmp, nc, 0, 64, rtemp);
+            int rc = radix_sort_pairs(s, ktmp, vals, ckey, vtmp, nc, 0, 64, rtemp);
             if (rc) return rc;
+            DM_HIP(hipMemcpyAsync(ckey, ktmp, (size_t)nc * 8, hipMemcpyDeviceToDevice, s));
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1, mt);
             DM_LAUNCH_CHECK();
         }

@@ -11,10 +11,32 @@ from deap_amd import tools, _lib
 from deap_amd.device import DevicePopulation
 m = 3
 n = 1 << 18
-rng = np.random.default_rng(103)
-d = np.abs(rng.normal(size=(n, m)))
-d /= np.linalg.norm(d, axis=1, keepdims=True)
-wv = -(d * (1.0 + rng.exponential(0.3, size=(n, 1))))
+if len(sys.argv) > 1 and sys.argv[1] == "c5":
+    # the C5 bench's own selection input: 2^17 DTLZ2 individuals after a few
+    # eaMuPlusLambda generations plus one varOr batch (bench.py bench_nsga2)
+    from deap_amd import algorithms, base, benchmarks
+    from deap_amd.ops import RandomStream
+    half = n // 2
+    stream = RandomStream(1234)
+    p0 = tools.initPopulation(n=half, dim=12, low=0.0, high=1.0, gtype="f64",
+                              weights=(-1.0,) * m, stream=stream)
+    tb = base.Toolbox()
+    tb.register("evaluate", benchmarks.dtlz2, obj=m)
+    tb.register("mate", tools.cxBlend, alpha=0.5)
+    tb.register("mutate", tools.mutGaussian, mu=0, sigma=0.1, indpb=1.0 / 12)
+    tb.register("select", tools.selNSGA2)
+    benchmarks.dtlz2(p0, obj=m)
+    step = algorithms.MuPlusLambdaStep(p0, tb, half, half, 0.6, 0.3)
+    for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 12):
+        step.step(stream)
+    comb = step.combined
+    off = algorithms.varOr(comb, tb, half, 0.6, 0.3, evaluate=True, stream=stream)
+    wv = np.concatenate([comb.wvalues[:half].cpu().numpy(), off.wvalues[:half].cpu().numpy()])
+else:
+    rng = np.random.default_rng(103)
+    d = np.abs(rng.normal(size=(n, m)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    wv = -(d * (1.0 + rng.exponential(0.3, size=(n, 1))))
 pop = DevicePopulation.from_numpy(np.zeros((n, 1)), weights=(-1.0,) * m, gtype="f64", wvalues=wv,
                                   valid=np.ones(n))
 lib = ctypes.CDLL(_lib.LIB_PATH)
