@@ -76,6 +76,7 @@ struct dm_ctx {
     size_t pinned_bytes = 0;
     int num_cus = 256;
     int peel_hint = 4;  // fronts the last fast sortNondominated peeled (first status batch)
+    int peel_trend = 0;  // ... and how many more than the call before it
     int64_t peel_hint_U = 0, peel_hint_N = 0;  // ... its unique fitnesses and its k
     double* zig = nullptr;  // ziggurat tables (device), see zig_normal
     // nevals counters (kEvalSpreadWords, zero between launches; see

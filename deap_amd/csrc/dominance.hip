@@ -1688,7 +1688,10 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     const bool hinted = 4 * U >= 3 * ctx->peel_hint_U && 3 * U <= 4 * ctx->peel_hint_U &&
                         N == ctx->peel_hint_N;
     const int hint = hinted ? ctx->peel_hint : 4;
-    int batch = std::max(2, std::min(hint + 1, PEEL_BATCH_MAX));
+    // while a run's front count still grows (its first generations: a few
+    // more fronts per call) the first batch adds the last change
+    const int trend = hinted ? std::max(0, std::min(ctx->peel_trend, 4)) : 0;
+    int batch = std::max(2, std::min(hint + 1 + trend, PEEL_BATCH_MAX));
     for (;;) {
         for (int b = 0; b < batch; ++b) {
             if (tab) {
@@ -1732,19 +1735,22 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
             DM_LAUNCH_CHECK();
         }
         // next batch from what is left: fronts grow along the peel, so the
-        // remaining individuals / the mean front size so far bounds the fronts
-        // still needed (each launch past `done` returns at once but costs
-        // ~10 us; each extra status check a round trip)
+        // remaining individuals over the last front's (or the mean front's,
+        // if larger) bound the fronts still needed (each launch past `done`
+        // returns at once but costs ~10 us; each extra status check a round
+        // trip; the bench's growing generations left 4-12 launch pairs idle
+        // per selection with the mean alone and two spare pairs)
         const double mean = (double)hst->sorted / (double)(hst->nfronts + 1);
+        const double per = std::max(mean, (double)hst->lastinds);
         const double left = (double)(hst->N - hst->sorted);
-        int need = mean > 0 ? (int)std::ceil(left / mean) : 32;
+        int need = per > 0 ? (int)std::ceil(left / per) : 32;
         // the previous call's front count, when it had more fronts than done
-        // so far, is the better estimate (later fronts are larger than the
-        // mean so far); launches past `done` return at once but cost ~10 us
+        // so far, is the better estimate
         if (hint > hst->nfronts) need = std::min(need, hint - hst->nfronts + 1);
-        batch = std::max(2, std::min(need + 2, PEEL_BATCH_MAX));
+        batch = std::max(2, std::min(need + 1, PEEL_BATCH_MAX));
     }
     const int32_t nf = hst->nfronts + 1;  // front 0 plus the peeled ones
+    ctx->peel_trend = hinted ? hst->nfronts - ctx->peel_hint : 0;
     ctx->peel_hint = hst->nfronts;
     ctx->peel_hint_U = U;
     ctx->peel_hint_N = N;

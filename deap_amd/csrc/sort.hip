@@ -213,7 +213,8 @@ int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t*
 }
 
 // ---------------------------------------------------------------------------
-// Scans: block-local scan -> scan of block sums -> add back.
+// Scans: reduce-then-scan up to 4 Mi elements; beyond, block-local scan ->
+// scan of block sums -> add back.
 // ---------------------------------------------------------------------------
 constexpr int SC_THREADS = 256;
 constexpr int SC_ITEMS = 8;
@@ -276,44 +277,112 @@ __global__ void scan_total_kernel(const int32_t* in, const int32_t* ex, int64_t 
     *total = n > 0 ? ex[n - 1] + in[n - 1] : 0;
 }
 
+// Reduce-then-scan for up to SC_TILE tiles (n <= 4 Mi): block b's aggregate
+// (scan_reduce_kernel), then every block combines the aggregates before it
+// -- at most SC_TILE ints, from the L2 -- and scans its tile from that
+// prefix (scan_down_kernel).  Two launches and no look-back, where the
+// tile / block-sum / add-back form took three (four with the total).
+template <bool MAX>
+__device__ __forceinline__ int32_t sc_block_reduce(int32_t v, int32_t* sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op2<MAX>(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int32_t r = sh[0];
+#pragma unroll
+    for (int w = 1; w < SC_THREADS / 64; ++w) r = op2<MAX>(r, sh[w]);
+    return r;
+}
+template <bool MAX>
+__global__ __launch_bounds__(SC_THREADS) void scan_reduce_kernel(const int32_t* in, int64_t n,
+                                                                 int32_t* sums) {
+    __shared__ int32_t sh[SC_THREADS / 64];
+    const int64_t base = (int64_t)blockIdx.x * SC_TILE + (int64_t)threadIdx.x * SC_ITEMS;
+    int32_t acc = MAX ? INT32_MIN : 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j)
+        if (base + j < n) acc = op2<MAX>(acc, in[base + j]);
+    acc = sc_block_reduce<MAX>(acc, sh);
+    if (threadIdx.x == 0) sums[blockIdx.x] = acc;
+}
+// total (may be null): the whole input's aggregate, from the last block
 template <bool MAX, bool INCL>
-static int scan_impl(hipStream_t s, const int32_t* in, int32_t* out, int64_t n, void* temp) {
-    if (n <= 0) return DM_OK;
+__global__ __launch_bounds__(SC_THREADS) void scan_down_kernel(const int32_t* in, int32_t* out,
+                                                               int64_t n, const int32_t* sums,
+                                                               int32_t* total) {
+    __shared__ int32_t sh[SC_THREADS];
+    __shared__ int32_t shr[SC_THREADS / 64];
+    const int32_t ident = MAX ? INT32_MIN : 0;
+    const int64_t base = (int64_t)blockIdx.x * SC_TILE + (int64_t)threadIdx.x * SC_ITEMS;
+    int32_t v[SC_ITEMS];
+    int32_t acc = ident;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j;
+        v[j] = i < n ? in[i] : ident;
+        acc = op2<MAX>(acc, v[j]);
+    }
+    int32_t p = ident;
+    for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += SC_THREADS) p = op2<MAX>(p, sums[b]);
+    p = sc_block_reduce<MAX>(p, shr);
+    const int32_t incl = block_incl_scan<SC_THREADS, MAX>(acc, sh);
+    int32_t run = __shfl_up(incl, 1, 64);
+    if ((threadIdx.x & 63) == 0) run = threadIdx.x > 0 ? sh[(threadIdx.x >> 6) - 1] : ident;
+    run = op2<MAX>(p, run);
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const int64_t i = base + j;
+        const int32_t nxt = op2<MAX>(run, v[j]);
+        if (i < n) out[i] = INCL ? nxt : run;
+        run = nxt;
+    }
+    if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SC_THREADS - 1) *total = run;
+}
+
+// total (may be null): the aggregate of the whole input, on the device
+template <bool MAX, bool INCL>
+static int scan_impl(hipStream_t s, const int32_t* in, int32_t* out, int64_t n, void* temp,
+                     int32_t* total) {
+    if (n <= 0) {
+        if (total) DM_HIP(hipMemsetAsync(total, 0, 4, s));
+        return DM_OK;
+    }
     const int64_t blocks = (n + SC_TILE - 1) / SC_TILE;
     if (blocks == 1) {
-        scan_tile_kernel<MAX, INCL><<<1, SC_THREADS, 0, s>>>(in, out, n, nullptr);
+        scan_tile_kernel<MAX, INCL><<<1, SC_THREADS, 0, s>>>(in, out, n, total);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
     int32_t* sums = (int32_t*)temp;
+    if (blocks <= SC_TILE) {
+        scan_reduce_kernel<MAX><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, n, sums);
+        scan_down_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums, total);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
     int32_t* pref = (int32_t*)((char*)temp + align_up((size_t)blocks * 8, 256));
     void* next = (char*)temp + 2 * align_up((size_t)blocks * 8, 256);
     scan_tile_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums);
     // exclusive scan of block aggregates
-    int rc = scan_impl<MAX, false>(s, sums, pref, blocks, next);
+    int rc = scan_impl<MAX, false>(s, sums, pref, blocks, next, nullptr);
     if (rc) return rc;
     scan_add_kernel<MAX><<<(unsigned)blocks, SC_THREADS, 0, s>>>(out, n, pref);
+    if (total) {
+        if (MAX) return DM_ERR_INVALID;  // no caller asks for the total of a max scan
+        scan_total_kernel<<<1, 1, 0, s>>>(in, out, n, total);
+    }
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
 
 int exclusive_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
                        int32_t* total, void* temp) {
-    int rc = scan_impl<false, false>(s, in, out, n, temp);
-    if (rc) return rc;
-    if (total) {
-        if (n > 0)
-            scan_total_kernel<<<1, 1, 0, s>>>(in, out, n, total);
-        else
-            DM_HIP(hipMemsetAsync(total, 0, 4, s));
-    }
-    DM_LAUNCH_CHECK();
-    return DM_OK;
+    return scan_impl<false, false>(s, in, out, n, temp, total);
 }
 
 int inclusive_max_scan_i32(hipStream_t s, const int32_t* in, int32_t* out, int64_t n,
                            void* temp) {
-    return scan_impl<true, true>(s, in, out, n, temp);
+    return scan_impl<true, true>(s, in, out, n, temp, nullptr);
 }
 
 // ---------------------------------------------------------------------------
