@@ -301,22 +301,26 @@ __global__ void sel_tournament_kernel(const double* wv, int nobj, int64_t n, int
     }
 }
 
-template <int VEC>
+// Rows copied in 16-B pieces by lpr lanes each (a power of two up to 64):
+// 64 / lpr rows per wave.  One wave per row left most lanes idle on short
+// rows (C5's 96-B genomes used 6 of 64, and its chosen-row gather ran ~8
+// dependent row copies per wave in sequence).
 __global__ void gather_kernel(const char* sg, const double* swv, const uint8_t* sv, int64_t sstride,
                               char* dg, double* dwv, uint8_t* dv, int64_t dstride,
-                              const int32_t* idx, int64_t k, int64_t row_bytes, int nobj) {
-    // one wave per row; rows copied in 16-B pieces
+                              const int32_t* idx, int64_t k, int64_t row_bytes, int nobj, int lpr) {
     const int lane = threadIdx.x & 63;
+    const int sub = lane & (lpr - 1);
+    const int64_t rpw = 64 / lpr;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t q = row_bytes / 16;
-    for (int64_t r = wave; r < k; r += nw) {
+    for (int64_t r = wave * rpw + lane / lpr; r < k; r += nw * rpw) {
         const int64_t s = idx ? idx[r] : r;
         const uint4* src = reinterpret_cast<const uint4*>(sg + s * sstride);
         uint4* dst = reinterpret_cast<uint4*>(dg + r * dstride);
-        for (int64_t i = lane; i < q; i += 64) dst[i] = src[i];
-        if (lane < nobj) dwv[r * nobj + lane] = swv[s * nobj + lane];
-        if (lane == 0) dv[r] = sv[s];
+        for (int64_t i = sub; i < q; i += lpr) dst[i] = src[i];
+        for (int o = sub; o < nobj; o += lpr) dwv[r * nobj + o] = swv[s * nobj + o];
+        if (sub == 0) dv[r] = sv[s];
     }
 }
 
@@ -712,9 +716,12 @@ int dm_gather(dm_ctx* ctx, const dm_pop* src, const int32_t* idx, dm_pop* dst) {
     if (!idx) DM_CHECK_ARG(dst->n <= src->n, "identity gather needs dst.n <= src.n");
     if (dst->n == 0) return DM_OK;
     const int64_t row_bytes = std::min(src->stride, dst->stride);
-    gather_kernel<16><<<grid_for(ctx, dst->n, 4), 256, 0, ctx->stream>>>(
+    int lpr = 1;  // lanes per row: the row's 16-B pieces, rounded up to a power of two
+    while (lpr < 64 && lpr * 16 < row_bytes) lpr *= 2;
+    const int64_t rows_per_block = 4 * (64 / lpr);
+    gather_kernel<<<grid_for(ctx, dst->n, (int)rows_per_block), 256, 0, ctx->stream>>>(
         (const char*)src->genes, src->wvalues, src->valid, src->stride, (char*)dst->genes,
-        dst->wvalues, dst->valid, dst->stride, idx, dst->n, row_bytes, src->nobj);
+        dst->wvalues, dst->valid, dst->stride, idx, dst->n, row_bytes, src->nobj, lpr);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

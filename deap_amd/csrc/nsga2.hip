@@ -67,18 +67,22 @@ static dim3 g1(int64_t n) {
 // ---------------------------------------------------------------------------
 // 1. grouping of equal fitnesses
 // ---------------------------------------------------------------------------
+// isrep is written for every row (perm is a permutation: no zeroing pass);
+// *nanflag (zeroed by the caller) is set when any objective value is NaN
 __global__ void seg_flag_kernel(const double* wv, int m, const int32_t* perm, int64_t n,
-                                int32_t* segstart_in, int32_t* isrep) {
+                                int32_t* segstart_in, int32_t* isrep, int32_t* nanflag) {
     GRID_LOOP(j, n) {
-        bool start = j == 0;
+        const double* a = wv + (int64_t)perm[j] * m;
+        bool start = j == 0, nan = false;
+        for (int o = 0; o < m; ++o) nan |= a[o] != a[o];
         if (!start) {
-            const double* a = wv + (int64_t)perm[j] * m;
             const double* b = wv + (int64_t)perm[j - 1] * m;
             for (int o = 0; o < m; ++o)
                 if (!(a[o] == b[o])) start = true;
         }
         segstart_in[j] = start ? (int32_t)j : 0;
-        if (start) isrep[perm[j]] = 1;
+        isrep[perm[j]] = start ? 1 : 0;
+        if (nan) *nanflag = 1;
     }
 }
 // After a stable sort by objective 0 alone (keys0: the sorted objective-0
@@ -173,14 +177,19 @@ __global__ __launch_bounds__(256) void lex_run_sort_kernel(const double* wv, int
         if (in) perm[i] = r.x;
     }
 }
-__global__ void nan_any_kernel(const double* wv, int64_t cnt, int32_t* flag) {
-    GRID_LOOP(i, cnt) if (wv[i] != wv[i]) *flag = 1;
-}
 __global__ void zero_i32_kernel(int32_t* p, int64_t n) {
     GRID_LOOP(i, n) p[i] = 0;
 }
 __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
     GRID_LOOP(i, n) p[i] = v;
+}
+// the per-unique-fit arrays of a sort: group sizes and counts 0, ranks -1
+__global__ void unique_init_kernel(int32_t* gsize, int32_t* count, int32_t* rankU, int64_t U) {
+    GRID_LOOP(i, U) {
+        gsize[i] = 0;
+        count[i] = 0;
+        rankU[i] = -1;
+    }
 }
 // ui[i] = unique index of individual i; ufit / useg / gsize per unique fit.
 __global__ void unique_kernel(const double* wv, int m, const int32_t* perm, const int32_t* segstart,
@@ -585,7 +594,8 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     const bool q32 = quick && m <= 3 && !ctx->knobs.lex_no32;
     int rc;
     auto group = [&](int nlex, int kshift) -> int {
-        DM_HIP(hipMemsetAsync(tieflag, 0, 4, s));
+        // the scalars: unique count, NaN flag, front-0 size, tie flag
+        DM_HIP(hipMemsetAsync(small, 0, 32, s));
         int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex, kshift);
         if (r) return r;
         if (nlex < m) {
@@ -594,14 +604,11 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
             lex_run_sort_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, s>>>(
                 wv, m, keys, perm, n, vtmp, tieflag, kshift);
         }
-        zero_i32_kernel<<<g1(n), 256, 0, s>>>(isrep, n);
-        seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep);
+        seg_flag_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, n, segin, isrep, nanflag);
         if ((r = inclusive_max_scan_i32(s, segin, segstart, n, stemp))) return r;
         return exclusive_scan_i32(s, isrep, uidx, n, utotal, stemp);
     };
     if ((rc = group(quick ? 1 : m, q32 ? 32 : 0))) return rc;
-    DM_HIP(hipMemsetAsync(nanflag, 0, 4, s));
-    nan_any_kernel<<<g1(n * m), 256, 0, s>>>(wv, n * m, nanflag);
     DM_HIP(hipMemcpyAsync(hostv, utotal, 28, hipMemcpyDeviceToHost, s));
     DM_HIP(hipStreamSynchronize(s));
     // a run longer than LEX_RUN_CAP: the whole-key objective-0 sort, then the
@@ -662,9 +669,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         if (!fwork) return DM_ERR_NOMEM;
     }
 
-    zero_i32_kernel<<<g1(U), 256, 0, s>>>(gsize, U);
-    zero_i32_kernel<<<g1(U), 256, 0, s>>>(count, U);
-    fill_i32_kernel<<<g1(U), 256, 0, s>>>(rankU, U, -1);
+    unique_init_kernel<<<g1(U), 256, 0, s>>>(gsize, count, rankU, U);
     unique_kernel<<<g1(n), 256, 0, s>>>(wv, m, perm, segstart, uidx, n, ui, ufit, useg, gsize);
     if (fast) {
         if ((rc = fast_dom_build(ctx, wv, m, n, perm, segin, uidx, ufit, U, D, count,
@@ -791,17 +796,6 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
 // ---------------------------------------------------------------------------
 // crowding distance
 // ---------------------------------------------------------------------------
-__global__ void front_id_kernel(const int32_t* fstart, int32_t nf, int64_t T, int32_t* fid) {
-    GRID_LOOP(j, T) {
-        int lo = 0, hi = nf - 1;  // last f with fstart[f] <= j
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (fstart[mid] <= j) lo = mid;
-            else hi = mid - 1;
-        }
-        fid[j] = lo;
-    }
-}
 struct Weights {
     double w[DM_MAX_OBJ];
 };
@@ -815,11 +809,20 @@ __global__ void crowd_key_kernel(const double* wv, int m, int obj, Weights wt, c
 __global__ void fid_key_kernel(const int32_t* fid, const int32_t* pos, uint64_t* keys, int64_t T) {
     GRID_LOOP(j, T) keys[j] = (uint64_t)(uint32_t)fid[pos[j]];
 }
-__global__ void iota32_kernel(int32_t* v, int64_t n) {
-    GRID_LOOP(i, n) v[i] = (int32_t)i;
-}
-__global__ void crowd_init_kernel(const int32_t* order, int64_t T, double* crowd) {
-    GRID_LOOP(j, T) crowd[order[j]] = 0.0;
+// front ids, crowding zeroed and the identity order in one pass
+__global__ void crowd_setup_kernel(const int32_t* fstart, int32_t nf, const int32_t* order,
+                                   int64_t T, int32_t* fid, double* crowd, int32_t* pos) {
+    GRID_LOOP(j, T) {
+        int lo = 0, hi = nf - 1;  // last f with fstart[f] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (fstart[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        fid[j] = lo;
+        crowd[order[j]] = 0.0;
+        pos[j] = (int32_t)j;
+    }
 }
 __global__ void crowd_update_kernel(const double* wv, int m, int obj, Weights wt,
                                     const int32_t* order, const int32_t* spos,
@@ -877,8 +880,7 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
     int32_t* fid = bp.take<int32_t>(T);
     int32_t* fpos = bp.take<int32_t>(T);
     void* rtemp = bp.take<char>(radix_sort_temp_bytes(T));
-    front_id_kernel<<<g1(T), 256, 0, s>>>(fstart_dev, nfronts, T, fid);
-    crowd_init_kernel<<<g1(T), 256, 0, s>>>(order, T, crowd);
+    crowd_setup_kernel<<<g1(T), 256, 0, s>>>(fstart_dev, nfronts, order, T, fid, crowd, pos);
     int fbits = 8;
     while (fbits < 32 && (1ll << fbits) <= nfronts) fbits += 8;
     // The reference sorts one `crowd` list by objective 0, then 1, ...
@@ -886,7 +888,6 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
     // one stably sorted by v_i, i.e. lexicographic in (v_i, ..., v_0,
     // position) — one 64-bit sort per objective carried over; the grouping
     // by front (a stable sort by front id) works on a copy.
-    iota32_kernel<<<g1(T), 256, 0, s>>>(pos, T);
     bool zero_w = false;
     for (int o = 0; o < m; ++o) zero_w = zero_w || weights[o] == 0.0;
     if (rk && !zero_w) {
