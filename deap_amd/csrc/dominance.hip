@@ -1114,10 +1114,11 @@ struct MemberTab {
     const int4* crec;   // the candidates' records in slot order (peel_release)
 };
 __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t* nseg, int64_t U,
-                                  int4* qrec) {
+                                  int4* qrec, unsigned long long* lastq) {
     DGRID_LOOP(q, U) {
         const int4 s = S[q];
         qrec[q] = make_int4(nseg[q / (64 * TD_WPW)], span[q].y, s.x, s.y);
+        lastq[q] = 0;  // the sliced peels' (front, last position) per v
     }
 }
 
@@ -1432,8 +1433,15 @@ __global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, cons
     }
 }
 
+// one workgroup per 4-KB page of the state and its candidate buckets: the
+// pages zeroed, then (workgroup 0) the state of front 0
 __global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int64_t* sorted0p,
                                   int64_t N, int64_t U, int32_t* fstarts) {
+    uint4* page = reinterpret_cast<uint4*>(reinterpret_cast<char*>(st) + CAND_PAGE * blockIdx.x);
+    for (int i = threadIdx.x; i < (int)(CAND_PAGE / 16); i += blockDim.x) page[i] = make_uint4(0, 0, 0, 0);
+    if (blockIdx.x != 0) return;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     const int32_t F0 = *F0p;
     const int64_t sorted0 = *sorted0p;
     st->F = F0;
@@ -1656,9 +1664,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     unsigned long long* lastq = (unsigned long long*)p;
     p += align_up((size_t)U * 8, 256);
     void* rtemp = p;
-    DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
-    DM_HIP(hipMemsetAsync(st, 0, CAND_PAGE * (CAND_BUCKETS + 1), s));
-    front_init_kernel<<<1, 1, 0, s>>>(st, F0, sorted0, N, U, fstarts);
+    front_init_kernel<<<CAND_BUCKETS + 1, 256, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     // table-fed peel: the bitset pass's tables in the part region
     const bool tab = fast_table_peel(ctx, m);
     const BitdomLayout TL = bitdom_layout(U, m);
@@ -1668,7 +1674,9 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     int4* crec = (int4*)(ws + L.crec);
     if (tab)
         member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
-                                                 nseg, U, qrec);
+                                                 nseg, U, qrec, lastq);
+    else
+        DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     const MemberTab mt{tab ? mtab : nullptr, qrec, crec};
     const CandRec cr{qrec, crec};
     member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow, mt);

@@ -594,8 +594,8 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     const bool q32 = quick && m <= 3 && !ctx->knobs.lex_no32;
     int rc;
     auto group = [&](int nlex, int kshift) -> int {
-        // the scalars: unique count, NaN flag, front-0 size, tie flag
-        DM_HIP(hipMemsetAsync(small, 0, 32, s));
+        // the scalars: unique count, NaN flag, front-0 size, tie flag, front-0 individuals
+        DM_HIP(hipMemsetAsync(small, 0, 48, s));
         int r = lex_sort_rows(s, wv, m, n, false, keys, ktmp, perm, vtmp, rtemp, nlex, kshift);
         if (r) return r;
         if (nlex < m) {
@@ -696,7 +696,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     flag_zero_count_kernel<<<g1(U), 256, 0, s>>>(count, U, flag);
     if ((rc = exclusive_scan_i32(s, flag, fpos, U, ftotal, ustemp))) return rc;
     compact_kernel<<<g1(U), 256, 0, s>>>(flag, fpos, U, ulist, nullptr, nullptr, rankU, 0);
-    DM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
+    // dtotal is zero (the grouping's scalar memset)
     const int64_t N = std::min<int64_t>(n, k);
     std::vector<int32_t> ufront{0};
     int64_t F = 0, sorted_inds = 0;

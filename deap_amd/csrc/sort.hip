@@ -396,6 +396,16 @@ __global__ void key_obj_kernel(const double* wv, int nobj, int obj, const int32_
         keys[i] = desc ? ~k : k;
     }
 }
+// key_obj_kernel over the identity order, which it also writes to vals
+__global__ void key_obj_iota_kernel(const double* wv, int nobj, int obj, int32_t* vals,
+                                    uint64_t* keys, int64_t n, bool desc) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ordered_key(wv[i * nobj + obj]);
+        keys[i] = desc ? ~k : k;
+        vals[i] = (int32_t)i;
+    }
+}
 __global__ void iota_kernel(int32_t* v, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -410,10 +420,13 @@ int lex_sort_rows(hipStream_t s, const double* wv, int nobj, int64_t n, bool des
                   uint64_t* ktmp, int32_t* vals, int32_t* vtmp, void* rtemp, int nlex,
                   int begin_bit) {
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-    iota_kernel<<<g, 256, 0, s>>>(vals, n);
     if (nlex < 0 || nlex > nobj) nlex = nobj;
+    if (nlex == 0) iota_kernel<<<g, 256, 0, s>>>(vals, n);
     for (int o = nlex - 1; o >= 0; --o) {  // LSD over objectives: last objective first
-        key_obj_kernel<<<g, 256, 0, s>>>(wv, nobj, o, vals, keys, n, desc);
+        if (o == nlex - 1)
+            key_obj_iota_kernel<<<g, 256, 0, s>>>(wv, nobj, o, vals, keys, n, desc);
+        else
+            key_obj_kernel<<<g, 256, 0, s>>>(wv, nobj, o, vals, keys, n, desc);
         int rc = radix_sort_pairs(s, keys, vals, ktmp, vtmp, n, begin_bit, 64, rtemp);
         if (rc) return rc;
     }
