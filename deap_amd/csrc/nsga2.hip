@@ -1161,14 +1161,35 @@ __device__ __forceinline__ bool dominates_wv(const double* a, const double* b, i
     return not_equal;
 }
 
-// keys of both permutations: segment q (0, 1) = the Philox keys of call q
-__global__ void dcd_keys_kernel(Rng rng, int64_t n, uint64_t* keys, int32_t* vals) {
+// random.sample(individuals, len(individuals)) twice (emo.py:186-187):
+// permutation q of [0, n) as a keyed pseudo-random permutation -- a 4-round
+// balanced Feistel network on 2 hb bits (2^(2 hb) >= n) whose round
+// functions are Philox draws (stage ST_DCD, item = the right half, sub =
+// 3 + 4 q + round), cycle-walked into [0, n) (x = F(x) until x < n: a
+// bijection of [0, n), expected under four steps since 2^(2 hb) < 4 n).  One
+// pass where sorting 2 n 64-bit Philox keys took a batched 8-pass radix sort.
+__device__ __forceinline__ uint32_t dcd_feistel(const Rng& rng, uint32_t q, uint32_t x, int hb,
+                                                uint32_t mask) {
+    uint32_t L = x >> hb, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t f = rng(ST_DCD, R, 3u + 4u * q + (uint32_t)r).x & mask;
+        const uint32_t t = L ^ f;
+        L = R;
+        R = t;
+    }
+    return (L << hb) | R;
+}
+__global__ void dcd_perm_kernel(Rng rng, int64_t n, int hb, int32_t* p1, int32_t* p2) {
+    const uint32_t mask = (1u << hb) - 1u;
     GRID_LOOP(t, 2 * n) {
         const uint32_t q = t >= n ? 1u : 0u;
         const int64_t i = t - (int64_t)q * n;
-        const u32x4 w = rng(ST_DCD, (uint32_t)i, q);
-        keys[t] = ((uint64_t)w.x << 32) | w.y;
-        vals[t] = (int32_t)i;
+        uint32_t x = (uint32_t)i;
+        do {
+            x = dcd_feistel(rng, q, x, hb, mask);
+        } while ((int64_t)x >= n);
+        (q ? p2 : p1)[i] = (int32_t)x;
     }
 }
 
@@ -1242,32 +1263,18 @@ extern "C" int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const doubl
     if (k == 0) return DM_OK;
     hipStream_t s = ctx->stream;
     if (mode != DM_RNG_INJECT) {
-        // random.sample(individuals, len(individuals)) twice: permutations from
-        // sorting Philox keys (stable radix sort, ties by index), both in ONE
-        // batched sort (two segments of n: 8 radix passes, not 16)
-        const size_t kb = align_up((size_t)n * 16, 256), vb = align_up((size_t)n * 8, 256);
-        char* w = (char*)scratch(ctx, 2 * kb + 2 * vb + radix_sort_batched_temp_bytes(2, n));
-        if (!w) return DM_ERR_NOMEM;
-        uint64_t* keys = (uint64_t*)w;
-        uint64_t* ktmp = (uint64_t*)(w + kb);
-        int32_t* vals = (int32_t*)(w + 2 * kb);
-        int32_t* vtmp = (int32_t*)(w + 2 * kb + vb);
-        void* rtemp = w + 2 * kb + 2 * vb;
-        dcd_keys_kernel<<<g1(2 * n), 256, 0, s>>>(Rng(rng), n, keys, vals);
-        bool in_tmp = false;
-        if ((rc = radix_sort_pairs_batched(s, keys, vals, ktmp, vtmp, 2, n, 0, 64, rtemp, &in_tmp)))
-            return rc;
-        int32_t* sorted = in_tmp ? vtmp : vals;
-        if (perm1) {  // the caller's dump buffers
-            DM_HIP(hipMemcpyAsync(perm1, sorted, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
-        } else {
-            perm1 = sorted;
+        // random.sample(individuals, len(individuals)) twice (dcd_perm_kernel)
+        int d = 1;
+        while ((1ll << d) < n) ++d;
+        const int hb = (d + 1) / 2;
+        int32_t* w = nullptr;
+        if (!perm1 || !perm2) {
+            w = (int32_t*)scratch(ctx, 2 * align_up((size_t)n * 4, 256));
+            if (!w) return DM_ERR_NOMEM;
         }
-        if (perm2) {
-            DM_HIP(hipMemcpyAsync(perm2, sorted + n, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
-        } else {
-            perm2 = sorted + n;
-        }
+        if (!perm1) perm1 = w;
+        if (!perm2) perm2 = (int32_t*)((char*)w + align_up((size_t)n * 4, 256));
+        dcd_perm_kernel<<<g1(2 * n), 256, 0, s>>>(Rng(rng), n, hb, perm1, perm2);
     }
     dcd_kernel<<<g1(k4), 256, 0, s>>>(pop->wvalues, pop->nobj, crowd, perm1, perm2, k4, Rng(rng),
                                       mode, coin, out_idx);

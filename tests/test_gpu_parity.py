@@ -810,6 +810,27 @@ def test_sel_tournament_dcd_native_replays_in_oracle(gpu):
     assert np.array_equal(again, got)
     # each individual appears at most twice per permutation pass (4 per call)
     assert np.bincount(got, minlength=n).max() <= 4
+    # the permutations (keyed Feistel networks, cycle-walked into [0, n)) carry
+    # no trace of the identity or of each other
+    idx = np.arange(n)
+    for p in (p1, p2):
+        assert abs(np.corrcoef(idx, p)[0, 1]) < 0.02
+        assert (p == idx).sum() < 10
+    assert abs(np.corrcoef(p1, p2)[0, 1]) < 0.02
+
+
+def test_sel_tournament_dcd_permutations_small_sizes(gpu):
+    """The cycle walk at every small size (domains of 2^2 .. 2^8 around n):
+    both permutations are bijections of [0, n)."""
+    from deap_amd import tools
+    from deap_amd.ops import RandomStream
+    rng = np.random.default_rng(5)
+    for n in list(range(4, 70, 4)) + [100, 128, 200, 256, 260]:
+        pop = _dcd_pop(rng.random((n, 2)), rng.random(n))
+        dec = {}
+        tools.selTournamentDCD(pop, n, mode="dump", decisions=dec, stream=RandomStream(n))
+        for key in ("perm1", "perm2"):
+            assert np.array_equal(np.sort(dec[key].cpu().numpy()), np.arange(n)), (n, key)
 
 
 def test_sel_tournament_dcd_errors(gpu):
