@@ -591,9 +591,9 @@ def peel_work(wv, fronts, peel_us):
 
 def peel_report(peel_us, usz, m=3):
     """C5's dominant kernel, the table-fed front peel (dominance.hip
-    peel_tab_kernel): one launch per front; launch i peels front i (usz[i]
-    unique fitnesses) and releases front i + 1, the launches after the last
-    front exit at once.  It is VALU-issue and latency bound (64 x 64 bit
+    peel_order_kernel): one launch per front; launch i peels front i (usz[i]
+    unique fitnesses), releasing front i + 1, and -- in its search workgroups
+    -- orders front i; the launches after the last front exit at once.  It is VALU-issue and latency bound (64 x 64 bit
     transposes of the members' rows), so its roofline is VALU
     wave-instructions issued per second against the issue peak (256 CU x 4
     SIMD x 2.4 GHz / 2 clk per wave64 instruction on SIMD-32): the
@@ -616,7 +616,7 @@ def peel_report(peel_us, usz, m=3):
         with open(path) as f:
             pmc = json.load(f)
     roof = {"bound": "valu-issue", "unit": "Ginstr/s",
-            "kernel": "peel_tab_kernel<%d>" % (m - 1) if m <= 3 else "peel_owned_kernel",
+            "kernel": "peel_order_kernel<%d>" % (m - 1) if m <= 3 else "peel_owned_kernel",
             "peak": round(VALU_PEAK_GINSTR, 1), "kernel_ms": round(tot_ms, 4),
             "peak_basis": "wave64 VALU instructions: 256 CU x 4 SIMD-32 x 2.4 GHz / 2 clk",
             "traffic": None, "achieved": None, "frac": None}

@@ -1,6 +1,6 @@
 // bitdom.hpp — bitset-table dominance (bitdom.hip): constants, the tables'
 // layout and the device helpers shared by the table passes and the
-// table-fed front peel (dominance.hip peel_tab_kernel).
+// table-fed front peel (dominance.hip peel_order_kernel).
 #pragma once
 #include "dominance.hpp"
 

@@ -27,6 +27,8 @@
 //    decides termination on the device.  The host only checks a status word
 //    every few fronts.
 #include "bitdom.hpp"
+
+#include <atomic>
 #include "transpose.hpp"
 
 namespace dm {
@@ -906,15 +908,6 @@ __global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_MINW) void peel_owned_kern
                         sust, snf, s, blockIdx.y, nsl, L, S);
 }
 
-// Table-fed peel (the default with the bitset pass, 2-3 objectives): one
-// workgroup per 512-v chunk c of the q order and member slice, as
-// peel_owned_kernel, but each member's row bits over c are computed from the
-// chunk's bitset tables (bd_row_words: a binary search of the chunk's sorted
-// ranks in LDS and one 64-byte prefix-set read from the global table per
-// objective; a workgroup reads only the sets its members need, mostly from
-// L2) instead of read from a stored D, so the dominance matrix is never
-// written.  Each member's (reach, tie-group end, ranks) record is read from
-// the front-ordered table (MemberTab), a window of 2,048 at a time.
 #ifndef DM_PEEL_TAB_MINW
 #define DM_PEEL_TAB_MINW 4  // min waves per SIMD (4: two 512-thread workgroups per CU)
 #endif
@@ -927,176 +920,6 @@ __device__ unsigned int g_pprof_n;
 #else
 #define PPROF_T(x)
 #endif
-template <int F>
-__global__ __launch_bounds__(PEEL_WAVES * 64, DM_PEEL_TAB_MINW) void peel_tab_kernel(
-    const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
-    const int4* __restrict__ mtab, const int32_t* __restrict__ gsize,
-    const int32_t* __restrict__ sigma, FrontState* st, int32_t* countq, unsigned long long* lastq,
-    uint64_t* ckey, int32_t* cq, int32_t* rankU, CandRec cr) {
-    static_assert(PEEL_WAVES * 64 == BD_CW, "one thread per v of the chunk (sorted ranks, release)");
-    constexpr int PW = BD_CW / 64;  // words of a chunk
-    __shared__ int32_t sR[F][BD_RP];
-    __shared__ uint16_t sB[F][BD_BKN];
-    __shared__ PeelLdsT<BD_CW> L;
-    __shared__ PeelSmallT<BD_CW> Sm;
-    __shared__ int32_t sF, sust, sstop, snf;
-    __shared__ int64_t sU;
-    // grid x = NG rounded up to a multiple of 8: the slices y of chunk c (linear
-    // workgroup ids c + y gridDim.x) land on one XCD, whose L2 then serves
-    // the chunk's table slice to all of them
-    PPROF_T(pt0);
-    const int64_t c = blockIdx.x;
-    const int64_t NG = (st->U + BD_CW - 1) / BD_CW;
-    if (c >= NG) return;
-    // loads that do not depend on the front go out first: the chunk's sorted
-    // ranks, and this thread's v (count, U index, individual count)
-    const int32_t* gR = R + c * F * BD_CW;
-    int32_t rr[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) rr[f] = gR[f * BD_CW + threadIdx.x];
-    if (threadIdx.x == 0) {
-        sF = st->F;
-        sust = st->ustart;
-        snf = st->nfronts;
-        sstop = st->done | st->overflow;
-        sU = st->U;
-    }
-    __syncthreads();
-    if (sstop) return;
-    const int64_t nsl = peel_slices(sF, c, NG, gridDim.y, DM_PEEL_TAB_SLICE_MIN);
-    if ((int64_t)blockIdx.y >= nsl) return;
-    const int64_t U = sU;
-    PeelPre<1> pre;
-    {
-        const int64_t v = c * BD_CW + threadIdx.x;
-        pre.cnt[0] = v < U ? countq[v] : 0;
-        pre.vu[0] = v < U ? sigma[v] : 0;
-        if (!BD_OK(pre.vu[0], U, "peel sigma")) pre.vu[0] = 0;
-        pre.gs[0] = v < U ? gsize[pre.vu[0]] : 0;
-    }
-    const int64_t slen = ((sF + nsl - 1) / nsl + 63) & ~63ll;
-    const int64_t j0s = blockIdx.y * slen;
-    const int64_t Fm = std::min<int64_t>(sF, j0s + slen);
-    // (reach, last q of the objective-0 tie group, ranks 1 and 2) per member,
-    // front order: built per q once per selection (member_rec_kernel), carried by the
-    // released candidates and written in front order by the ordering (MemberTab)
-    const int4* members = mtab + sust;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int STEP = PEEL_WAVES * 64;
-    constexpr int WIN = 2048;       // 4 members per thread (8 spilled, and so did
-                                    // loading the first window in the prologue)
-    constexpr int WR = WIN / STEP;  // members per thread per window
-    static_assert(WIN * sizeof(int4) <= sizeof(PeelLdsT<BD_CW>), "window list in the release's LDS");
-#pragma unroll
-    for (int f = 0; f < F; ++f) sR[f][bd_rpad(threadIdx.x)] = rr[f];
-    bd_load_buckets<F>(BK, c, sB);
-    const int sh = bd_bucket_shift(U);
-    const BdGlobalSets sets{reinterpret_cast<const uint4*>(P + c * F * BD_K * 16)};
-    const TransposerX tr(lane);
-    int32_t dec[PW], last[PW];
-#pragma unroll
-    for (int w = 0; w < PW; ++w) {
-        dec[w] = 0;
-        last[w] = -1;
-    }
-    const int64_t v0 = c * BD_CW;
-    // The slice is taken in windows of WIN members.  A window's members whose
-    // row reaches chunk c are compacted, in front order, into LDS as (ranks,
-    // tie-group end, front position) -- the release's LDS, not yet in use --
-    // and processed
-    // 64 at a time, so no group carries members that do not reach the chunk
-    // (a front's members reach chunks up to their objective-0 position: in
-    // front order about half of a group's lanes were idle on the high
-    // chunks).  Positions rise within a group, so the top set bit of a
-    // transposed word is its last dominator, read back by a lane shuffle.
-    int4* sM = reinterpret_cast<int4*>(&L);
-    PPROF_T(pt1);
-    for (int64_t wb = j0s; wb < Fm; wb += WIN) {
-        uint64_t bal[WR];
-        int4 mr[WR];
-        int nw = 0;
-#pragma unroll
-        for (int r = 0; r < WR; ++r) {
-            const int64_t j = wb + (int64_t)(wave * WR + r) * 64 + lane;
-            mr[r] = j < Fm && BD_OK(sust + j, U, "peel member") ? members[j] : make_int4(0, 0, 0, 0);
-            bal[r] = __ballot(j < Fm && c < mr[r].x);
-            nw += __popcll(bal[r]);
-        }
-        if (lane == 0) Sm.wcnt[0][wave] = nw;
-        __syncthreads();
-        int base = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < PEEL_WAVES; ++w) {
-            const int x = Sm.wcnt[0][w];
-            base += w < wave ? x : 0;
-            total += x;
-        }
-        const uint64_t below = (1ull << lane) - 1;
-#pragma unroll
-        for (int r = 0; r < WR; ++r) {
-            if ((bal[r] >> lane) & 1)
-                sM[base + __popcll(bal[r] & below)] =
-                    make_int4(mr[r].z, mr[r].w, mr[r].y,
-                              (int32_t)(wb - j0s + (int64_t)(wave * WR + r) * 64 + lane));
-            base += __popcll(bal[r]);
-        }
-        __syncthreads();
-        // (rank 1, rank 2, tie-group end, front position in the slice)
-        auto mget = [&](int g) { return g < total ? sM[g] : make_int4(0, 0, 0, -1); };
-        for (int g0 = wave * 64; g0 < total; g0 += STEP) {
-            const int4 mA = mget(g0 + lane);
-            const bool has = mA.w >= 0;
-            const int4 suA = make_int4(mA.x, mA.y, 0, 0);
-            const int32_t lim = (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mA.z - v0, BD_CW));
-            int k[F];
-            if (has && lim >= 0) {
-                bd_row_k<F>(suA, sR, sB, sh, k);
-#ifdef DM_BD_CHECK
-                for (int f = 0; f < F; ++f)
-                    if (!BD_OK(k[f], BD_K, "peel k")) k[f] = 0;
-#endif
-            } else {
-#pragma unroll
-                for (int f = 0; f < F; ++f) k[f] = 0;
-            }
-            uint4 raw[F][4], w[4];
-            bd_row_fetch<F>(sets, k, raw);
-            bd_row_merge<F, false>(raw, lim, -1, w);
-            uint32_t lo[8], hi[8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                lo[2 * i] = w[i].x;
-                hi[2 * i] = w[i].y;
-                lo[2 * i + 1] = w[i].z;
-                hi[2 * i + 1] = w[i].w;
-            }
-            tr.run<8>(lo, hi);  // lane v: bit i <-> group member i dominates v
-            const int32_t posA = (int32_t)(j0s + mA.w);
-#pragma unroll
-            for (int w2 = 0; w2 < 8; ++w2) {
-                dec[w2] += __popc(lo[w2]) + __popc(hi[w2]);
-                const int32_t top = hi[w2] ? 63 - __clz(hi[w2]) : (lo[w2] ? 31 - __clz(lo[w2]) : 0);
-                const int32_t pt = __shfl(posA, top);
-                if (lo[w2] | hi[w2]) last[w2] = pt;
-            }
-        }
-        __syncthreads();  // the window's list is read out before the next (or the release) reuses it
-    }
-    PPROF_T(pt2);
-    peel_release<false, PW>(dec, last, v0, gsize, sigma, st, countq, lastq, ckey, cq, rankU, U,
-                            snf, nsl, L, Sm, &pre, cr);
-#ifdef DM_PEEL_PROF
-    PPROF_T(pt3);
-    if (threadIdx.x == 0) {
-        const unsigned int e = atomicAdd(&g_pprof_n, 1u);
-        if (e < (1u << 17)) {
-            unsigned long long* o = g_pprof + (size_t)e * 8;
-            o[0] = c; o[1] = blockIdx.y; o[2] = sF; o[3] = pt0; o[4] = pt1; o[5] = pt2; o[6] = pt3; o[7] = 0;
-        }
-    }
-#endif
-}
-
 constexpr int ORDER_CAP = 16384;  // candidates sorted in registers + LDS by one workgroup
 
 // member i of a front: (its row in q order, the row segments it reaches)
@@ -1118,7 +941,7 @@ __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t
     DGRID_LOOP(q, U) {
         const int4 s = S[q];
         qrec[q] = make_int4(nseg[q / (64 * TD_WPW)], span[q].y, s.x, s.y);
-        lastq[q] = 0;  // the sliced peels' (front, last position) per v
+        if (lastq) lastq[q] = 0;  // the sliced peels' (front, last position) per v
     }
 }
 
@@ -1460,6 +1283,736 @@ __global__ void front_init_kernel(FrontState* st, const int32_t* F0p, const int6
 }
 
 // ---------------------------------------------------------------------------
+// 3b. the table peel with the ordering one launch behind it (2-3 objectives)
+// ---------------------------------------------------------------------------
+// Which fits form front j+1 depends only on front j's membership: a v is
+// released when the front's members that dominate it bring its count to
+// zero, whatever their order.  Only the ORDER of front j+1 (emo.py:96-104:
+// a fit is appended when its last dominator -- in front order -- is
+// processed, after the ones that dominator released before it, in U order)
+// needs front j's order.  So the two chains are separated:
+//  * the peel of front j (the chunk workgroups) takes its members in slot
+//    order and only counts; it releases front j+1's members into candidate
+//    buffer (j+1) % 3 (eight slot buckets, as above);
+//  * TAB_NA search workgroups of the same launch find, for each member v of
+//    front j (released by the previous launch), its last dominator: front
+//    j-1's members sit in front order in the record table (mtab), and a scan
+//    from the end of that front stops at the first member u with q(v) <=
+//    tie-group end(u) and r_i(v) <= r_i(u) -- the relation the bitset rows
+//    encode -- which is the one of largest position.  The key (position, U
+//    index) goes to the candidate's slot with a coherent store; the last
+//    search workgroup to arrive sorts front j by it (counting sort), writes
+//    it to ulist and its records to mtab in front order, and hands the state
+//    to launch j+1.
+// One launch per front, where the peel and the ordering took two dependent
+// ones; the ordering is off the peel chain as long as it finishes within the
+// peel's launch.
+struct FrontStep {
+    int64_t sorted;  // individuals in the fronts before j
+    int32_t ustart;  // front j's start in ulist / mtab
+    int32_t Fprev;   // size of front j - 1
+    uint32_t valid;  // the call's epoch when written (entries of earlier calls stay in the workspace)
+    int32_t done;    // no front j (emo.py:109, or every fit sorted)
+    int32_t pad[2];
+};
+struct FrontSum {      // read by the host after each batch of launches
+    int32_t nfronts;   // the last front ordered (fronts 1..nfronts after front 0)
+    int32_t done;
+    int32_t overflow;  // front nfronts + 1 has more members than the sorting workgroup holds
+    int32_t ncand;
+    int64_t sorted, lastinds;
+    int32_t arrive[3];  // search workgroups done, per candidate buffer
+};
+struct CandBufs {
+    char* pages;     // [3][8] counter pages: slot count at +0, released individuals at +64
+    uint64_t* ckey;  // [3][8 cap]: U index, then (last position << 32 | U index)
+    int32_t* cq;     // [3][8 cap]: q
+    int4* crec;      // [3][8 cap]: the member record (reach, tie-group end, rank 1, rank 2)
+    int64_t cap;
+    __device__ __forceinline__ int32_t* count(int buf, int b) const {
+        return reinterpret_cast<int32_t*>(pages + CAND_PAGE * (buf * CAND_BUCKETS + b));
+    }
+    __device__ __forceinline__ unsigned long long* pending(int buf, int b) const {
+        return reinterpret_cast<unsigned long long*>(pages + CAND_PAGE * (buf * CAND_BUCKETS + b) + 64);
+    }
+    __device__ __forceinline__ int64_t base(int buf) const { return (int64_t)buf * CAND_BUCKETS * cap; }
+};
+struct TabArgs {
+    const uint32_t* P;
+    const int32_t* R;
+    const uint16_t* BK;
+    const int4* qrec;
+    const int32_t* gsize;
+    const int32_t* sigma;
+    const int32_t* pos;  // U index -> q
+    int32_t* countq;
+    int32_t* rankU;
+    int32_t* ulist;
+    int32_t* fstarts;
+    int4* mtab;  // [U] member records in front order: front j at [ustart_j, ustart_j + n_j)
+    int32_t* gslot;  // [U] a large front's members' places in their bins (tab_sort_big)
+    int32_t* gtmp;   // [U] ... and its U indices binned
+    FrontStep* stf;
+    FrontSum* sum;
+    CandBufs cb;
+    int64_t U, N;
+    int64_t gx;      // chunk workgroups per slice row (NG rounded up to 8)
+    uint32_t epoch;  // this call's stamp for stf entries
+};
+constexpr int TAB_NT = PEEL_WAVES * 64;       // the launch's workgroup size
+constexpr int TAB_NA = 128;                   // search workgroups per launch (a multiple of 8)
+constexpr int TAB_WIN = 2048;                 // peel members per window
+constexpr int TAB_SWIN = 2048;                // previous-front members per search window
+constexpr int TAB_ORDER_CAP = 16 * TAB_NT;    // members the sorting workgroup orders
+template <int F>
+struct TabLds {  // byte offsets in the launch's shared buffer
+    static constexpr size_t sR = 0;
+    static constexpr size_t sB = sR + 4 * F * BD_RP;
+    static constexpr size_t dec = (sB + 2 * F * BD_BKN + 15) / 16 * 16;
+    static constexpr size_t sM = dec + 4 * PEEL_WAVES * BD_CW;
+    static constexpr size_t peel = sM + 16 * TAB_WIN;
+    static constexpr size_t search = 16 * TAB_SWIN;
+    static constexpr size_t order = sizeof(OrderLds<TAB_ORDER_CAP>);
+    static constexpr size_t bytes = std::max(std::max(peel, search), order);
+};
+struct TabScalars {
+    FrontStep sf;
+    CandMap cm;
+    int64_t pend;
+    int32_t n, go, smax, sbase, last;
+    int32_t wcnt[PEEL_WAVES];
+    int64_t wgs[PEEL_WAVES];
+    int32_t part[64];
+};
+
+// buffer `buf`'s candidate list (thread 0)
+__device__ __forceinline__ void tab_cand_list(const CandBufs& cb, int buf, TabScalars& sc) {
+    int32_t run = 0;
+    int64_t p = 0;
+    for (int b = 0; b < CAND_BUCKETS; ++b) {
+        sc.cm.pre[b] = run;
+        run += *cb.count(buf, b);
+        p += (int64_t)*cb.pending(buf, b);
+    }
+    sc.cm.pre[CAND_BUCKETS] = run;
+    sc.cm.cap = cb.cap;
+    sc.n = run;
+    sc.pend = p;
+}
+
+// Front j is ordered: empty front j-1's buffer and this launch's arrival
+// count, hand the state to launch j+1 (thread 0).
+__device__ void tab_finish(const TabArgs& a, int32_t j, int32_t n, int64_t pend, const FrontStep& sf) {
+    const int rb = (j + 2) % 3;
+    for (int b = 0; b < CAND_BUCKETS; ++b) {
+        *a.cb.count(rb, b) = 0;
+        *a.cb.pending(rb, b) = 0ull;
+    }
+    a.sum->arrive[j % 3] = 0;
+    FrontStep nx{};
+    nx.sorted = sf.sorted + pend;
+    nx.ustart = sf.ustart + n;
+    nx.Fprev = n;
+    nx.valid = a.epoch;
+    nx.done = (nx.sorted >= a.N || nx.ustart >= a.U) ? 1 : 0;
+    a.stf[j + 1] = nx;
+    a.fstarts[j + 1] = nx.ustart;
+    a.sum->nfronts = j;
+    a.sum->sorted = nx.sorted;
+    a.sum->lastinds = pend;
+    a.sum->done = nx.done;
+    a.sum->overflow = 0;
+}
+
+// counting sort of front j by its keys (last position l < Fr, U index):
+// binned in LDS, ranked inside the bin (as order_count); false when a bin
+// holds more than ORDER_BIN_MAX (the bitonic sort orders them)
+template <int NT, int E>
+__device__ bool tab_sort_count(const TabArgs& a, int64_t bbase, const CandMap& cm, int32_t n,
+                               int32_t Fr, int32_t ustart, OrderLds<TAB_ORDER_CAP>& lds,
+                               TabScalars& sc) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i <= Fr; i += NT) lds.cs.base[i] = 0;
+    uint64_t key[E];
+    int32_t sidx[E], slot[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        sidx[e] = i < n ? (int32_t)cm.slot(i) : 0;
+        key[e] = i < n ? cld<true>(a.cb.ckey + bbase + sidx[e]) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        if (i < n) {
+            int32_t l = (int32_t)(key[e] >> 32);
+            if (!BD_OK(l, Fr, "tab sort bin")) l = 0;
+            slot[e] = atomicAdd(&lds.cs.base[l], 1);
+        }
+    }
+    __syncthreads();
+    const int C = (Fr + NT - 1) / NT;
+    const int b0 = tid * C, b1 = min(Fr, b0 + C);
+    int32_t sum = 0, mx = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = lds.cs.base[b];
+        sum += c;
+        mx = max(mx, c);
+    }
+    if (mx > ORDER_BIN_MAX) atomicMax(&sc.smax, mx);
+    int32_t run = block_excl_scan<NT>(sum, sc.part);
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = lds.cs.base[b];
+        lds.cs.base[b] = run;
+        run += c;
+    }
+    if (tid == 0) lds.cs.base[Fr] = n;
+    __syncthreads();
+    if (sc.smax != 0) {
+        __syncthreads();  // the bitonic fallback reuses the LDS
+        return false;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * NT;
+        if (i < n) {
+            const int32_t l = (int32_t)(key[e] >> 32), vu = (int32_t)(uint32_t)key[e];
+            const int32_t beg = lds.cs.base[l], end = lds.cs.base[l + 1];
+            int32_t r = beg;
+            for (int32_t q = beg; q < end; ++q) r += lds.cs.tmp[q] < vu ? 1 : 0;
+            a.ulist[ustart + r] = vu;
+            a.mtab[ustart + r] = a.cb.crec[bbase + sidx[e]];
+        }
+    }
+    return true;
+}
+template <int NT, int E>
+__device__ void tab_sort_bitonic(const TabArgs& a, int64_t bbase, const CandMap& cm, int32_t n,
+                                 int32_t ustart, uint64_t* lds) {
+    uint64_t k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = threadIdx.x * E + e;
+        k[e] = i < n ? cld<true>(a.cb.ckey + bbase + cm.slot(i)) : ~0ull;
+    }
+    block_bitonic<NT, E>(k, lds);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = threadIdx.x * E + e;
+        if (i < n) {
+            const int32_t vu = (int32_t)(uint32_t)k[e];
+            a.ulist[ustart + i] = vu;
+            if (BD_OK(vu, a.U, "tab sorted vu")) a.mtab[ustart + i] = a.qrec[a.pos[vu]];
+        }
+    }
+}
+
+// A front of more than TAB_ORDER_CAP members: the same counting sort with
+// the bins' starts in LDS (Fr + 1 <= TAB_BIG_BINS) and each member's place
+// in its bin and the binned U indices in global memory (L2; agent-scope
+// accesses); false when a bin holds more than TAB_BIG_BIN_MAX members (the
+// host sorts the front then).
+constexpr int TAB_BIG_BINS = TAB_ORDER_CAP * 2;  // ints of OrderLds<TAB_ORDER_CAP>
+constexpr int TAB_BIG_BIN_MAX = 512;
+template <int NT>
+__device__ bool tab_sort_big(const TabArgs& a, int64_t bbase, const CandMap& cm, int32_t n,
+                             int32_t Fr, int32_t ustart, int32_t* base, TabScalars& sc) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i <= Fr; i += NT) base[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += NT) {
+        int32_t l = (int32_t)(cld<true>(a.cb.ckey + bbase + cm.slot(i)) >> 32);
+        if (!BD_OK(l, Fr, "tab big bin")) l = 0;
+        cst<true>(a.gslot + i, atomicAdd(&base[l], 1));
+    }
+    __syncthreads();
+    const int C = (Fr + NT - 1) / NT;
+    const int b0 = tid * C, b1 = min(Fr, b0 + C);
+    int32_t sum = 0, mx = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = base[b];
+        sum += c;
+        mx = max(mx, c);
+    }
+    if (mx > TAB_BIG_BIN_MAX) atomicMax(&sc.smax, mx);
+    int32_t run = block_excl_scan<NT>(sum, sc.part);
+    for (int b = b0; b < b1; ++b) {
+        const int32_t c = base[b];
+        base[b] = run;
+        run += c;
+    }
+    if (tid == 0) base[Fr] = n;
+    __syncthreads();
+    if (sc.smax != 0) return false;
+    for (int i = tid; i < n; i += NT) {
+        const uint64_t k = cld<true>(a.cb.ckey + bbase + cm.slot(i));
+        const int32_t l = (int32_t)(k >> 32);
+        cst<true>(a.gtmp + base[l] + cld<true>(a.gslot + i), (int32_t)(uint32_t)k);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int i = tid; i < n; i += NT) {
+        const int64_t sl = bbase + cm.slot(i);
+        const uint64_t k = cld<true>(a.cb.ckey + sl);
+        const int32_t l = (int32_t)(k >> 32), vu = (int32_t)(uint32_t)k;
+        const int32_t beg = base[l], end = base[l + 1];
+        int32_t r = beg;
+        for (int32_t q = beg; q < end; ++q) r += cld<true>(a.gtmp + q) < vu ? 1 : 0;
+        a.ulist[ustart + r] = vu;
+        a.mtab[ustart + r] = a.cb.crec[sl];
+    }
+    return true;
+}
+
+// the last search workgroup of launch j: front j in order (n <= TAB_ORDER_CAP)
+template <int NT>
+__device__ void tab_sort_front(const TabArgs& a, int32_t j, char* smem, TabScalars& sc) {
+    const int32_t n = sc.n;
+    const CandMap cm = sc.cm.uniform();
+    const int64_t bbase = a.cb.base(j % 3);
+    const int32_t Fr = sc.sf.Fprev, ustart = sc.sf.ustart;
+    auto& lds = *reinterpret_cast<OrderLds<TAB_ORDER_CAP>*>(smem);
+    if (threadIdx.x == 0) sc.smax = 0;
+    __syncthreads();
+    bool done = false;
+    if (Fr <= TAB_ORDER_CAP) {
+        if (n <= 4 * NT)
+            done = tab_sort_count<NT, 4>(a, bbase, cm, n, Fr, ustart, lds, sc);
+        else if (n <= 8 * NT)
+            done = tab_sort_count<NT, 8>(a, bbase, cm, n, Fr, ustart, lds, sc);
+        else
+            done = tab_sort_count<NT, 16>(a, bbase, cm, n, Fr, ustart, lds, sc);
+    }
+    if (!done) {
+        if (n <= 2 * NT)
+            tab_sort_bitonic<NT, 2>(a, bbase, cm, n, ustart, lds.keys);
+        else if (n <= 4 * NT)
+            tab_sort_bitonic<NT, 4>(a, bbase, cm, n, ustart, lds.keys);
+        else if (n <= 8 * NT)
+            tab_sort_bitonic<NT, 8>(a, bbase, cm, n, ustart, lds.keys);
+        else
+            tab_sort_bitonic<NT, 16>(a, bbase, cm, n, ustart, lds.keys);
+    }
+    if (threadIdx.x == 0) tab_finish(a, j, n, sc.pend, sc.sf);
+}
+
+// Search workgroup aw of launch j >= 1 (see the top of this section).
+template <int F>
+__device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabScalars& sc) {
+    const int tid = threadIdx.x;
+    const int buf = j % 3;
+    if (tid == 0) {
+        sc.sf = a.stf[j];
+        sc.go = sc.sf.valid == a.epoch && !sc.sf.done;
+        if (sc.go) tab_cand_list(a.cb, buf, sc);
+    }
+    __syncthreads();
+    if (!sc.go) return;
+    const int32_t n = sc.n;
+    if (n == 0) {  // nothing released: every fit is in a front
+        if (aw == 0 && tid == 0) {
+            FrontStep nx{};
+            nx.valid = a.epoch;
+            nx.done = 1;
+            a.stf[j + 1] = nx;
+            a.sum->done = 1;
+        }
+        return;
+    }
+    const CandMap cm = sc.cm.uniform();
+    const int64_t bbase = a.cb.base(buf);
+    const int32_t n1 = sc.sf.Fprev;
+    const int64_t us0 = (int64_t)sc.sf.ustart - n1;  // front j-1 in mtab
+    int4* sP = reinterpret_cast<int4*>(smem);         // (tie-group end, rank 1, rank 2) per member
+    const int32_t per = (n + TAB_NA - 1) / TAB_NA;
+    const int32_t i0 = aw * per, i1 = min(n, i0 + per);
+    // the share in chunks of TAB_NT candidates, 64 per wave; a wave tests 64
+    // members of front j-1 per step for one candidate (one ballot), its
+    // members read from the LDS window 512 at a time into registers, so the
+    // candidates of the wave reuse them
+    const int lane = tid & 63;
+    for (int32_t c0 = i0; c0 < i1; c0 += TAB_NT) {  // workgroup-uniform
+        // candidate c0 + 8 lane + wave: a small share spreads over every wave
+        const int32_t i = c0 + 8 * lane + (tid >> 6);
+        const bool mine = i < i1;
+        int64_t sl = 0;
+        int32_t vq = 0, vr1 = 0, vr2 = 0;
+        uint32_t vu = 0;
+        if (mine) {
+            sl = bbase + cm.slot(i);
+            const int4 rec = a.cb.crec[sl];
+            vq = a.cb.cq[sl];
+            vr1 = rec.z;
+            vr2 = rec.w;
+            vu = (uint32_t)a.cb.ckey[sl];
+        }
+        int32_t last = -1;
+        uint64_t open = __ballot(mine);  // the wave's candidates without their last dominator yet
+        for (int32_t wend = n1; wend > 0; wend -= TAB_SWIN) {
+            if (__syncthreads_and(open == 0)) break;  // all found (and the window read out)
+            const int32_t wb = max(0, wend - TAB_SWIN);
+            for (int32_t t = wb + tid; t < wend; t += TAB_NT) {
+                const int4 r = a.mtab[us0 + t];
+                sP[t - wb] = make_int4(r.y, r.z, r.w, 0);
+            }
+            __syncthreads();
+            // 512-member segments from the window's end; member k of this lane
+            // is position sb - 1 - 64 k - lane (descending in k and lane)
+            for (int32_t sb = wend; sb > wb && open; sb -= 8 * 64) {
+                int4 mk[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int32_t pk = sb - 1 - 64 * k - lane;
+                    mk[k] = pk >= wb ? sP[pk - wb] : make_int4(-1, 0, 0, 0);  // te -1: dominates nothing
+                }
+                uint64_t todo = open;
+                while (todo) {
+                    const int cl = __ffsll((unsigned long long)todo) - 1;
+                    todo &= todo - 1;
+                    const int32_t cq1 = __builtin_amdgcn_readlane(vq, cl);
+                    const int32_t cr1 = __builtin_amdgcn_readlane(vr1, cl);
+                    const int32_t cr2 = __builtin_amdgcn_readlane(vr2, cl);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        bool dom = cq1 <= mk[k].x && cr1 <= mk[k].y;
+                        if (F == 2) dom = dom && cr2 <= mk[k].z;
+                        const uint64_t hit = __ballot(dom);
+                        if (hit) {  // the lowest lane holds the largest position
+                            if (lane == cl) last = sb - 1 - 64 * k - (__ffsll((unsigned long long)hit) - 1);
+                            open &= ~(1ull << cl);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        if (mine) {
+            if (!BD_OK(last, n1, "tab last dominator")) last = 0;
+            cst<true>(a.cb.ckey + sl, ((uint64_t)(uint32_t)last << 32) | vu);
+        }
+        __syncthreads();  // the next chunk's first window overwrites sP
+    }
+    // every key stored (coherently) before this workgroup counts itself in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        sc.last = __hip_atomic_fetch_add(a.sum->arrive + buf, 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == TAB_NA - 1;
+    __syncthreads();
+    if (!sc.last) return;
+    if (!BD_OK(sc.sf.ustart + (int64_t)n - 1, a.U, "tab front end")) return;
+    if (n > TAB_ORDER_CAP) {
+        if (tid == 0) sc.smax = 0;
+        __syncthreads();
+        if (sc.sf.Fprev < TAB_BIG_BINS &&
+            tab_sort_big<TAB_NT>(a, a.cb.base(buf), sc.cm.uniform(), n, sc.sf.Fprev, sc.sf.ustart,
+                                 reinterpret_cast<int32_t*>(smem), sc)) {
+            if (tid == 0) tab_finish(a, j, n, sc.pend, sc.sf);
+        } else if (tid == 0) {  // the host sorts this front (tab_presorted_kernel)
+            a.sum->ncand = n;
+            a.sum->overflow = 1;
+        }
+        return;
+    }
+    tab_sort_front<TAB_NT>(a, j, smem, sc);
+}
+
+// The members [wb, we) of the front being peeled (member i at slot bbase +
+// cm.slot(i)) whose row reaches chunk c, into LDS: sM = (rank 1, rank 2,
+// tie-group end, 0).  Returns how many.
+__device__ int tab_window(const TabArgs& a, int64_t bbase, const CandMap& cm, int64_t wb,
+                          int64_t we, int64_t c, int4* sM, TabScalars& sc) {
+    constexpr int WR = TAB_WIN / TAB_NT;  // members per thread
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t bal[WR];
+    int4 mr[WR];
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+        const int64_t i = wb + (int64_t)(wave * WR + r) * 64 + lane;
+        mr[r] = i < we ? a.cb.crec[bbase + cm.slot((int32_t)i)] : make_int4(0, 0, 0, 0);
+    }
+    int nw = 0;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+        const int64_t i = wb + (int64_t)(wave * WR + r) * 64 + lane;
+        bal[r] = __ballot(i < we && c < mr[r].x);
+        nw += __popcll(bal[r]);
+    }
+    if (lane == 0) sc.wcnt[wave] = nw;
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < PEEL_WAVES; ++w) {
+        const int x = sc.wcnt[w];
+        base += w < wave ? x : 0;
+        total += x;
+    }
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+        if ((bal[r] >> lane) & 1) sM[base + __popcll(bal[r] & below)] = make_int4(mr[r].z, mr[r].w, mr[r].y, 0);
+        base += __popcll(bal[r]);
+    }
+    __syncthreads();
+    return total;
+}
+
+// chunk c, member slice y of launch j: front j's dominators subtracted from
+// countq; the v whose count reaches zero go to buffer (j + 1) % 3
+template <int F>
+__device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int64_t nslices,
+                         char* smem, TabScalars& sc) {
+    constexpr int PW = BD_CW / 64;
+    PPROF_T(pt0);
+    const int64_t U = a.U;
+    const int64_t NG = (U + BD_CW - 1) / BD_CW;
+    if (c >= NG) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t* gR = a.R + c * F * BD_CW;
+    int32_t rr[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) rr[f] = gR[f * BD_CW + tid];
+    const int buf = j % 3, nbuf = (j + 1) % 3;
+    if (tid == 0) {
+        sc.sf = a.stf[j];
+        sc.go = 0;
+        if (sc.sf.valid == a.epoch && !sc.sf.done) {
+            tab_cand_list(a.cb, buf, sc);
+            // emo.py:109: front j is peeled while pareto_sorted < N
+            sc.go = sc.n > 0 && sc.sf.sorted + sc.pend < a.N && (int64_t)sc.sf.ustart + sc.n < U;
+        }
+    }
+    const int64_t v = c * BD_CW + tid;
+    int32_t pcnt = 0, pvu = 0, pgs = 0;
+    if (v < U) {
+        pcnt = a.countq[v];
+        pvu = a.sigma[v];
+        if (!BD_OK(pvu, U, "tab sigma")) pvu = 0;
+        pgs = a.gsize[pvu];
+    }
+    __syncthreads();
+    if (!sc.go) return;
+    const int32_t n = sc.n;
+    const int64_t nsl = peel_slices(n, c, NG, nslices, DM_PEEL_TAB_SLICE_MIN);
+    if (y >= nsl) return;
+    const CandMap cm = sc.cm.uniform();
+    const int64_t bbase = a.cb.base(buf);
+    auto& sR = *reinterpret_cast<int32_t(*)[F][BD_RP]>(smem + TabLds<F>::sR);
+    auto& sB = *reinterpret_cast<uint16_t(*)[F][BD_BKN]>(smem + TabLds<F>::sB);
+    int32_t* sdec = reinterpret_cast<int32_t*>(smem + TabLds<F>::dec);
+    int4* sM = reinterpret_cast<int4*>(smem + TabLds<F>::sM);
+#pragma unroll
+    for (int f = 0; f < F; ++f) sR[f][bd_rpad(tid)] = rr[f];
+    bd_load_buckets<F>(a.BK, c, sB);
+    const int sh = bd_bucket_shift(U);
+    const BdGlobalSets sets{reinterpret_cast<const uint4*>(a.P + c * F * BD_K * 16)};
+    const TransposerX tr(lane);
+    const int64_t slen = ((n + nsl - 1) / nsl + 63) & ~63ll;
+    const int64_t j0s = y * slen;
+    const int64_t Fm = std::min<int64_t>(n, j0s + slen);
+    const int64_t v0 = c * BD_CW;
+    int32_t dec[PW];
+#pragma unroll
+    for (int w = 0; w < PW; ++w) dec[w] = 0;
+    PPROF_T(pt1);
+    for (int64_t wb = j0s; wb < Fm; wb += TAB_WIN) {
+        const int total = tab_window(a, bbase, cm, wb, std::min<int64_t>(Fm, wb + TAB_WIN), c, sM, sc);
+        for (int g0 = wave * 64; g0 < total; g0 += TAB_NT) {
+            const int g = g0 + lane;
+            const int4 mA = g < total ? sM[g] : make_int4(0, 0, 0, 0);
+            const int32_t lim =
+                g < total ? (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mA.z - v0, BD_CW)) : -1;
+            int k[F];
+            if (lim >= 0) {
+                bd_row_k<F>(make_int4(mA.x, mA.y, 0, 0), sR, sB, sh, k);
+#ifdef DM_BD_CHECK
+                for (int f = 0; f < F; ++f)
+                    if (!BD_OK(k[f], BD_K, "tab peel k")) k[f] = 0;
+#endif
+            } else {
+#pragma unroll
+                for (int f = 0; f < F; ++f) k[f] = 0;
+            }
+            uint4 raw[F][4], w[4];
+            bd_row_fetch<F>(sets, k, raw);
+            bd_row_merge<F, false>(raw, lim, -1, w);
+            uint32_t lo[8], hi[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                lo[2 * i] = w[i].x;
+                hi[2 * i] = w[i].y;
+                lo[2 * i + 1] = w[i].z;
+                hi[2 * i + 1] = w[i].w;
+            }
+            tr.run<8>(lo, hi);  // lane v: bit i <-> group member i dominates v
+#pragma unroll
+            for (int w2 = 0; w2 < 8; ++w2) dec[w2] += __popc(lo[w2]) + __popc(hi[w2]);
+        }
+        __syncthreads();  // the window's list is read out before the next one
+    }
+    PPROF_T(pt2);
+    // release: the waves' counts reduced in LDS, applied to countq
+#pragma unroll
+    for (int w = 0; w < PW; ++w) sdec[wave * BD_CW + w * 64 + lane] = dec[w];
+    __syncthreads();
+    int32_t d = 0;
+#pragma unroll
+    for (int wv = 0; wv < PEEL_WAVES; ++wv) d += sdec[wv * BD_CW + tid];
+    bool fresh = false;
+    if (v < U && d > 0) {
+        if (nsl == 1) {
+            const int32_t left = pcnt - d;
+            a.countq[v] = left;
+            fresh = left == 0;
+        } else {
+            const int32_t old = __hip_atomic_fetch_add(a.countq + v, -d, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            fresh = old == d;
+        }
+    }
+    int4 rq = make_int4(0, 0, 0, 0);
+    if (fresh) rq = a.qrec[v];  // in flight across the slot reservation
+    const uint64_t fm = __ballot(fresh);
+    int64_t gs = fresh ? pgs : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
+    if (lane == 0) {
+        sc.wcnt[wave] = __popcll(fm);
+        sc.wgs[wave] = gs;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int32_t tot = 0;
+        int64_t gtot = 0;
+        for (int wv = 0; wv < PEEL_WAVES; ++wv) {
+            const int32_t x = sc.wcnt[wv];
+            sc.wcnt[wv] = tot;
+            tot += x;
+            gtot += sc.wgs[wv];
+        }
+        const int b = (int)(c & (CAND_BUCKETS - 1));
+        sc.sbase = tot ? (int32_t)(b * a.cb.cap) + atomicAdd(a.cb.count(nbuf, b), tot) : 0;
+        if (gtot) atomicAdd(a.cb.pending(nbuf, b), (unsigned long long)gtot);
+    }
+    __syncthreads();
+    if (fresh) {
+        const int32_t at = sc.sbase + sc.wcnt[wave] + __popcll(fm & ((1ull << lane) - 1));
+        const int64_t slot = a.cb.base(nbuf) + at;
+        if (BD_OK(at, CAND_BUCKETS * a.cb.cap, "tab slot") && BD_OK(pvu, U, "tab vu")) {
+            a.cb.ckey[slot] = (uint64_t)(uint32_t)pvu;
+            a.cb.cq[slot] = (int32_t)v;
+            a.cb.crec[slot] = rq;
+            a.rankU[pvu] = j + 1;
+        }
+    }
+#ifdef DM_PEEL_PROF
+    PPROF_T(pt3);
+    if (tid == 0) {
+        const unsigned int e = atomicAdd(&g_pprof_n, 1u);
+        if (e < (1u << 17)) {
+            unsigned long long* o = g_pprof + (size_t)e * 8;
+            o[0] = c; o[1] = y; o[2] = n; o[3] = pt0; o[4] = pt1; o[5] = pt2; o[6] = pt3; o[7] = 0;
+        }
+    }
+#endif
+}
+
+// Launch j: workgroups [0, TAB_NA) search and sort front j, the others peel
+// it (chunk c, slice y; TAB_NA and gx are multiples of 8, so the slices of a
+// chunk land on one XCD).
+template <int F>
+__global__ __launch_bounds__(TAB_NT, DM_PEEL_TAB_MINW) void peel_order_kernel(TabArgs a, int32_t j) {
+    __shared__ __attribute__((aligned(16))) char smem[TabLds<F>::bytes];
+    __shared__ TabScalars sc;
+    if (blockIdx.x < TAB_NA) {
+        if (j >= 1) tab_search<F>(a, j, blockIdx.x, smem, sc);
+        return;
+    }
+    const int64_t t = (int64_t)blockIdx.x - TAB_NA;
+    tab_peel<F>(a, j, t % a.gx, t / a.gx, PEEL_SLICES, smem, sc);
+}
+
+// front 0 (ulist[0, F0), U order): buffer 0's members, its records in mtab,
+// and the state of launches 0 and 1 (workgroup 0, thread 0)
+__global__ void tab_front0_kernel(TabArgs a, const int32_t* F0p, const int64_t* sorted0p) {
+    const int64_t F0 = *F0p;
+    DGRID_LOOP(i, F0) {
+        const int32_t u = a.ulist[i];
+        if (!BD_OK(u, a.U, "tab front 0")) continue;
+        const int32_t q = a.pos[u];
+        const int4 rec = a.qrec[q];
+        a.cb.ckey[i] = (uint64_t)(uint32_t)u;
+        a.cb.cq[i] = q;
+        a.cb.crec[i] = rec;
+        a.mtab[i] = rec;
+    }
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int64_t s0 = *sorted0p;
+    for (int b = 0; b < CAND_BUCKETS; ++b) {
+        *a.cb.count(0, b) = (int32_t)std::max<int64_t>(0, std::min<int64_t>(a.cb.cap, F0 - b * a.cb.cap));
+        *a.cb.pending(0, b) = b == 0 ? (unsigned long long)s0 : 0ull;
+    }
+    FrontStep s{};
+    s.valid = a.epoch;
+    s.done = F0 == 0;
+    a.stf[0] = s;
+    FrontStep s1{};
+    s1.sorted = s0;
+    s1.ustart = (int32_t)F0;
+    s1.Fprev = (int32_t)F0;
+    s1.valid = a.epoch;
+    s1.done = (s0 >= a.N || F0 >= a.U || F0 == 0) ? 1 : 0;
+    a.stf[1] = s1;
+    a.sum->nfronts = 0;
+    a.sum->done = s1.done;
+    a.sum->overflow = 0;
+    a.sum->ncand = 0;
+    a.sum->sorted = s0;
+    a.sum->lastinds = s0;
+    a.fstarts[0] = 0;
+    a.fstarts[1] = (int32_t)F0;
+}
+// A front past the sorting workgroup: its keys (bucket blockIdx.y after the
+// earlier buckets) and slots into keys / vals for a radix sort ...
+__global__ void tab_compact_kernel(TabArgs a, int buf, uint64_t* keys, int32_t* vals) {
+    const int b = blockIdx.y;
+    int32_t pre = 0;
+    for (int k = 0; k < b; ++k) pre += *a.cb.count(buf, k);
+    const int32_t cnt = *a.cb.count(buf, b);
+    const int64_t src = a.cb.base(buf) + b * a.cb.cap;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        keys[pre + i] = a.cb.ckey[src + i];
+        vals[pre + i] = (int32_t)(b * a.cb.cap + i);
+    }
+}
+// ... and written out in that order as front j
+__global__ __launch_bounds__(1024) void tab_presorted_kernel(TabArgs a, int32_t j, const uint64_t* keys,
+                                                             const int32_t* vals) {
+    __shared__ TabScalars sc;
+    if (threadIdx.x == 0) {
+        sc.sf = a.stf[j];
+        tab_cand_list(a.cb, j % 3, sc);
+    }
+    __syncthreads();
+    const int32_t n = sc.n;
+    if (!BD_OK(sc.sf.ustart + (int64_t)n - 1, a.U, "tab presorted end")) return;
+    const int64_t bbase = a.cb.base(j % 3);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        a.ulist[sc.sf.ustart + i] = (int32_t)(uint32_t)keys[i];
+        a.mtab[sc.sf.ustart + i] = a.cb.crec[bbase + vals[i]];
+    }
+    if (threadIdx.x == 0) tab_finish(a, j, n, sc.pend, sc.sf);
+}
+
+// ---------------------------------------------------------------------------
 // host drivers (called from nsga2.hip)
 // ---------------------------------------------------------------------------
 // Workspace of the fast path: the buffers that live from the ranks to the
@@ -1477,11 +2030,32 @@ static size_t ranks_work_bytes(int64_t n, int64_t U) {
            std::max(radix_sort_temp_bytes(n), radix_sort_batched_temp_bytes(3, U)) +
            scan_temp_bytes(e);
 }
-static size_t fronts_work_bytes(int64_t U) {
-    return CAND_PAGE * (CAND_BUCKETS + 1) +
-           align_up((size_t)CAND_BUCKETS * cand_cap(U) * 8, 256) + 2 * align_up((size_t)U * 8, 256) +
-           2 * align_up((size_t)U * 4, 256) + radix_sort_temp_bytes(U);
+// the peel loop's part of the work region: the state page and the three
+// candidate buffers' counter pages, their keys, the overflow sort's buffers
+// (ktmp2 is the D peel's lastq) and the per-front state of the table peel
+struct FrontsWork {
+    size_t pages, ckey, ktmp, ktmp2, vals, vtmp, rtemp, stf, total;
+};
+static FrontsWork fronts_work(int64_t U) {
+    FrontsWork W;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(std::max<size_t>(bytes, 1), 256);
+        return o;
+    };
+    W.pages = take(CAND_PAGE * (1 + 3 * CAND_BUCKETS));
+    W.ckey = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 8);
+    W.ktmp = take((size_t)U * 8);
+    W.ktmp2 = take((size_t)U * 8);
+    W.vals = take((size_t)U * 4);
+    W.vtmp = take((size_t)U * 4);
+    W.rtemp = take(radix_sort_temp_bytes(U));
+    W.stf = take((size_t)(U + 2) * sizeof(FrontStep));
+    W.total = off;
+    return W;
 }
+static size_t fronts_work_bytes(int64_t U) { return fronts_work(U).total; }
 static FastLayout fast_layout(int64_t n, int64_t U) {
     FastLayout L;
     L.NB = (U + 63) / 64;
@@ -1506,9 +2080,9 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
     L.mrow = take((size_t)U * 8);
     L.mtab = take((size_t)U * 16);
     L.qrec = take((size_t)U * 16);
-    L.crec = take((size_t)CAND_BUCKETS * cand_cap(U) * 16);
+    L.crec = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 16);
     L.countq = take((size_t)U * 4);
-    L.cq = take((size_t)CAND_BUCKETS * cand_cap(U) * 4);
+    L.cq = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 4);
     L.work = take(std::max(ranks_work_bytes(n, U), fronts_work_bytes(U)));
     L.total = off;
     return L;
@@ -1526,7 +2100,7 @@ int64_t fast_dom_words(int64_t U) {
 // them read from global memory alike -- and never in the range-checked,
 // workspace-poisoning DM_BD_CHECK build, which printed no out-of-range index;
 // DESIGN.md §8.)  With the bitset pass the peel reads the tables, not a D
-// matrix (peel_tab_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
+// matrix (peel_order_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
 // D peel.
 bool fast_bitset(const dm_ctx* ctx, int m) {
     return m >= 2 && m <= 3 && ctx->dom_path != DM_DOM_COMPARE;
@@ -1631,6 +2205,126 @@ int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, con
     return DM_OK;
 }
 
+// fast_fronts for the bitset tables: one launch per front (peel_order_kernel:
+// the peel of front j beside the search and sort of front j), the status
+// read after each batch.
+static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32_t* F0,
+                           const int64_t* sorted0, int64_t N, const int32_t* gsize, int32_t* ulist,
+                           int32_t* rankU, int32_t* fstarts, char* ws, std::vector<int32_t>& ufront,
+                           int64_t* sorted, int64_t* last_inds) {
+    hipStream_t s = ctx->stream;
+    const FastLayout L = fast_layout(n, U);
+    const FrontsWork W = fronts_work(U);
+    char* p = ws + L.work;
+    const BitdomLayout TL = bitdom_layout(U, m);
+    const char* tws = ws + L.part;
+    DM_CHECK_ARG(U < (1ll << 31) - 1, "more than 2^31 unique fitnesses");
+    TabArgs a;
+    a.P = (const uint32_t*)(tws + TL.P);
+    a.R = (const int32_t*)(tws + TL.R);
+    a.BK = (const uint16_t*)(tws + TL.BK);
+    a.qrec = (const int4*)(ws + L.qrec);
+    a.gsize = gsize;
+    a.sigma = (const int32_t*)(ws + L.sigma);
+    a.pos = (const int32_t*)(ws + L.pos);
+    a.countq = (int32_t*)(ws + L.countq);
+    a.rankU = rankU;
+    a.ulist = ulist;
+    a.fstarts = fstarts;
+    a.mtab = (int4*)(ws + L.mtab);
+    a.gslot = (int32_t*)(p + W.vals);
+    a.gtmp = (int32_t*)(p + W.vtmp);
+    a.stf = (FrontStep*)(p + W.stf);
+    a.sum = (FrontSum*)(p + W.pages);
+    a.cb.pages = p + W.pages + CAND_PAGE;
+    a.cb.ckey = (uint64_t*)(p + W.ckey);
+    a.cb.cq = (int32_t*)(ws + L.cq);
+    a.cb.crec = (int4*)(ws + L.crec);
+    a.cb.cap = cand_cap(U);
+    a.U = U;
+    a.N = N;
+    a.gx = (TL.NG + 7) & ~7ll;
+    static std::atomic<uint32_t> epochs{0};
+    do {
+        a.epoch = ++epochs;
+    } while (a.epoch == 0);
+    DM_HIP(hipMemsetAsync(p + W.pages, 0, CAND_PAGE * (1 + 3 * CAND_BUCKETS), s));
+    member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
+                                             (const int32_t*)(ws + L.nseg), U, (int4*)(ws + L.qrec),
+                                             nullptr);
+    tab_front0_kernel<<<dg1(U), 256, 0, s>>>(a, F0, sorted0);
+    char* hbuf = (char*)pinned(ctx, 2048);
+    if (!hbuf) return DM_ERR_NOMEM;
+    FrontSum* hsum = (FrontSum*)hbuf;
+    int32_t* hfs = (int32_t*)(hbuf + 256);
+    const int64_t npre = std::min<int64_t>((2048 - 256) / 4, U + 2);
+    // as fast_fronts: the first batch from the previous call's front count
+    // and its trend; launch j orders front j, so the fronts up to J take J+1
+    constexpr int PEEL_BATCH_MAX = 96;
+    const bool hinted = 4 * U >= 3 * ctx->peel_hint_U && 3 * U <= 4 * ctx->peel_hint_U &&
+                        N == ctx->peel_hint_N;
+    const int hint = hinted ? ctx->peel_hint : 4;
+    const int trend = hinted ? std::max(0, std::min(ctx->peel_trend, 4)) : 0;
+    int batch = std::max(2, std::min(hint + 1 + trend, PEEL_BATCH_MAX));
+    const unsigned grid = (unsigned)(TAB_NA + a.gx * PEEL_SLICES);
+    int32_t j = 0;  // the next launch's front
+    for (;;) {
+        for (int b = 0; b < batch; ++b) {
+            timing_begin(ctx, DM_TIME_PEEL);
+            if (m == 2)
+                peel_order_kernel<1><<<grid, TAB_NT, 0, s>>>(a, j + b);
+            else
+                peel_order_kernel<2><<<grid, TAB_NT, 0, s>>>(a, j + b);
+            timing_end(ctx, DM_TIME_PEEL);
+        }
+        DM_LAUNCH_CHECK();
+        DM_HIP(hipMemcpyAsync(hsum, a.sum, sizeof(FrontSum), hipMemcpyDeviceToHost, s));
+        DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+        if (hsum->done) break;
+        if (hsum->overflow) {
+            // front js has more members than the sorting workgroup holds:
+            // the radix sort orders their (final) keys
+            const int32_t js = hsum->nfronts + 1, nc = hsum->ncand;
+            uint64_t* ktmp = (uint64_t*)(p + W.ktmp);
+            uint64_t* ktmp2 = (uint64_t*)(p + W.ktmp2);
+            int32_t* vals = (int32_t*)(p + W.vals);
+            int32_t* vtmp = (int32_t*)(p + W.vtmp);
+            tab_compact_kernel<<<dim3((unsigned)((a.cb.cap + 255) / 256), CAND_BUCKETS), 256, 0, s>>>(
+                a, js % 3, ktmp, vals);
+            int rc = radix_sort_pairs(s, ktmp, vals, ktmp2, vtmp, nc, 0, 64, p + W.rtemp);
+            if (rc) return rc;
+            tab_presorted_kernel<<<1, 1024, 0, s>>>(a, js, ktmp, vals);
+            DM_LAUNCH_CHECK();
+            j = js + 1;
+        } else {
+            j += batch;
+        }
+        // the next batch from what is left (as fast_fronts)
+        const double mean = (double)hsum->sorted / (double)(hsum->nfronts + 1);
+        const double per = std::max(mean, (double)hsum->lastinds);
+        const double left = (double)(N - hsum->sorted);
+        int need = per > 0 ? (int)std::ceil(left / per) : 32;
+        if (hint > hsum->nfronts) need = std::min(need, hint - hsum->nfronts + 1);
+        batch = std::max(2, std::min(need + 2, PEEL_BATCH_MAX));
+    }
+    const int32_t nf = hsum->nfronts + 1;
+    ctx->peel_trend = hinted ? hsum->nfronts - ctx->peel_hint : 0;
+    ctx->peel_hint = hsum->nfronts;
+    ctx->peel_hint_U = U;
+    ctx->peel_hint_N = N;
+    ufront.resize(nf + 1);
+    if (nf + 1 <= npre) {
+        std::copy(hfs, hfs + nf + 1, ufront.begin());
+    } else {
+        DM_HIP(hipMemcpyAsync(ufront.data(), fstarts, (size_t)(nf + 1) * 4, hipMemcpyDeviceToHost, s));
+        DM_HIP(hipStreamSynchronize(s));
+    }
+    *sorted = hsum->sorted;
+    *last_inds = hsum->lastinds;
+    return DM_OK;
+}
+
 // Fronts 1.. after front 0 (ulist[0, *F0), rankU set): peel on the device,
 // checking the status every few fronts.  F0 and sorted0 (front 0's unique
 // fitnesses and individuals) stay on the device.  Fills ufront (front starts
@@ -1649,36 +2343,23 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     int2* mrow = (int2*)(ws + L.mrow);
     int32_t* countq = (int32_t*)(ws + L.countq);
     int32_t* cq = (int32_t*)(ws + L.cq);
+    if (fast_table_peel(ctx, m))
+        return fast_fronts_tab(ctx, m, n, U, F0, sorted0, N, gsize, ulist, rankU, fstarts, ws,
+                               ufront, sorted, last_inds);
     char* p = ws + L.work;
-    FrontState* st = (FrontState*)p;  // + the eight candidate-bucket pages
-    p += CAND_PAGE * (CAND_BUCKETS + 1);
-    uint64_t* ckey = (uint64_t*)p;
-    p += align_up((size_t)CAND_BUCKETS * cand_cap(U) * 8, 256);
-    uint64_t* ktmp = (uint64_t*)p;
-    p += align_up((size_t)U * 8, 256);
-    int32_t* vals = (int32_t*)p;
-    p += align_up((size_t)U * 4, 256);
-    int32_t* vtmp = (int32_t*)p;
-    p += align_up((size_t)U * 4, 256);
+    const FrontsWork W = fronts_work(U);
+    FrontState* st = (FrontState*)(p + W.pages);  // + the eight candidate-bucket pages
+    uint64_t* ckey = (uint64_t*)(p + W.ckey);
+    uint64_t* ktmp = (uint64_t*)(p + W.ktmp);
+    int32_t* vals = (int32_t*)(p + W.vals);
+    int32_t* vtmp = (int32_t*)(p + W.vtmp);
     // sliced peels: per v the max (front + 1, last releasing position)
-    unsigned long long* lastq = (unsigned long long*)p;
-    p += align_up((size_t)U * 8, 256);
-    void* rtemp = p;
+    unsigned long long* lastq = (unsigned long long*)(p + W.ktmp2);
+    void* rtemp = p + W.rtemp;
     front_init_kernel<<<CAND_BUCKETS + 1, 256, 0, s>>>(st, F0, sorted0, N, U, fstarts);
-    // table-fed peel: the bitset pass's tables in the part region
-    const bool tab = fast_table_peel(ctx, m);
-    const BitdomLayout TL = bitdom_layout(U, m);
-    const char* tws = ws + L.part;
-    int4* mtab = (int4*)(ws + L.mtab);
-    int4* qrec = (int4*)(ws + L.qrec);
-    int4* crec = (int4*)(ws + L.crec);
-    if (tab)
-        member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
-                                                 nseg, U, qrec, lastq);
-    else
-        DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
-    const MemberTab mt{tab ? mtab : nullptr, qrec, crec};
-    const CandRec cr{qrec, crec};
+    DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
+    // the D peel reads member rows (mrow), which its ordering writes
+    const MemberTab mt{nullptr, nullptr, nullptr};
     member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow, mt);
     // status word and the first front starts come back together: when the
     // peel is done they are usually all that is needed (one round trip)
@@ -1702,25 +2383,10 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     int batch = std::max(2, std::min(hint + 1 + trend, PEEL_BATCH_MAX));
     for (;;) {
         for (int b = 0; b < batch; ++b) {
-            if (tab) {
-                const dim3 g((unsigned)((TL.NG + 7) & ~7ll), PEEL_SLICES);
-                const uint32_t* P = (const uint32_t*)(tws + TL.P);
-                const int32_t* R = (const int32_t*)(tws + TL.R);
-                const uint16_t* BK = (const uint16_t*)(tws + TL.BK);
-                timing_begin(ctx, DM_TIME_PEEL);
-                if (m == 2)
-                    peel_tab_kernel<1><<<g, PEEL_WAVES * 64, 0, s>>>(P, R, BK, mtab, gsize, sigma,
-                                                                     st, countq, lastq, ckey, cq, rankU, cr);
-                else
-                    peel_tab_kernel<2><<<g, PEEL_WAVES * 64, 0, s>>>(P, R, BK, mtab, gsize, sigma,
-                                                                     st, countq, lastq, ckey, cq, rankU, cr);
-                timing_end(ctx, DM_TIME_PEEL);
-            } else {
-                timing_begin(ctx, DM_TIME_PEEL);
-                peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
-                    D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
-                timing_end(ctx, DM_TIME_PEEL);
-            }
+            timing_begin(ctx, DM_TIME_PEEL);
+            peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
+                D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
+            timing_end(ctx, DM_TIME_PEEL);
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0, mt);
         }
         DM_LAUNCH_CHECK();

@@ -3,7 +3,7 @@
 counter-collection CSV (not a test; run on the GPU box after
 ``rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -- python
 bench.py --config c5 ...``).  Selection boundaries are the count-pass
-dispatches (one bd_count_kernel per selNSGA2); the peel_tab_kernel dispatches
+dispatches (one bd_count_kernel per selNSGA2); the peel_order_kernel dispatches
 between two of them belong to one selection.  Writes the median selection's
 sums as profiles/c5_peel_pmc.json (bench.py's C5 roofline reads it).
 
@@ -34,14 +34,14 @@ def main():
         if "bd_count_kernel" in name:
             cur = defaultdict(float)
             sels.append(cur)
-        elif "peel_tab_kernel" in name and cur is not None:
+        elif "peel_order_kernel" in name and cur is not None:
             for c, v in disp[k].items():
                 if c != "name":
                     cur[c] += v
             cur["launches"] += 1
     sels = [s for s in sels if s.get("launches")]
     med = sorted(sels, key=lambda s: s["SQ_INSTS_VALU"])[len(sels) // 2]
-    res = {"kernel": "peel_tab_kernel<2>", "selections": len(sels),
+    res = {"kernel": "peel_order_kernel<2>", "selections": len(sels),
            "SQ_INSTS_VALU_per_selection": med["SQ_INSTS_VALU"],
            "SQ_WAVE_CYCLES_per_selection": med.get("SQ_WAVE_CYCLES"),
            "SQ_ACTIVE_INST_VALU_per_selection": med.get("SQ_ACTIVE_INST_VALU"),
