@@ -1351,7 +1351,8 @@ struct TabArgs {
     int32_t* fstarts;
     int4* mtab;  // [U] member records in front order: front j at [ustart_j, ustart_j + n_j)
     int32_t* gslot;  // [U] a large front's members' places in their bins (tab_sort_big)
-    int32_t* gtmp;   // [U] ... and its U indices binned
+    int32_t* gtmp;   // [U] ... its U indices binned
+    uint64_t* gkey;  // [U] ... and its keys
     FrontStep* stf;
     FrontSum* sum;
     CandBufs cb;
@@ -1524,13 +1525,30 @@ constexpr int TAB_BIG_BIN_MAX = 512;
 template <int NT>
 __device__ bool tab_sort_big(const TabArgs& a, int64_t bbase, const CandMap& cm, int32_t n,
                              int32_t Fr, int32_t ustart, int32_t* base, TabScalars& sc) {
+    // the keys are read coherently once (the search workgroups stored them)
+    // into the workgroup's own scratch (plain accesses from here on: one
+    // workgroup, ordered by its barriers), four members per thread in flight
+    constexpr int B = 4;
     const int tid = threadIdx.x;
     for (int i = tid; i <= Fr; i += NT) base[i] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += NT) {
-        int32_t l = (int32_t)(cld<true>(a.cb.ckey + bbase + cm.slot(i)) >> 32);
-        if (!BD_OK(l, Fr, "tab big bin")) l = 0;
-        cst<true>(a.gslot + i, atomicAdd(&base[l], 1));
+    for (int i0 = tid; i0 < n; i0 += B * NT) {
+        uint64_t k[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * NT;
+            k[b] = i < n ? cld<true>(a.cb.ckey + bbase + cm.slot(i)) : 0;
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * NT;
+            if (i < n) {
+                int32_t l = (int32_t)(k[b] >> 32);
+                if (!BD_OK(l, Fr, "tab big bin")) l = 0;
+                a.gkey[i] = k[b];
+                a.gslot[i] = atomicAdd(&base[l], 1);
+            }
+        }
     }
     __syncthreads();
     const int C = (Fr + NT - 1) / NT;
@@ -1551,22 +1569,39 @@ __device__ bool tab_sort_big(const TabArgs& a, int64_t bbase, const CandMap& cm,
     if (tid == 0) base[Fr] = n;
     __syncthreads();
     if (sc.smax != 0) return false;
-    for (int i = tid; i < n; i += NT) {
-        const uint64_t k = cld<true>(a.cb.ckey + bbase + cm.slot(i));
-        const int32_t l = (int32_t)(k >> 32);
-        cst<true>(a.gtmp + base[l] + cld<true>(a.gslot + i), (int32_t)(uint32_t)k);
+    for (int i0 = tid; i0 < n; i0 += B * NT) {
+        uint64_t k[B];
+        int32_t g[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * NT;
+            k[b] = i < n ? a.gkey[i] : 0;
+            g[b] = i < n ? a.gslot[i] : 0;
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (i0 + b * NT < n) a.gtmp[base[(int32_t)(k[b] >> 32)] + g[b]] = (int32_t)(uint32_t)k[b];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int i = tid; i < n; i += NT) {
-        const int64_t sl = bbase + cm.slot(i);
-        const uint64_t k = cld<true>(a.cb.ckey + sl);
-        const int32_t l = (int32_t)(k >> 32), vu = (int32_t)(uint32_t)k;
-        const int32_t beg = base[l], end = base[l + 1];
-        int32_t r = beg;
-        for (int32_t q = beg; q < end; ++q) r += cld<true>(a.gtmp + q) < vu ? 1 : 0;
-        a.ulist[ustart + r] = vu;
-        a.mtab[ustart + r] = a.cb.crec[sl];
+    for (int i0 = tid; i0 < n; i0 += B * NT) {
+        uint64_t k[B];
+        int4 rec[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = i0 + b * NT;
+            k[b] = i < n ? a.gkey[i] : 0;
+            rec[b] = i < n ? a.cb.crec[bbase + cm.slot(i)] : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (i0 + b * NT >= n) continue;
+            const int32_t l = (int32_t)(k[b] >> 32), vu = (int32_t)(uint32_t)k[b];
+            const int32_t beg = base[l], end = base[l + 1];
+            int32_t r = beg;
+            for (int32_t q = beg; q < end; ++q) r += a.gtmp[q] < vu ? 1 : 0;
+            a.ulist[ustart + r] = vu;
+            a.mtab[ustart + r] = rec[b];
+        }
     }
     return true;
 }
@@ -2234,6 +2269,7 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
     a.mtab = (int4*)(ws + L.mtab);
     a.gslot = (int32_t*)(p + W.vals);
     a.gtmp = (int32_t*)(p + W.vtmp);
+    a.gkey = (uint64_t*)(p + W.ktmp2);
     a.stf = (FrontStep*)(p + W.stf);
     a.sum = (FrontSum*)(p + W.pages);
     a.cb.pages = p + W.pages + CAND_PAGE;
