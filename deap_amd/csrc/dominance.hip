@@ -673,29 +673,12 @@ struct PeelSmallT {
 typedef PeelLdsT<PEEL_PV> PeelLds;
 typedef PeelSmallT<PEEL_PV> PeelSmall;
 
-// Per-v values a peel kernel may load in its prologue, long before the
-// release needs them (the release's chain countq -> sigma -> gsize is then
-// three dependent loads shorter): the count, the U index and the individual
-// count of each v of the thread.
-template <int IT>
-struct PeelPre {
-    int32_t cnt[IT], vu[IT], gs[IT];
-};
-// The table peel's member records (MemberTab): a released v's record qrec[v]
-// is copied to crec[slot] beside its candidate key, so that the ordering
-// reads it in slot order with the key instead of gathering it by q.
-struct CandRec {
-    const int4* qrec;
-    int4* crec;
-};
 template <bool COH, int PW>
 __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW], int64_t vbase,
                              const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
-                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
-                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre = nullptr,
-                             CandRec cr = CandRec{nullptr, nullptr});
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S);
 
 // Slice y of the nsl slices of row segment s for the front of sF unique
 // fitnesses starting at sust in ulist / mrow (front number snf).
@@ -785,8 +768,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
                              const int32_t* __restrict__ gsize, const int32_t* __restrict__ sigma,
                              FrontState* st, int32_t* countq, unsigned long long* lastq,
                              uint64_t* ckey, int32_t* cq, int32_t* rankU, int64_t U, int32_t snf,
-                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S,
-                             const PeelPre<PeelSmallT<PW * 64>::IT>* pre, CandRec cr) {
+                             int64_t nsl, PeelLdsT<PW * 64>& L, PeelSmallT<PW * 64>& S) {
     constexpr int PEEL_IT = PeelSmallT<PW * 64>::IT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -800,7 +782,6 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
     // waves on the large fronts)
     bool fresh[PEEL_IT];
     int32_t lk[PEEL_IT], vu[PEEL_IT];
-    int4 rq[PEEL_IT];
     unsigned long long fm[PEEL_IT];
 #pragma unroll
     for (int it = 0; it < PEEL_IT; ++it) {
@@ -815,7 +796,7 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         fresh[it] = false;
         if (v < U && d > 0) {
             if (nsl == 1) {
-                const int32_t left = (pre ? pre->cnt[it] : cld<COH>(countq + v)) - d;
+                const int32_t left = cld<COH>(countq + v) - d;
                 cst<COH>(countq + v, left);
                 fresh[it] = left == 0;
             } else {
@@ -836,11 +817,9 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
             }
         }
         lk[it] = l;
-        // in flight across the slot reservation below (barriers wait on LDS only)
-        if (cr.crec && fresh[it]) rq[it] = cr.qrec[v];
-        vu[it] = fresh[it] ? (pre ? pre->vu[it] : sigma[v]) : 0;
+        vu[it] = fresh[it] ? sigma[v] : 0;
         fm[it] = __ballot(fresh[it]);
-        int64_t gs = fresh[it] ? (pre ? pre->gs[it] : gsize[vu[it]]) : 0;
+        int64_t gs = fresh[it] ? gsize[vu[it]] : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) gs += __shfl_xor(gs, o, 64);
         if (lane == 0) {
@@ -872,7 +851,6 @@ __device__ void peel_release(const int32_t (&dec)[PW], const int32_t (&last)[PW]
         if (!BD_OK(slot, CAND_BUCKETS * cand_cap(U), "release slot") || !BD_OK(vu[it], U, "release vu")) continue;
         cst<COH>(ckey + slot, ((uint64_t)(uint32_t)lk[it] << 32) | (uint32_t)vu[it]);
         cst<COH>(cq + slot, (int32_t)v);
-        if (cr.crec) cr.crec[slot] = rq[it];
         cst<COH>(rankU + vu[it], snf + 1);
     }
     __syncthreads();  // the LDS is reused by the caller's next task
@@ -927,15 +905,6 @@ __device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const 
     const int32_t r = pos[u];
     return make_int2(r, nseg[r / (64 * TD_WPW)]);
 }
-// What the table-fed peel needs of a member -- (reach, last q of its
-// objective-0 tie group, ranks of objectives 1 and 2) -- built per q once per
-// selection (member_rec_kernel) and copied into front order by the ordering,
-// instead of gathered from three arrays by every chunk's workgroup.
-struct MemberTab {
-    int4* out;          // [U] records in front order (null: the D peel, which reads mrow)
-    const int4* qrec;   // [U] records in q order
-    const int4* crec;   // the candidates' records in slot order (peel_release)
-};
 __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t* nseg, int64_t U,
                                   int4* qrec, unsigned long long* lastq) {
     DGRID_LOOP(q, U) {
@@ -948,7 +917,7 @@ __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t
 template <int NT, int E, bool COH>
 __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2* mout,
                              const int32_t* pos, const int32_t* nseg, uint64_t* lds,
-                             const MemberTab& mt, int4* tout, const CandMap& cm) {
+                             const CandMap& cm) {
     uint64_t k[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -962,11 +931,7 @@ __device__ void order_sorted(const uint64_t* ckey, int32_t n, int32_t* out, int2
         if (i < n) {
             const int32_t u = (int32_t)(uint32_t)k[e];
             cst<COH>(out + i, u);
-            if (tout) {
-                tout[i] = mt.qrec[pos[u]];
-            } else {
-                cst2<COH>(mout + i, member_row(u, pos, nseg));
-            }
+            cst2<COH>(mout + i, member_row(u, pos, nseg));
         }
     }
 }
@@ -1030,7 +995,7 @@ __device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* sh) {
 // registers (and scratch spills) of the 16-slot form.
 template <int NT, int E, int CAP, bool COH>
 __device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* out, int2* mout,
-                            int4* tout, const int32_t* nseg, const MemberTab& mt,
+                            const int32_t* nseg,
                             const CandMap& cm, int32_t n, int32_t Fr, OrderLds<CAP>& lds,
                             int32_t* part, OrderScalars& sc) {
     const int tid = threadIdx.x;
@@ -1039,11 +1004,6 @@ __device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* ou
     __syncthreads();
     uint64_t key[E];
     int32_t qv[E], slot[E];
-    // the first PF candidates' records (slot order, beside the keys) are
-    // fetched here, in flight across the binning's barriers (they wait
-    // on LDS only)
-    constexpr int PF = E < 4 ? E : 4;
-    int4 rec[PF];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = tid + e * NT;
@@ -1051,7 +1011,6 @@ __device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* ou
             const int64_t sl = cm.slot(i);
             key[e] = cld<COH>(ckey + sl);
             qv[e] = cld<COH>(cq + sl);
-            if (e < PF && tout) rec[e] = mt.crec[sl];
         }
     }
 #pragma unroll
@@ -1085,7 +1044,7 @@ __device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* ou
             if (i < n) lds.cs.tmp[lds.cs.base[(int32_t)(key[e] >> 32)] + slot[e]] = (int32_t)(uint32_t)key[e];
         }
         __syncthreads();
-        // ranks first, then the record copies as one batch of loads
+        // ranks first, then the member rows
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int i = tid + e * NT;
@@ -1101,12 +1060,7 @@ __device__ bool order_count(const uint64_t* ckey, const int32_t* cq, int32_t* ou
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int i = tid + e * NT;
-            if (i < n) {
-                if (tout)
-                    tout[slot[e]] = e < PF ? rec[e] : mt.crec[cm.slot(i)];
-                else
-                    cst2<COH>(mout + slot[e], make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
-            }
+            if (i < n) cst2<COH>(mout + slot[e], make_int2(qv[e], nseg[qv[e] / (64 * TD_WPW)]));
         }
         sorted_here = true;
     }
@@ -1118,7 +1072,7 @@ template <int NT, int CAP, bool COH>
 __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t* cq,
                             int32_t* ulist, int2* mrow, const int32_t* pos, const int32_t* nseg,
                             int32_t* fstarts, int presorted, OrderLds<CAP>& lds, int32_t* part,
-                            OrderScalars& sc, const MemberTab& mt) {
+                            OrderScalars& sc) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         const int32_t done = cld<COH>(&st->done), ovf = cld<COH>(&st->overflow);
@@ -1158,44 +1112,39 @@ __device__ void order_front(FrontState* st, const uint64_t* ckey, const int32_t*
     }
     int32_t* out = ulist + sc.snstart;
     int2* mout = mrow + sc.snstart;
-    int4* tout = mt.out ? mt.out + sc.snstart : nullptr;
     bool sorted_here = false;
     if (presorted) {
         for (int i = tid; i < n; i += NT) {
             const int32_t u = (int32_t)(uint32_t)cld<COH>(ckey + i);
             cst<COH>(out + i, u);
-            if (tout) {
-                tout[i] = mt.qrec[pos[u]];
-            } else {
-                cst2<COH>(mout + i, member_row(u, pos, nseg));
-            }
+            cst2<COH>(mout + i, member_row(u, pos, nseg));
         }
         sorted_here = true;
     } else if (sc.sF <= CAP) {
         // slots per thread for this front: 4 covers the C5 fronts (< 4,096)
         if (n <= 4 * NT)
-            sorted_here = order_count<NT, 4, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt, cm, n,
+            sorted_here = order_count<NT, 4, CAP, COH>(ckey, cq, out, mout, nseg, cm, n,
                                                        sc.sF, lds, part, sc);
         else if (n <= 8 * NT)
-            sorted_here = order_count<NT, 8, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt, cm, n,
+            sorted_here = order_count<NT, 8, CAP, COH>(ckey, cq, out, mout, nseg, cm, n,
                                                        sc.sF, lds, part, sc);
         else
-            sorted_here = order_count<NT, CAP / NT, CAP, COH>(ckey, cq, out, mout, tout, nseg, mt,
+            sorted_here = order_count<NT, CAP / NT, CAP, COH>(ckey, cq, out, mout, nseg,
                                                               cm, n, sc.sF, lds, part, sc);
     }
     if (!sorted_here) {
         uint64_t* keys = lds.keys;
         if (n <= NT) {
-            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
+            order_sorted<NT, 1, COH>(ckey, n, out, mout, pos, nseg, keys, cm);
         } else if (n <= 2 * NT) {
-            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
+            order_sorted<NT, 2, COH>(ckey, n, out, mout, pos, nseg, keys, cm);
         } else if (n <= 4 * NT) {
-            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
+            order_sorted<NT, 4, COH>(ckey, n, out, mout, pos, nseg, keys, cm);
         } else if (n <= 8 * NT) {
-            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
+            order_sorted<NT, 8, COH>(ckey, n, out, mout, pos, nseg, keys, cm);
         } else {
             static_assert(CAP <= 16 * NT, "order capacity exceeds the bitonic sizes");
-            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys, mt, tout, cm);
+            order_sorted<NT, 16, COH>(ckey, n, out, mout, pos, nseg, keys, cm);
         }
     }
     if (tid == 0) {
@@ -1224,12 +1173,12 @@ __global__ __launch_bounds__(1024) void front_order_kernel(FrontState* st, const
                                                            const int32_t* cq, int32_t* ulist,
                                                            int2* mrow, const int32_t* pos,
                                                            const int32_t* nseg, int32_t* fstarts,
-                                                           int presorted, MemberTab mt) {
+                                                           int presorted) {
     __shared__ OrderLds<ORDER_CAP> lds;
     __shared__ int32_t part[1024];
     __shared__ OrderScalars sc;
     order_front<1024, ORDER_CAP, false>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, presorted,
-                                        lds, part, sc, mt);
+                                        lds, part, sc);
 }
 
 // The overflow path's compaction: bucket blockIdx.y's candidates to
@@ -1246,13 +1195,10 @@ __global__ void cand_compact_kernel(FrontState* st, const uint64_t* ckey, int64_
 }
 
 __global__ void member_rows_kernel(const int32_t* ulist, const int32_t* Fp, const int32_t* pos,
-                                   const int32_t* nseg, int2* mrow, MemberTab mt) {
+                                   const int32_t* nseg, int2* mrow) {
     const int64_t F = *Fp;
     DGRID_LOOP(j, F) {
-        if (mt.out)
-            mt.out[j] = mt.qrec[pos[ulist[j]]];
-        else
-            mrow[j] = member_row(ulist[j], pos, nseg);
+        mrow[j] = member_row(ulist[j], pos, nseg);
     }
 }
 
@@ -2395,8 +2341,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     front_init_kernel<<<CAND_BUCKETS + 1, 256, 0, s>>>(st, F0, sorted0, N, U, fstarts);
     DM_HIP(hipMemsetAsync(lastq, 0, (size_t)U * 8, s));
     // the D peel reads member rows (mrow), which its ordering writes
-    const MemberTab mt{nullptr, nullptr, nullptr};
-    member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow, mt);
+    member_rows_kernel<<<dg1(U), 256, 0, s>>>(ulist, F0, pos, nseg, mrow);
     // status word and the first front starts come back together: when the
     // peel is done they are usually all that is needed (one round trip)
     char* hbuf = (char*)pinned(ctx, 2048);
@@ -2423,7 +2368,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
             peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
                 D, L.NQ, mrow, gsize, sigma, st, countq, lastq, ckey, cq, rankU);
             timing_end(ctx, DM_TIME_PEEL);
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0, mt);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
         }
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
@@ -2441,7 +2386,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
             int rc = radix_sort_pairs(s, ktmp, vals, ckey, vtmp, nc, 0, 64, rtemp);
             if (rc) return rc;
             DM_HIP(hipMemcpyAsync(ckey, ktmp, (size_t)nc * 8, hipMemcpyDeviceToDevice, s));
-            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1, mt);
+            front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 1);
             DM_LAUNCH_CHECK();
         }
         // next batch from what is left: fronts grow along the peel, so the
