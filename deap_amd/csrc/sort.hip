@@ -61,7 +61,8 @@ constexpr uint32_t RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_COUNT = (1u << 30
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     const uint64_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
     uint64_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t seglen, int64_t tps,
-    int shift, const int32_t* __restrict__ ghist, uint32_t* status, uint32_t* ticket) {
+    int shift, const int32_t* __restrict__ ghist, uint32_t* status, uint32_t* ticket,
+    const uint8_t* __restrict__ dig = nullptr) {
     __shared__ int32_t cnt[RS_ROUNDS][RS_THREADS / 64][RS_BINS];
     __shared__ int32_t gofs[RS_BINS];
     __shared__ uint32_t tile_id;
@@ -93,7 +94,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
         const bool ok = i < n;
         k[r] = ok ? keys_in[i] : 0;
         v[r] = ok ? vals_in[i] : 0;
-        d[r] = ok ? (int)((k[r] >> shift) & 0xFF) : -1;
+        // dig (sample sort): the digit is the key's bucket, stored by ss_classify_kernel
+        d[r] = ok ? (dig ? (int)dig[i] : (int)((k[r] >> shift) & 0xFF)) : -1;
     }
 #pragma unroll
     for (int r = 0; r < RS_ROUNDS; ++r) {
@@ -156,6 +158,348 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small and mid-size sorts.  The one-sweep pass above costs a launch per 8-bit
+// digit whatever n is, and at the sizes NSGA-II sorts (a last front of a few
+// thousand, 2^18 objective values) a pass is latency, not bytes: 17-21 us per
+// pass of 2^18 keys, 8 passes per 64-bit key (profiles/r05fin4).
+//  - seglen <= LS_CAP: one workgroup per segment sorts the pairs in LDS
+//    (lds_radix below) -- one launch.
+//  - seglen <= SS_MAX and more than SS_MIN_PASSES digits: sample sort.  255
+//    splitters per segment from a sorted jittered-regular sample of (key
+//    bits, position) pairs; a classify pass stores each key's bucket byte and
+//    histograms the buckets; ONE one-sweep pass (rs_pass_kernel on the bytes)
+//    scatters the pairs into bucket order, stably; one workgroup per bucket
+//    sorts it in LDS, stably (lds_radix).  The splitters
+//    carry the position, so equal keys spread over buckets and every pair is
+//    distinct: the result is exactly the stable order.  A bucket larger than
+//    LS_CAP (a sample that missed a cluster) is sorted by a workgroup-local
+//    LSD radix sort through global memory instead: slower, same result.
+// Five launches (memset, splitters, classify, scatter, buckets) instead of ten.
+// ---------------------------------------------------------------------------
+constexpr int LS_THREADS = 1024;
+constexpr int LS_WAVES = LS_THREADS / 64;
+constexpr int LS_CAP = 4096;       // pairs one workgroup sorts in LDS
+constexpr int SS_SAMPLE = 4096;    // sample per segment (16 per bucket)
+constexpr int SS_BUCKETS = 256;    // = RS_BINS: the bucket is the scatter digit
+constexpr int64_t SS_MAX = 1 << 19;
+constexpr int SS_MIN_PASSES = 5;
+static_assert(SS_SAMPLE <= LS_CAP, "the sample is sorted in LDS");
+
+// the bits [begin, begin + width) of a key that the sort compares
+template <bool FULL>
+__device__ __forceinline__ uint64_t kbits(uint64_t k, int begin, uint64_t mask) {
+    return FULL ? k : (k >> begin) & mask;
+}
+
+// A workgroup's LSD radix sort in LDS: n <= LS_CAP (key, index) pairs in
+// k[0] / i[0], 8-bit digits.  Wave w owns the contiguous elements [w chunk,
+// (w + 1) chunk) in rounds of 64; a digit's rank inside a round is a ballot
+// match over the 8 bit planes (as in rs_pass_kernel) plus the wave's running
+// count of that digit; one thread per digit turns the per-wave counts into
+// offsets; the scatter goes to the other buffer.  Stable, ~5 barriers per
+// digit.  (A bitonic network over the same LDS arrays ran 52-104 us for
+// 4,096 pairs -- 78 stages of LDS-bandwidth-bound compare-exchanges; r05_ssort.)
+struct LdsRadix {
+    uint64_t k[2][LS_CAP];
+    uint32_t i[2][LS_CAP];
+    int32_t wc[LS_WAVES][RS_BINS];  // per-wave digit counts -> offsets
+    int32_t wsum[LS_WAVES];
+    int32_t same;                   // the pass's digit is one value: no scatter
+};
+
+// returns the buffer (0 or 1) holding the sorted pairs
+template <bool FULL>
+__device__ __forceinline__ int lds_radix(LdsRadix& L, int n, int begin, uint64_t mask, int passes) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int chunk = (n + LS_THREADS - 1) / LS_THREADS * 64;  // per wave, whole rounds
+    const int rounds = chunk / 64;                             // <= LS_CAP / LS_THREADS
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int cur = 0;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        for (int q = lane; q < RS_BINS; q += 64) L.wc[wave][q] = 0;
+        if (tid == 0) L.same = 0;
+        uint64_t kk[LS_CAP / LS_THREADS];
+        uint32_t ii[LS_CAP / LS_THREADS];
+        int dd[LS_CAP / LS_THREADS], rr[LS_CAP / LS_THREADS];
+#pragma unroll
+        for (int r = 0; r < LS_CAP / LS_THREADS; ++r) {
+            dd[r] = -1;
+            if (r < rounds) {  // wave-uniform
+                const int e = wave * chunk + r * 64 + lane;
+                const bool ok = e < n;
+                kk[r] = ok ? L.k[cur][e] : 0;
+                ii[r] = ok ? L.i[cur][e] : 0;
+                const int d = ok ? (int)((kbits<FULL>(kk[r], begin, mask) >> shift) & 0xFF) : -1;
+                uint64_t same = __ballot(ok);
+#pragma unroll
+                for (int bit = 0; bit < 8; ++bit) {
+                    const uint64_t plane = __ballot(ok && ((d >> bit) & 1));
+                    same &= ((d >> bit) & 1) ? plane : ~plane;
+                }
+                const int rk = __popcll(same & below);
+                // in-order LDS within the wave: every lane reads the running
+                // count before the digit's first lane advances it
+                const int base = ok ? L.wc[wave][d] : 0;
+                if (ok && rk == 0) L.wc[wave][d] = base + __popcll(same);
+                dd[r] = d;
+                rr[r] = base + rk;
+            }
+        }
+        __syncthreads();
+        int32_t tot = 0;
+        if (tid < RS_BINS)
+#pragma unroll
+            for (int w = 0; w < LS_WAVES; ++w) {
+                const int32_t c = L.wc[w][tid];
+                L.wc[w][tid] = tot;
+                tot += c;
+            }
+        const int32_t ex = block_incl_scan<LS_THREADS, false>(tid < RS_BINS ? tot : 0, L.wsum) - tot;
+        if (tid < RS_BINS) {
+#pragma unroll
+            for (int w = 0; w < LS_WAVES; ++w) L.wc[w][tid] += ex;
+            if (tot == n) L.same = 1;
+        }
+        __syncthreads();
+        if (!L.same) {  // workgroup-uniform
+#pragma unroll
+            for (int r = 0; r < LS_CAP / LS_THREADS; ++r)
+                if (dd[r] >= 0) {
+                    const int pos = L.wc[wave][dd[r]] + rr[r];
+                    L.k[cur ^ 1][pos] = kk[r];
+                    L.i[cur ^ 1][pos] = ii[r];
+                }
+            cur ^= 1;
+        }
+        __syncthreads();
+    }
+    return cur;
+}
+
+// one workgroup per segment of seglen <= LS_CAP, sorted in place
+template <bool FULL>
+__global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restrict__ keys,
+                                                             int32_t* __restrict__ vals,
+                                                             int64_t seglen, int begin,
+                                                             uint64_t mask, int passes) {
+    __shared__ LdsRadix L;
+    __shared__ int32_t sv[LS_CAP];
+    const int64_t base = (int64_t)blockIdx.x * seglen;
+    const int n = (int)seglen;
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        L.k[0][i] = keys[base + i];
+        L.i[0][i] = (uint32_t)i;
+        sv[i] = vals[base + i];
+    }
+    __syncthreads();
+    const int c = lds_radix<FULL>(L, n, begin, mask, passes);
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        keys[base + i] = L.k[c][i];
+        vals[base + i] = sv[L.i[c][i]];
+    }
+}
+
+// splitters of segment blockIdx.x: a jittered regular sample of (bits,
+// position) pairs, sorted (stable by bits = by (bits, position): the sample
+// positions ascend); splitter j = sample (j + 1) * 16 (j < 255)
+template <bool FULL>
+__global__ __launch_bounds__(LS_THREADS) void ss_splitter_kernel(const uint64_t* __restrict__ keys,
+                                                                 int64_t seglen, int begin,
+                                                                 uint64_t mask, int passes,
+                                                                 uint64_t* __restrict__ spk,
+                                                                 uint32_t* __restrict__ spp) {
+    __shared__ LdsRadix L;
+    const int64_t base = (int64_t)blockIdx.x * seglen;
+    const int64_t stride = seglen / SS_SAMPLE;  // >= 1: seglen > LS_CAP = SS_SAMPLE
+    for (int i = threadIdx.x; i < SS_SAMPLE; i += LS_THREADS) {
+        const uint32_t h = (uint32_t)i * 2654435761u;
+        const int64_t p = (int64_t)i * stride + (int64_t)((h >> 8) % (uint32_t)stride);
+        L.k[0][i] = kbits<FULL>(keys[base + p], begin, mask);
+        L.i[0][i] = (uint32_t)p;
+    }
+    __syncthreads();
+    const int c = lds_radix<true>(L, SS_SAMPLE, 0, ~0ull, passes);
+    constexpr int per = SS_SAMPLE / SS_BUCKETS;
+    if (threadIdx.x < SS_BUCKETS - 1) {
+        spk[(int64_t)blockIdx.x * SS_BUCKETS + threadIdx.x] = L.k[c][(threadIdx.x + 1) * per];
+        spp[(int64_t)blockIdx.x * SS_BUCKETS + threadIdx.x] = L.i[c][(threadIdx.x + 1) * per];
+    }
+}
+
+// bucket of every key (the number of splitters below its (bits, position)
+// pair) -> dig, and the segment's bucket histogram -> ghist (pass-0 row)
+template <bool FULL>
+__global__ __launch_bounds__(RS_THREADS) void ss_classify_kernel(
+    const uint64_t* __restrict__ keys, int64_t seglen, int64_t tps, int begin, uint64_t mask,
+    const uint64_t* __restrict__ spk, const uint32_t* __restrict__ spp, uint8_t* __restrict__ dig,
+    int32_t* __restrict__ ghist) {
+    __shared__ uint64_t sk[SS_BUCKETS];
+    __shared__ uint32_t sp[SS_BUCKETS];
+    __shared__ int32_t h[SS_BUCKETS];
+    static_assert(SS_BUCKETS == RS_THREADS, "thread b loads splitter b");
+    const int tid = threadIdx.x;
+    const int64_t seg = blockIdx.x / tps, lt = blockIdx.x - seg * tps;
+    if (tid < SS_BUCKETS - 1) {
+        sk[tid] = spk[seg * SS_BUCKETS + tid];
+        sp[tid] = spp[seg * SS_BUCKETS + tid];
+    }
+    h[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+        const int64_t p = lt * RS_TILE + r * RS_THREADS + tid;
+        if (p < seglen) {
+            const uint64_t b = kbits<FULL>(keys[seg * seglen + p], begin, mask);
+            int lo = 0, hi = SS_BUCKETS - 1;  // lower bound over the 255 splitters
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const bool below = sk[mid] < b || (sk[mid] == b && sp[mid] < (uint32_t)p);
+                if (below) lo = mid + 1;
+                else hi = mid;
+            }
+            dig[seg * seglen + p] = (uint8_t)lo;
+            atomicAdd(&h[lo], 1);
+        }
+    }
+    __syncthreads();
+    if (h[tid]) atomicAdd(&ghist[seg * (RS_GHIST_BYTES / 4) + tid], h[tid]);
+}
+
+// bucket (blockIdx.x % 256) of segment (blockIdx.x / 256): its pairs, in input
+// order at [start, start + cnt) of ksrc / vsrc, sorted into kdst / vdst
+template <bool FULL>
+__global__ __launch_bounds__(LS_THREADS) void ss_bucket_kernel(
+    uint64_t* __restrict__ ksrc, int32_t* __restrict__ vsrc, uint64_t* __restrict__ kdst,
+    int32_t* __restrict__ vdst, int64_t seglen, int begin, uint64_t mask, int passes,
+    const int32_t* __restrict__ ghist) {
+    __shared__ LdsRadix L;
+    __shared__ int32_t dbase[RS_BINS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t seg = blockIdx.x / SS_BUCKETS;
+    const int b = (int)(blockIdx.x % SS_BUCKETS);
+    const int32_t* gh = ghist + seg * (RS_GHIST_BYTES / 4);
+    // start = the counts of the buckets before b
+    int32_t v = tid < b ? gh[tid] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) L.wsum[wave] = v;
+    __syncthreads();
+    int32_t start = 0;
+#pragma unroll
+    for (int w = 0; w < LS_WAVES; ++w) start += L.wsum[w];
+    const int cnt = gh[b];
+    const int64_t off = seg * seglen + start;
+    if (cnt <= 1) {
+        if (cnt == 1 && tid == 0) {
+            kdst[off] = ksrc[off];
+            vdst[off] = vsrc[off];
+        }
+        return;
+    }
+    if (cnt <= LS_CAP) {
+        for (int i = tid; i < cnt; i += LS_THREADS) {
+            L.k[0][i] = ksrc[off + i];
+            L.i[0][i] = (uint32_t)i;
+        }
+        __syncthreads();
+        const int c = lds_radix<FULL>(L, cnt, begin, mask, passes);
+        for (int i = tid; i < cnt; i += LS_THREADS) {
+            kdst[off + i] = L.k[c][i];
+            vdst[off + i] = vsrc[off + L.i[c][i]];
+        }
+        return;
+    }
+    // fallback: stable LSD radix sort of the bucket by this workgroup, through
+    // global memory (src <-> dst at the same offsets); chunks of LS_THREADS
+    // pairs ranked by wave ballots as in rs_pass_kernel
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint64_t* kin = ksrc + off;
+    int32_t* vin = vsrc + off;
+    uint64_t* kout = kdst + off;
+    int32_t* vout = vdst + off;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        if (tid < RS_BINS) dbase[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < cnt; i += LS_THREADS)
+            atomicAdd(&dbase[(kbits<FULL>(kin[i], begin, mask) >> shift) & 0xFF], 1);
+        __syncthreads();
+        if (wave == 0) {  // exclusive scan of the 256 digit counts, 4 per lane
+            int32_t c[4], run = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = dbase[lane * 4 + q];
+                run += c[q];
+            }
+            int32_t x = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            int32_t e = x - run;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                dbase[lane * 4 + q] = e;
+                e += c[q];
+            }
+        }
+        __syncthreads();
+        for (int c0 = 0; c0 < cnt; c0 += LS_THREADS) {
+            const int i = c0 + tid;
+            const bool ok = i < cnt;
+            const uint64_t k = ok ? kin[i] : 0;
+            const int32_t val = ok ? vin[i] : 0;
+            const int d = ok ? (int)((kbits<FULL>(k, begin, mask) >> shift) & 0xFF) : -1;
+            uint64_t same = __ballot(ok);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+                const uint64_t plane = __ballot(ok && ((d >> bit) & 1));
+                same &= ((d >> bit) & 1) ? plane : ~plane;
+            }
+            const int rk = __popcll(same & below);
+            for (int q = lane; q < RS_BINS; q += 64) L.wc[wave][q] = 0;
+            __syncthreads();
+            if (ok && rk == 0) L.wc[wave][d] = __popcll(same);
+            __syncthreads();
+            if (tid < RS_BINS) {  // digit tid: waves' exclusive offsets, the chunk's total
+                int32_t run = 0;
+#pragma unroll
+                for (int w = 0; w < LS_WAVES; ++w) {
+                    const int32_t t = L.wc[w][tid];
+                    L.wc[w][tid] = run;
+                    run += t;
+                }
+                L.i[0][tid] = (uint32_t)run;
+            }
+            __syncthreads();
+            if (ok) {
+                const int pos = dbase[d] + L.wc[wave][d] + rk;
+                kout[pos] = k;
+                vout[pos] = val;
+            }
+            __syncthreads();
+            if (tid < RS_BINS) dbase[tid] += (int32_t)L.i[0][tid];
+            __syncthreads();
+        }
+        uint64_t* kt = kin;
+        kin = kout;
+        kout = kt;
+        int32_t* vt = vin;
+        vin = vout;
+        vout = vt;
+        __syncthreads();
+    }
+    if ((passes & 1) == 0) {  // the result is back in src
+        for (int i = tid; i < cnt; i += LS_THREADS) {
+            kdst[off + i] = ksrc[off + i];
+            vdst[off + i] = vsrc[off + i];
+        }
+    }
+}
+
 int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
                              int32_t* vals_tmp, int64_t nseg, int64_t seglen, int begin_bit,
                              int end_bit, void* temp, bool* in_tmp) {
@@ -170,6 +514,51 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
     int32_t* ghist = (int32_t*)temp;
     uint32_t* ticket = (uint32_t*)((char*)temp + nseg * RS_GHIST_BYTES);
     uint32_t* status = (uint32_t*)((char*)temp + nseg * RS_GHIST_BYTES + RS_TICKET_BYTES);
+    const int width = std::min(64, end_bit - begin_bit);
+    const bool full = begin_bit == 0 && width == 64;
+    const uint64_t mask = width == 64 ? ~0ull : ((1ull << width) - 1);
+    if (seglen <= LS_CAP) {
+        if (full)
+            ls_sort_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, seglen, 0, mask,
+                                                                     passes);
+        else
+            ls_sort_kernel<false><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, seglen,
+                                                                      begin_bit, mask, passes);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    if (passes >= SS_MIN_PASSES && seglen <= SS_MAX) {
+        // temp: ghist | ticket | one pass of look-back status | bucket bytes | splitters
+        // (within radix_sort_batched_temp_bytes: tiles * 8 KB covers them)
+        uint8_t* dig = (uint8_t*)status + align_up((size_t)tiles * RS_BINS * 4, 256);
+        uint64_t* spk = (uint64_t*)(dig + align_up((size_t)n, 256));
+        uint32_t* spp = (uint32_t*)(spk + nseg * SS_BUCKETS);
+        DM_HIP(hipMemsetAsync(temp, 0,
+                              nseg * RS_GHIST_BYTES + RS_TICKET_BYTES + (size_t)tiles * RS_BINS * 4,
+                              s));
+        if (full) {
+            ss_splitter_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, seglen, 0, mask,
+                                                                           passes, spk, spp);
+            ss_classify_kernel<true><<<(unsigned)tiles, RS_THREADS, 0, s>>>(
+                keys, seglen, tps, 0, mask, spk, spp, dig, ghist);
+        } else {
+            ss_splitter_kernel<false><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, seglen, begin_bit,
+                                                                            mask, passes, spk, spp);
+            ss_classify_kernel<false><<<(unsigned)tiles, RS_THREADS, 0, s>>>(
+                keys, seglen, tps, begin_bit, mask, spk, spp, dig, ghist);
+        }
+        rs_pass_kernel<<<(unsigned)tiles, RS_THREADS, 0, s>>>(keys, vals, keys_tmp, vals_tmp, seglen,
+                                                             tps, 0, ghist, status, ticket, dig);
+        const unsigned nb = (unsigned)(nseg * SS_BUCKETS);
+        if (full)
+            ss_bucket_kernel<true><<<nb, LS_THREADS, 0, s>>>(keys_tmp, vals_tmp, keys, vals, seglen,
+                                                             0, mask, passes, ghist);
+        else
+            ss_bucket_kernel<false><<<nb, LS_THREADS, 0, s>>>(keys_tmp, vals_tmp, keys, vals, seglen,
+                                                              begin_bit, mask, passes, ghist);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
     DM_HIP(hipMemsetAsync(temp, 0,
                           nseg * RS_GHIST_BYTES + RS_TICKET_BYTES +
                               (size_t)passes * tiles * RS_BINS * 4,
@@ -811,4 +1200,23 @@ extern "C" int dm_sel_best(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* o
 }
 extern "C" int dm_sel_worst(dm_ctx* ctx, const dm_pop* pop, int64_t k, int32_t* out_idx) {
     return sel_sorted(ctx, pop, k, out_idx, false);
+}
+
+// Test hook (not part of include/deapmi.h): sort nseg segments of seglen
+// (key, value) pairs in place by key bits [begin_bit, end_bit), stably,
+// through the dispatcher above (LDS / sample / radix sort by size), then wait.
+extern "C" int dm_test_sort_pairs(dm_ctx* ctx, uint64_t* keys, int32_t* vals, int64_t nseg,
+                                  int64_t seglen, int begin_bit, int end_bit) {
+    DM_CHECK_ARG(ctx && keys && vals, "null argument");
+    DM_CHECK_ARG(nseg >= 0 && seglen >= 0 && begin_bit >= 0 && end_bit <= 64, "bad sort shape");
+    const int64_t n = nseg * seglen;
+    const size_t kb = align_up((size_t)std::max<int64_t>(n, 1) * 8, 256);
+    const size_t vb = align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);
+    char* t = (char*)scratch(ctx, kb + vb + radix_sort_batched_temp_bytes(nseg, seglen));
+    if (!t) return DM_ERR_NOMEM;
+    int rc = radix_sort_pairs_batched(ctx->stream, keys, vals, (uint64_t*)t, (int32_t*)(t + kb),
+                                      nseg, seglen, begin_bit, end_bit, t + kb + vb);
+    if (rc) return rc;
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    return DM_OK;
 }
