@@ -208,6 +208,40 @@ struct LdsRadix {
     int32_t same;                   // the pass's digit is one value: no scatter
 };
 
+// the digit passes the n pairs in k[0] need: the high digits their minimum
+// and maximum share are constant in all of them (LSD: only the low digits
+// below run); one workgroup-wide min / max in LDS
+template <bool FULL>
+__device__ __forceinline__ int lds_passes_needed(LdsRadix& L, int n, int begin, uint64_t mask,
+                                                 int passes) {
+    __shared__ unsigned long long mn, mx;
+    if (threadIdx.x == 0) {
+        mn = ~0ull;
+        mx = 0ull;
+    }
+    __syncthreads();
+    uint64_t a = ~0ull, z = 0ull;
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        const uint64_t b = kbits<FULL>(L.k[0][i], begin, mask);
+        a = b < a ? b : a;
+        z = b > z ? b : z;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a2 = __shfl_xor(a, o, 64), z2 = __shfl_xor(z, o, 64);
+        a = a2 < a ? a2 : a;
+        z = z2 > z ? z2 : z;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&mn, (unsigned long long)a);
+        atomicMax(&mx, (unsigned long long)z);
+    }
+    __syncthreads();
+    const uint64_t d = (uint64_t)mn ^ (uint64_t)mx;
+    const int vary = d == 0 ? 0 : 64 - __clzll((long long)d);
+    return min(passes, (vary + 7) / 8);
+}
+
 // returns the buffer (0 or 1) holding the sorted pairs
 template <bool FULL>
 __device__ __forceinline__ int lds_radix(LdsRadix& L, int n, int begin, uint64_t mask, int passes) {
@@ -294,6 +328,7 @@ __global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restric
         sv[i] = vals[base + i];
     }
     __syncthreads();
+    passes = lds_passes_needed<FULL>(L, n, begin, mask, passes);
     const int c = lds_radix<FULL>(L, n, begin, mask, passes);
     for (int i = threadIdx.x; i < n; i += LS_THREADS) {
         keys[base + i] = L.k[c][i];
@@ -320,6 +355,7 @@ __global__ __launch_bounds__(LS_THREADS) void ss_splitter_kernel(const uint64_t*
         L.i[0][i] = (uint32_t)p;
     }
     __syncthreads();
+    passes = lds_passes_needed<true>(L, SS_SAMPLE, 0, ~0ull, passes);
     const int c = lds_radix<true>(L, SS_SAMPLE, 0, ~0ull, passes);
     constexpr int per = SS_SAMPLE / SS_BUCKETS;
     if (threadIdx.x < SS_BUCKETS - 1) {
@@ -373,7 +409,7 @@ template <bool FULL>
 __global__ __launch_bounds__(LS_THREADS) void ss_bucket_kernel(
     uint64_t* __restrict__ ksrc, int32_t* __restrict__ vsrc, uint64_t* __restrict__ kdst,
     int32_t* __restrict__ vdst, int64_t seglen, int begin, uint64_t mask, int passes,
-    const int32_t* __restrict__ ghist) {
+    const int32_t* __restrict__ ghist, const uint64_t* __restrict__ spk) {
     __shared__ LdsRadix L;
     __shared__ int32_t dbase[RS_BINS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -391,10 +427,19 @@ __global__ __launch_bounds__(LS_THREADS) void ss_bucket_kernel(
     for (int w = 0; w < LS_WAVES; ++w) start += L.wsum[w];
     const int cnt = gh[b];
     const int64_t off = seg * seglen + start;
-    if (cnt <= 1) {
-        if (cnt == 1 && tid == 0) {
-            kdst[off] = ksrc[off];
-            vdst[off] = vsrc[off];
+    // the bucket's keys lie between its two splitters: the high digits the
+    // splitters share are constant in it, only the digits below need passes
+    // (a bucket of 1/256 of a 2^18 key range: 5-6 of 8)
+    {
+        const uint64_t lo = b > 0 ? spk[seg * SS_BUCKETS + b - 1] : 0ull;
+        const uint64_t hi = b < SS_BUCKETS - 1 ? spk[seg * SS_BUCKETS + b] : ~0ull;
+        const int vary = lo == hi ? 0 : 64 - __clzll((long long)(lo ^ hi));
+        passes = min(passes, (vary + 7) / 8);
+    }
+    if (cnt <= 1 || passes == 0) {  // one pair, or one key value: input order is the order
+        for (int i = tid; i < cnt; i += LS_THREADS) {
+            kdst[off + i] = ksrc[off + i];
+            vdst[off + i] = vsrc[off + i];
         }
         return;
     }
@@ -552,10 +597,10 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
         const unsigned nb = (unsigned)(nseg * SS_BUCKETS);
         if (full)
             ss_bucket_kernel<true><<<nb, LS_THREADS, 0, s>>>(keys_tmp, vals_tmp, keys, vals, seglen,
-                                                             0, mask, passes, ghist);
+                                                             0, mask, passes, ghist, spk);
         else
             ss_bucket_kernel<false><<<nb, LS_THREADS, 0, s>>>(keys_tmp, vals_tmp, keys, vals, seglen,
-                                                              begin_bit, mask, passes, ghist);
+                                                              begin_bit, mask, passes, ghist, spk);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }

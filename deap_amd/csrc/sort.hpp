@@ -37,29 +37,40 @@ int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t*
                          int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp,
                          bool* in_tmp);
 
+// Inclusive scan (sum, or max when MAX) of a wave through DPP moves: within
+// each row of 16 lanes by row_shr 1, 2, 4, 8, then row 0's / rows 0-1's last
+// lane broadcast into the rows above (row_bcast:15, row_bcast:31).  Lanes a
+// move does not reach take the identity.  Six VALU ops with DPP operands
+// instead of six ds_bpermute round trips through the LDS crossbar.
+template <bool MAX>
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t x, int width = 64) {
+    constexpr int32_t ident = MAX ? INT32_MIN : 0;
+    auto op = [](int32_t a, int32_t b) { return MAX ? max(a, b) : a + b; };
+    x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    if (width > 16)
+        x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    if (width > 32)
+        x = op(x, __builtin_amdgcn_update_dpp(ident, x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return x;
+}
+
 // Inclusive scan (sum, or max when MAX) over the NT threads of a workgroup:
-// lane shuffles within each wave, one wave scans the wave totals -- two
+// a DPP scan within each wave, one wave scans the wave totals -- two
 // barriers (an LDS Hillis-Steele scan over 256 slots takes 16).  sh: NT / 64
 // ints of LDS.  Every thread must call it.
 template <int NT, bool MAX>
 __device__ __forceinline__ int32_t block_incl_scan(int32_t v, int32_t* sh) {
     static_assert(NT % 64 == 0 && NT / 64 <= 64, "whole waves, at most 64");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x = MAX ? max(x, y) : x + y;
-    }
+    const int32_t x = wave_incl_scan<MAX>(v);
     if (lane == 63) sh[wave] = x;
     __syncthreads();
     if (wave == 0) {
         int32_t w = lane < NT / 64 ? sh[lane] : (MAX ? INT32_MIN : 0);
-#pragma unroll
-        for (int o = 1; o < NT / 64; o <<= 1) {
-            const int32_t y = __shfl_up(w, o, 64);
-            if (lane >= o) w = MAX ? max(w, y) : w + y;
-        }
+        w = wave_incl_scan<MAX>(w, NT / 64);
         if (lane < NT / 64) sh[lane] = w;
     }
     __syncthreads();
