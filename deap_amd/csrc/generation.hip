@@ -7,6 +7,23 @@
 namespace dm {
 
 // Lanes per offspring pair: enough lanes to cover the row in few chunks.
+// zero two int arrays of n entries in one launch (16-B stores): the ordered
+// plans' slot counts and labels, two hipMemsetAsync fills of 4 MB at 2^20
+// that ran 8.6 us each (profiles/r05fin2/c3_kernel_stats.csv)
+__global__ __launch_bounds__(256) void zero2_kernel(int32_t* __restrict__ a, int32_t* __restrict__ b,
+                                                    int64_t n) {
+    const int64_t n4 = n >> 2;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += step) {
+        reinterpret_cast<int4*>(a)[i] = make_int4(0, 0, 0, 0);
+        if (b) reinterpret_cast<int4*>(b)[i] = make_int4(0, 0, 0, 0);
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+        a[i] = 0;
+        if (b) b[i] = 0;
+    }
+}
+
 static int pick_group_float(int dim) {
     const int q = (dim + 3) / 4;  // lane-slots of 4 genes
     if (q <= 4) return 4;
@@ -141,7 +158,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
             int32_t* keys = (int32_t*)(w + 2 * pb + 2 * hb);
             int32_t* tick = (int32_t*)(w + 2 * pb + 2 * hb + kb);
             void* stemp = w + 2 * pb + 2 * hb + 2 * kb;
-            DM_HIP(hipMemsetAsync(hist, 0, (size_t)a.np * 4, ctx->stream));
+            const unsigned zg = (unsigned)std::min<int64_t>(2048, (a.np / 4 + 255) / 256 + 1);
             if (!ctx->knobs.pipe_key_fitter) {
                 int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
                 // bins: labels of the parent graph's neighbourhoods (round 1
@@ -149,7 +166,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 // DM_PIPE_LABEL_ROUNDS=0 the degree keys
                 const int rounds = ctx->knobs.pipe_label_rounds;
                 int32_t* lab = rounds > 0 ? deg : nullptr;  // zeroed: labels unset
-                DM_HIP(hipMemsetAsync(deg, 0, (size_t)a.np * 4, ctx->stream));
+                zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, deg, a.np);
                 int2* pairs2 = lab ? (int2*)((char*)deg + hb) : nullptr;  // 2 kb
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
                                   nullptr, lab ? nullptr : deg, nullptr, lab, pairs2);
@@ -157,6 +174,7 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 launch_plan_degree_keys(plans, pairs2, deg, lab, keys, tick, hist, npairs,
                                         ctx->stream);
             } else {
+                zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, nullptr, a.np);
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,
                                   hist, tick);
             }
