@@ -165,7 +165,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
 // pass of 2^18 keys, 8 passes per 64-bit key (profiles/r05fin4).
 //  - seglen <= LS_CAP: one workgroup per segment sorts the pairs in LDS
 //    (lds_radix below) -- one launch.
-//  - seglen <= SS_MAX and more than SS_MIN_PASSES digits: sample sort.  255
+//  - SS_MIN <= seglen <= SS_MAX and at least SS_MIN_PASSES digits: sample sort.  255
 //    splitters per segment from a sorted jittered-regular sample of (key
 //    bits, position) pairs; a classify pass stores each key's bucket byte and
 //    histograms the buckets; ONE one-sweep pass (rs_pass_kernel on the bytes)
@@ -182,6 +182,7 @@ constexpr int LS_WAVES = LS_THREADS / 64;
 constexpr int LS_CAP = 4096;       // pairs one workgroup sorts in LDS
 constexpr int SS_SAMPLE = 4096;    // sample per segment (16 per bucket)
 constexpr int SS_BUCKETS = 256;    // = RS_BINS: the bucket is the scatter digit
+constexpr int64_t SS_MIN = 1 << 16;  // below, its fixed ~90 us (splitter + bucket sorts) loses to radix
 constexpr int64_t SS_MAX = 1 << 19;
 constexpr int SS_MIN_PASSES = 5;
 static_assert(SS_SAMPLE <= LS_CAP, "the sample is sorted in LDS");
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(LS_THREADS) void ss_splitter_kernel(const uint64_t*
                                                                  uint32_t* __restrict__ spp) {
     __shared__ LdsRadix L;
     const int64_t base = (int64_t)blockIdx.x * seglen;
-    const int64_t stride = seglen / SS_SAMPLE;  // >= 1: seglen > LS_CAP = SS_SAMPLE
+    const int64_t stride = seglen / SS_SAMPLE;  // >= 16: seglen >= SS_MIN
     for (int i = threadIdx.x; i < SS_SAMPLE; i += LS_THREADS) {
         const uint32_t h = (uint32_t)i * 2654435761u;
         const int64_t p = (int64_t)i * stride + (int64_t)((h >> 8) % (uint32_t)stride);
@@ -572,7 +573,7 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
-    if (passes >= SS_MIN_PASSES && seglen <= SS_MAX) {
+    if (passes >= SS_MIN_PASSES && seglen >= SS_MIN && seglen <= SS_MAX) {
         // temp: ghist | ticket | one pass of look-back status | bucket bytes | splitters
         // (within radix_sort_batched_temp_bytes: tiles * 8 KB covers them)
         uint8_t* dig = (uint8_t*)status + align_up((size_t)tiles * RS_BINS * 4, 256);

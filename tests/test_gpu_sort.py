@@ -1,9 +1,9 @@
 """The library's stable (uint64 key, int32 value) pair sort against numpy's
 stable argsort, on every path the dispatcher takes (sort.hip
 radix_sort_pairs_batched): the one-workgroup LDS sort (seglen <= 4,096), the
-sample sort (4,096 < seglen <= 2^19, more than four 8-bit digits), its
+sample sort (2^16 <= seglen <= 2^19, more than four 8-bit digits), its
 per-bucket radix fallback (a bucket the sample missed), and the one-sweep
-radix sort (larger, or fewer digits).
+radix sort (4,096 < seglen < 2^16, larger, or fewer digits).
 
 The sort carries every ordering the NSGA-II path makes -- objective ranks,
 the lexicographic order of the fitnesses, crowding and the last-front cut
@@ -80,7 +80,7 @@ def test_lds_sort_on_a_bit_range_and_batched(gpu):
     _check(gpu, keys, 5, 3000)
 
 
-@pytest.mark.parametrize("n", [LS_CAP + 1, 8193, 100_000, 1 << 18, 1 << 19])
+@pytest.mark.parametrize("n", [1 << 16, 100_000, 1 << 18, 1 << 19])
 def test_sample_sort_matches_stable_argsort(gpu, n):
     rng = np.random.default_rng(n)
     x = rng.random(n)
@@ -103,8 +103,8 @@ def test_sample_sort_batched_segments_and_bit_range(gpu):
     seglen = 212_736  # the unique-fitness count of a C5 generation
     keys = _doubles_as_keys(rng.random(2 * seglen))
     _check(gpu, keys, 2, seglen)
-    raw = rng.integers(0, 2**64, 3 * 20_000, dtype=np.uint64)
-    _check(gpu, raw, 3, 20_000, begin=8, end=56)  # 6 digits: sample sort on masked bits
+    raw = rng.integers(0, 2**64, 3 * 70_000, dtype=np.uint64)
+    _check(gpu, raw, 3, 70_000, begin=8, end=56)  # 6 digits: sample sort on masked bits
 
 
 def test_sample_sort_bucket_fallback(gpu):
@@ -112,7 +112,7 @@ def test_sample_sort_bucket_fallback(gpu):
     keys: one bucket holds nearly everything and is sorted by the
     workgroup-local radix fallback (sort.hip ss_bucket_kernel)."""
     n = 1 << 17
-    stride = n // SS_SAMPLE
+    stride = n // SS_SAMPLE  # (the sample sort's range starts at 2^16)
     i = np.arange(SS_SAMPLE, dtype=np.uint64)
     h = (i * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
     sampled = i * np.uint64(stride) + (h >> np.uint64(8)) % np.uint64(stride)
@@ -124,7 +124,7 @@ def test_sample_sort_bucket_fallback(gpu):
     _check(gpu, keys, 1, n)
 
 
-@pytest.mark.parametrize("n,end", [(1 << 20, 64), (300_000, 24)])
+@pytest.mark.parametrize("n,end", [(1 << 20, 64), (300_000, 24), (LS_CAP + 1, 64), (20_000, 64)])
 def test_radix_sort_paths_match_stable_argsort(gpu, n, end):
     rng = np.random.default_rng(end)
     keys = rng.integers(0, 2**64, n, dtype=np.uint64)
