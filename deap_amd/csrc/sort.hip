@@ -165,13 +165,13 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
 // pass of 2^18 keys, 8 passes per 64-bit key (profiles/r05fin4).
 //  - seglen <= LS_CAP: one workgroup per segment sorts the pairs in LDS
 //    (lds_radix below) -- one launch.
-//  - SS_MIN <= seglen <= SS_MAX and at least SS_MIN_PASSES digits: sample sort.  255
-//    splitters per segment from a sorted jittered-regular sample of (key
-//    bits, position) pairs; a classify pass stores each key's bucket byte and
-//    histograms the buckets; ONE one-sweep pass (rs_pass_kernel on the bytes)
-//    scatters the pairs into bucket order, stably; one workgroup per bucket
-//    sorts it in LDS, stably (lds_radix).  The splitters
-//    carry the position, so equal keys spread over buckets and every pair is
+//  - SS_MIN <= seglen <= SS_MAX with at least SS_MIN_PASSES digits: sample
+//    sort.  255 splitters per segment from a sorted jittered-regular sample
+//    of (key bits, position) pairs; a classify pass stores each key's bucket
+//    byte and histograms the buckets; ONE one-sweep pass (rs_pass_kernel on
+//    the bytes) scatters the pairs into bucket order, stably; one workgroup
+//    per bucket sorts it in LDS, stably (lds_radix).  The splitters carry
+//    the position, so equal keys spread over buckets and every pair is
 //    distinct: the result is exactly the stable order.  A bucket larger than
 //    LS_CAP (a sample that missed a cluster) is sorted by a workgroup-local
 //    LSD radix sort through global memory instead: slower, same result.
