@@ -1267,6 +1267,7 @@ struct FrontSum {      // read by the host after each batch of launches
     int32_t overflow;  // front nfronts + 1 has more members than the sorting workgroup holds
     int32_t ncand;
     int64_t sorted, lastinds;
+    int64_t maxinds;    // individuals of the largest front so far (crowding's segmented sort)
     int32_t arrive[3];  // search workgroups done, per candidate buffer
 };
 struct CandBufs {
@@ -1367,6 +1368,7 @@ __device__ void tab_finish(const TabArgs& a, int32_t j, int32_t n, int64_t pend,
     a.sum->nfronts = j;
     a.sum->sorted = nx.sorted;
     a.sum->lastinds = pend;
+    a.sum->maxinds = pend > a.sum->maxinds ? pend : a.sum->maxinds;
     a.sum->done = nx.done;
     a.sum->overflow = 0;
 }
@@ -1957,6 +1959,7 @@ __global__ void tab_front0_kernel(TabArgs a, const int32_t* F0p, const int64_t* 
     a.sum->ncand = 0;
     a.sum->sorted = s0;
     a.sum->lastinds = s0;
+    a.sum->maxinds = s0;
     a.fstarts[0] = 0;
     a.fstarts[1] = (int32_t)F0;
 }
@@ -2192,7 +2195,7 @@ int fast_rank_keys(dm_ctx* ctx, const char* ws, int64_t n, int64_t U, int m, con
 static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32_t* F0,
                            const int64_t* sorted0, int64_t N, const int32_t* gsize, int32_t* ulist,
                            int32_t* rankU, int32_t* fstarts, char* ws, std::vector<int32_t>& ufront,
-                           int64_t* sorted, int64_t* last_inds) {
+                           int64_t* sorted, int64_t* last_inds, int64_t* max_inds) {
     hipStream_t s = ctx->stream;
     const FastLayout L = fast_layout(n, U);
     const FrontsWork W = fronts_work(U);
@@ -2304,6 +2307,7 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
     }
     *sorted = hsum->sorted;
     *last_inds = hsum->lastinds;
+    if (max_inds) *max_inds = hsum->maxinds;
     return DM_OK;
 }
 
@@ -2316,10 +2320,11 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
-                int64_t* last_inds) {
+                int64_t* last_inds, int64_t* max_inds) {
     hipStream_t s = ctx->stream;
     const FastLayout L = fast_layout(n, U);
     const int32_t* sigma = (const int32_t*)(ws + L.sigma);
+    if (max_inds) *max_inds = INT64_MAX;  // unknown unless the table peel reports it
     const int32_t* pos = (const int32_t*)(ws + L.pos);
     const int32_t* nseg = (const int32_t*)(ws + L.nseg);
     int2* mrow = (int2*)(ws + L.mrow);
@@ -2327,7 +2332,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     int32_t* cq = (int32_t*)(ws + L.cq);
     if (fast_table_peel(ctx, m))
         return fast_fronts_tab(ctx, m, n, U, F0, sorted0, N, gsize, ulist, rankU, fstarts, ws,
-                               ufront, sorted, last_inds);
+                               ufront, sorted, last_inds, max_inds);
     char* p = ws + L.work;
     const FrontsWork W = fronts_work(U);
     FrontState* st = (FrontState*)(p + W.pages);  // + the eight candidate-bucket pages

@@ -40,7 +40,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
                 const int64_t* sorted0,
                 int64_t N, const int32_t* gsize, int32_t* ulist, int32_t* rankU, int32_t* count,
                 int32_t* fstarts, char* ws, std::vector<int32_t>& ufront, int64_t* sorted,
-                int64_t* last_inds);
+                int64_t* last_inds, int64_t* max_inds = nullptr);
 
 // ---------------------------------------------------------------------------
 // Workspace bump allocator over the context scratch
@@ -527,6 +527,7 @@ struct SortResult {
     int64_t nsorted = 0;
     int32_t nfronts = 0;
     int64_t last_inds = 0;  // individuals of the last emitted front
+    int64_t max_inds = INT64_MAX;  // individuals of the largest emitted front (if known)
     int64_t U = 0;          // unique fitnesses
     bool rank_keys = false; // rank_keys filled (fast path)
 };
@@ -704,7 +705,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     int32_t rnk = 0;
     int64_t* hostd = (int64_t*)(hostv + 8);
     const bool device_fronts = fast && !first_only;
-    int64_t last_inds = 0;
+    int64_t last_inds = 0, max_inds = 0;
     if (device_fronts) {
         // front 0's size and individual count stay on the device: the peel's
         // first kernel reads them (no host round trip)
@@ -712,7 +713,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         int64_t total = 0;
         // ufs doubles as the device front-start array
         if ((rc = fast_fronts(ctx, D, m, n, U, ftotal, dtotal, N, gsize, ulist, rankU, count, ufs,
-                              fwork, ufront, &total, &last_inds)))
+                              fwork, ufront, &total, &last_inds, &max_inds)))
             return rc;
         sorted_inds = total;
     } else {
@@ -724,6 +725,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         DM_HIP(hipStreamSynchronize(s));
         sorted_inds = hostd[0];
         last_inds = hostd[0];
+        max_inds = last_inds;
         ufront.push_back((int32_t)F);
     }
     while (!fast && !first_only && sorted_inds < N && ustart + F < U && F > 0) {
@@ -759,6 +761,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
         DM_HIP(hipStreamSynchronize(s));
         sorted_inds += hostd[0];
         last_inds = hostd[0];
+        max_inds = std::max(max_inds, last_inds);
         ustart = nstart;
         F = F2;
         ++rnk;
@@ -789,6 +792,7 @@ static int sort_nondominated_impl(dm_ctx* ctx, const dm_pop* pop, int64_t k, boo
     res->nsorted = sorted_inds;
     res->nfronts = nfronts;
     res->last_inds = last_inds;
+    res->max_inds = max_inds;
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -854,15 +858,20 @@ __global__ void crowd_rank_key_kernel(const int32_t* rk, int64_t U, bool neg, co
     GRID_LOOP(j, T) {
         const int32_t p = pos[j];
         const uint32_t r = (uint32_t)(neg ? (int32_t)(U - 1) - rk[p] : rk[p]);
-        keys[j] = ((uint64_t)(uint32_t)fid[p] << rbits) | r;
+        keys[j] = fid ? ((uint64_t)(uint32_t)fid[p] << rbits) | r : (uint64_t)r;  // fid null: rank alone
     }
 }
 
 // rk (nullable): per-objective integer ranks of the T individuals (m x T,
 // sort_nondominated_impl's rank_keys) over U unique fitnesses.
+// max_front: individuals of the largest front, when known -- at most
+// LDS_SORT_CAP and each objective's order is ONE segmented LDS sort (a
+// workgroup per front, by rank alone: a front never leaves its range)
+// instead of a 24-bit (front, rank) one-sweep radix sort of all T.
 static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                          const int32_t* order, const int32_t* fstart_dev, int32_t nfronts,
-                         int64_t T, double* crowd, const int32_t* rk = nullptr, int64_t U = 0) {
+                         int64_t T, double* crowd, const int32_t* rk = nullptr, int64_t U = 0,
+                         int64_t max_front = INT64_MAX) {
     hipStream_t s = ctx->stream;
     const int m = pop->nobj;
     if (T <= 0 || nfronts <= 0) return DM_OK;
@@ -898,6 +907,19 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
         while (rbits < 31 && (1ll << rbits) < U) ++rbits;
         int kbits = rbits;
         while (kbits < 64 && (1ll << (kbits - rbits)) <= nfronts) ++kbits;
+        if (max_front <= LDS_SORT_CAP) {
+            for (int i = 0; i < m; ++i) {
+                crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U,
+                                                            weights[i] < 0.0, nullptr, pos, rbits,
+                                                            keys, T);
+                int rc = seg_sort_pairs_small(s, keys, pos, fstart_dev, nfronts, 0, rbits);
+                if (rc) return rc;
+                crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
+                                                          fstart_dev, T, crowd);
+            }
+            DM_LAUNCH_CHECK();
+            return DM_OK;
+        }
         for (int i = 0; i < m; ++i) {
             crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U, weights[i] < 0.0,
                                                         fid, pos, rbits, keys, T);
@@ -1108,7 +1130,7 @@ extern "C" int dm_sel_nsga2(dm_ctx* ctx, const dm_pop* pop, const double* weight
     rc = sort_nondominated_impl(ctx, pop, k, false, order, fstart, nullptr, &r, rkeys);
     if (rc) return rc;
     rc = crowding_impl(ctx, pop, weights, order, fstart, r.nfronts, r.nsorted, crowd,
-                       r.rank_keys ? rkeys : nullptr, r.U);
+                       r.rank_keys ? rkeys : nullptr, r.U, r.max_inds);
     if (rc) return rc;
     return take_chosen(ctx, order, r, k, crowd, out_idx);
 }

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(
 // ---------------------------------------------------------------------------
 constexpr int LS_THREADS = 1024;
 constexpr int LS_WAVES = LS_THREADS / 64;
-constexpr int LS_CAP = 4096;       // pairs one workgroup sorts in LDS
+constexpr int LS_CAP = LDS_SORT_CAP;  // pairs one workgroup sorts in LDS
 constexpr int SS_SAMPLE = 4096;    // sample per segment (16 per bucket)
 constexpr int SS_BUCKETS = 256;    // = RS_BINS: the bucket is the scatter digit
 constexpr int64_t SS_MIN = 1 << 16;  // below, its fixed ~90 us (splitter + bucket sorts) loses to radix
@@ -313,16 +313,19 @@ __device__ __forceinline__ int lds_radix(LdsRadix& L, int n, int begin, uint64_t
     return cur;
 }
 
-// one workgroup per segment of seglen <= LS_CAP, sorted in place
+// one workgroup per segment of at most LS_CAP pairs, sorted in place: segment
+// g is [g seglen, (g + 1) seglen), or [starts[g], starts[g + 1]) with starts
 template <bool FULL>
 __global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restrict__ keys,
                                                              int32_t* __restrict__ vals,
                                                              int64_t seglen, int begin,
-                                                             uint64_t mask, int passes) {
+                                                             uint64_t mask, int passes,
+                                                             const int32_t* __restrict__ starts) {
     __shared__ LdsRadix L;
     __shared__ int32_t sv[LS_CAP];
-    const int64_t base = (int64_t)blockIdx.x * seglen;
-    const int n = (int)seglen;
+    const int64_t base = starts ? (int64_t)starts[blockIdx.x] : (int64_t)blockIdx.x * seglen;
+    const int n = starts ? min(starts[blockIdx.x + 1] - starts[blockIdx.x], LS_CAP) : (int)seglen;
+    if (n <= 1) return;  // workgroup-uniform
     for (int i = threadIdx.x; i < n; i += LS_THREADS) {
         L.k[0][i] = keys[base + i];
         L.i[0][i] = (uint32_t)i;
@@ -566,10 +569,11 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
     if (seglen <= LS_CAP) {
         if (full)
             ls_sort_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, seglen, 0, mask,
-                                                                     passes);
+                                                                     passes, nullptr);
         else
             ls_sort_kernel<false><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, seglen,
-                                                                      begin_bit, mask, passes);
+                                                                      begin_bit, mask, passes,
+                                                                      nullptr);
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
@@ -631,6 +635,23 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
         DM_HIP(hipMemcpyAsync(keys, kin, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
         DM_HIP(hipMemcpyAsync(vals, vin, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
     }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+}
+
+int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int32_t* starts,
+                         int64_t nseg, int begin_bit, int end_bit) {
+    if (nseg <= 0 || end_bit <= begin_bit) return DM_OK;
+    DM_CHECK_ARG(nseg <= (1ll << 31) - 1, "too many segments");
+    const int width = std::min(64, end_bit - begin_bit);
+    const int passes = std::min(RS_MAX_PASSES, (width + 7) / 8);
+    const uint64_t mask = width == 64 ? ~0ull : ((1ull << width) - 1);
+    if (begin_bit == 0 && width == 64)
+        ls_sort_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, 0, 0, mask, passes,
+                                                                 starts);
+    else
+        ls_sort_kernel<false><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, 0, begin_bit, mask,
+                                                                  passes, starts);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }

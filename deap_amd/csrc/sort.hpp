@@ -37,6 +37,15 @@ int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t*
                          int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp,
                          bool* in_tmp);
 
+// Pairs one workgroup sorts in LDS.
+constexpr int LDS_SORT_CAP = 4096;
+// Stable sort of nseg variable-length segments [starts[g], starts[g + 1])
+// (starts on the device), each of at most LDS_SORT_CAP pairs -- the caller
+// guarantees it -- by key bits [begin_bit, end_bit): one workgroup per
+// segment, in LDS, one launch.
+int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int32_t* starts,
+                         int64_t nseg, int begin_bit, int end_bit);
+
 // Inclusive scan (sum, or max when MAX) of a wave through DPP moves: within
 // each row of 16 lanes by row_shr 1, 2, 4, 8, then row 0's / rows 0-1's last
 // lane broadcast into the rows above (row_bcast:15, row_bcast:31).  Lanes a
