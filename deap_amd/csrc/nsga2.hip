@@ -865,7 +865,7 @@ __global__ void crowd_rank_key_kernel(const int32_t* rk, int64_t U, bool neg, co
 // rk (nullable): per-objective integer ranks of the T individuals (m x T,
 // sort_nondominated_impl's rank_keys) over U unique fitnesses.
 // max_front: individuals of the largest front, when known -- at most
-// LDS_SORT_CAP and each objective's order is ONE segmented LDS sort (a
+// LDS_SORT_CAP32 and each objective's order is ONE segmented LDS sort (a
 // workgroup per front, by rank alone: a front never leaves its range)
 // instead of a 24-bit (front, rank) one-sweep radix sort of all T.
 static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
@@ -907,7 +907,7 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
         while (rbits < 31 && (1ll << rbits) < U) ++rbits;
         int kbits = rbits;
         while (kbits < 64 && (1ll << (kbits - rbits)) <= nfronts) ++kbits;
-        if (max_front <= LDS_SORT_CAP) {
+        if (max_front <= (rbits <= 32 ? LDS_SORT_CAP32 : LDS_SORT_CAP)) {
             for (int i = 0; i < m; ++i) {
                 crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U,
                                                             weights[i] < 0.0, nullptr, pos, rbits,

@@ -202,18 +202,34 @@ __device__ __forceinline__ uint64_t kbits(uint64_t k, int begin, uint64_t mask) 
 // digit.  (A bitonic network over the same LDS arrays ran 52-104 us for
 // 4,096 pairs -- 78 stages of LDS-bandwidth-bound compare-exchanges; r05_ssort.)
 struct LdsRadix {
+    using Key = uint64_t;
+    using Idx = uint32_t;
+    static constexpr int cap = LS_CAP;
     uint64_t k[2][LS_CAP];
     uint32_t i[2][LS_CAP];
     int32_t wc[LS_WAVES][RS_BINS];  // per-wave digit counts -> offsets
     int32_t wsum[LS_WAVES];
     int32_t same;                   // the pass's digit is one value: no scatter
 };
+// keys of at most 32 bits: twice the pairs in the same LDS (with the values,
+// 144 KiB for 8,192) -- the crowding distance's per-front rank sorts
+constexpr int LS_CAP32 = LDS_SORT_CAP32;
+struct LdsRadix32 {
+    using Key = uint32_t;
+    using Idx = uint16_t;
+    static constexpr int cap = LS_CAP32;
+    uint32_t k[2][LS_CAP32];
+    uint16_t i[2][LS_CAP32];
+    int32_t wc[LS_WAVES][RS_BINS];
+    int32_t wsum[LS_WAVES];
+    int32_t same;
+};
 
 // the digit passes the n pairs in k[0] need: the high digits their minimum
 // and maximum share are constant in all of them (LSD: only the low digits
 // below run); one workgroup-wide min / max in LDS
-template <bool FULL>
-__device__ __forceinline__ int lds_passes_needed(LdsRadix& L, int n, int begin, uint64_t mask,
+template <bool FULL, class LR>
+__device__ __forceinline__ int lds_passes_needed(LR& L, int n, int begin, uint64_t mask,
                                                  int passes) {
     __shared__ unsigned long long mn, mx;
     if (threadIdx.x == 0) {
@@ -244,22 +260,25 @@ __device__ __forceinline__ int lds_passes_needed(LdsRadix& L, int n, int begin, 
 }
 
 // returns the buffer (0 or 1) holding the sorted pairs
-template <bool FULL>
-__device__ __forceinline__ int lds_radix(LdsRadix& L, int n, int begin, uint64_t mask, int passes) {
+template <bool FULL, class LR>
+__device__ __forceinline__ int lds_radix(LR& L, int n, int begin, uint64_t mask, int passes) {
+    constexpr int PER = LR::cap / LS_THREADS;  // rounds per wave at most
+    using Key = typename LR::Key;
+    using Idx = typename LR::Idx;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int chunk = (n + LS_THREADS - 1) / LS_THREADS * 64;  // per wave, whole rounds
-    const int rounds = chunk / 64;                             // <= LS_CAP / LS_THREADS
+    const int rounds = chunk / 64;                             // <= PER
     const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int cur = 0;
     for (int p = 0; p < passes; ++p) {
         const int shift = 8 * p;
         for (int q = lane; q < RS_BINS; q += 64) L.wc[wave][q] = 0;
         if (tid == 0) L.same = 0;
-        uint64_t kk[LS_CAP / LS_THREADS];
-        uint32_t ii[LS_CAP / LS_THREADS];
-        int dd[LS_CAP / LS_THREADS], rr[LS_CAP / LS_THREADS];
+        Key kk[PER];
+        Idx ii[PER];
+        int dd[PER], rr[PER];
 #pragma unroll
-        for (int r = 0; r < LS_CAP / LS_THREADS; ++r) {
+        for (int r = 0; r < PER; ++r) {
             dd[r] = -1;
             if (r < rounds) {  // wave-uniform
                 const int e = wave * chunk + r * 64 + lane;
@@ -300,7 +319,7 @@ __device__ __forceinline__ int lds_radix(LdsRadix& L, int n, int begin, uint64_t
         __syncthreads();
         if (!L.same) {  // workgroup-uniform
 #pragma unroll
-            for (int r = 0; r < LS_CAP / LS_THREADS; ++r)
+            for (int r = 0; r < PER; ++r)
                 if (dd[r] >= 0) {
                     const int pos = L.wc[wave][dd[r]] + rr[r];
                     L.k[cur ^ 1][pos] = kk[r];
@@ -334,6 +353,31 @@ __global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restric
     __syncthreads();
     passes = lds_passes_needed<FULL>(L, n, begin, mask, passes);
     const int c = lds_radix<FULL>(L, n, begin, mask, passes);
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        keys[base + i] = L.k[c][i];
+        vals[base + i] = sv[L.i[c][i]];
+    }
+}
+
+// ls_sort_kernel for keys of at most 32 bits (< 2^32; sorted by bits [0,
+// width)) over segments [starts[g], starts[g + 1]) of at most LS_CAP32 pairs
+__global__ __launch_bounds__(LS_THREADS) void ls_sort32_kernel(uint64_t* __restrict__ keys,
+                                                               int32_t* __restrict__ vals,
+                                                               uint64_t mask, int passes,
+                                                               const int32_t* __restrict__ starts) {
+    __shared__ LdsRadix32 L;
+    __shared__ int32_t sv[LS_CAP32];
+    const int64_t base = starts[blockIdx.x];
+    const int n = min(starts[blockIdx.x + 1] - starts[blockIdx.x], LS_CAP32);
+    if (n <= 1) return;  // workgroup-uniform
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        L.k[0][i] = (uint32_t)keys[base + i];
+        L.i[0][i] = (uint16_t)i;
+        sv[i] = vals[base + i];
+    }
+    __syncthreads();
+    passes = lds_passes_needed<false>(L, n, 0, mask, passes);
+    const int c = lds_radix<false>(L, n, 0, mask, passes);
     for (int i = threadIdx.x; i < n; i += LS_THREADS) {
         keys[base + i] = L.k[c][i];
         vals[base + i] = sv[L.i[c][i]];
@@ -646,7 +690,9 @@ int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int
     const int width = std::min(64, end_bit - begin_bit);
     const int passes = std::min(RS_MAX_PASSES, (width + 7) / 8);
     const uint64_t mask = width == 64 ? ~0ull : ((1ull << width) - 1);
-    if (begin_bit == 0 && width == 64)
+    if (begin_bit == 0 && width <= 32)
+        ls_sort32_kernel<<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, mask, passes, starts);
+    else if (begin_bit == 0 && width == 64)
         ls_sort_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, 0, 0, mask, passes,
                                                                  starts);
     else
@@ -1283,6 +1329,17 @@ extern "C" int dm_test_sort_pairs(dm_ctx* ctx, uint64_t* keys, int32_t* vals, in
     if (!t) return DM_ERR_NOMEM;
     int rc = radix_sort_pairs_batched(ctx->stream, keys, vals, (uint64_t*)t, (int32_t*)(t + kb),
                                       nseg, seglen, begin_bit, end_bit, t + kb + vb);
+    if (rc) return rc;
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    return DM_OK;
+}
+
+// Test hook: seg_sort_pairs_small over device segment starts (nseg + 1 ints).
+extern "C" int dm_test_seg_sort_pairs(dm_ctx* ctx, uint64_t* keys, int32_t* vals,
+                                      const int32_t* starts, int64_t nseg, int begin_bit,
+                                      int end_bit) {
+    DM_CHECK_ARG(ctx && keys && vals && starts, "null argument");
+    int rc = seg_sort_pairs_small(ctx->stream, keys, vals, starts, nseg, begin_bit, end_bit);
     if (rc) return rc;
     DM_HIP(hipStreamSynchronize(ctx->stream));
     return DM_OK;

@@ -37,11 +37,13 @@ int radix_sort_pairs_any(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t*
                          int32_t* vals_tmp, int64_t n, int begin_bit, int end_bit, void* temp,
                          bool* in_tmp);
 
-// Pairs one workgroup sorts in LDS.
+// Pairs one workgroup sorts in LDS; keys of at most 32 bits: twice as many.
 constexpr int LDS_SORT_CAP = 4096;
+constexpr int LDS_SORT_CAP32 = 8192;
 // Stable sort of nseg variable-length segments [starts[g], starts[g + 1])
-// (starts on the device), each of at most LDS_SORT_CAP pairs -- the caller
-// guarantees it -- by key bits [begin_bit, end_bit): one workgroup per
+// (starts on the device), each of at most LDS_SORT_CAP pairs (LDS_SORT_CAP32
+// when begin_bit = 0 and end_bit <= 32, keys then < 2^32) -- the caller
+// guarantees both -- by key bits [begin_bit, end_bit): one workgroup per
 // segment, in LDS, one launch.
 int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int32_t* starts,
                          int64_t nseg, int begin_bit, int end_bit);

@@ -130,3 +130,41 @@ def test_radix_sort_paths_match_stable_argsort(gpu, n, end):
     keys = rng.integers(0, 2**64, n, dtype=np.uint64)
     keys[rng.integers(0, n, n // 5)] = keys[1]
     _check(gpu, keys, 1, n, 0, end)
+
+
+def _seg_sort(gpu, keys, vals, starts, begin, end):
+    import torch
+    from deap_amd import _lib
+    from deap_amd.device import Context
+    fn = _lib.load().dm_test_seg_sort_pairs
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    k = torch.from_numpy(keys.view(np.int64).copy()).to(gpu)
+    v = torch.from_numpy(vals.copy()).to(gpu)
+    st = torch.from_numpy(starts.astype(np.int32)).to(gpu)
+    ctx = Context.get(gpu)
+    _lib.check(fn(ctx.handle, ctypes.c_void_p(k.data_ptr()), ctypes.c_void_p(v.data_ptr()),
+                  ctypes.c_void_p(st.data_ptr()), len(starts) - 1, begin, end),
+               "dm_test_seg_sort_pairs")
+    return k.cpu().numpy().view(np.uint64), v.cpu().numpy()
+
+
+@pytest.mark.parametrize("end,cap", [(18, 8192), (64, LS_CAP)])
+def test_segmented_lds_sort_matches_stable_argsort(gpu, end, cap):
+    """Variable-length segments (the crowding distance's per-front sorts,
+    nsga2.hip crowding_impl): empty, single, ragged and full-capacity ones;
+    keys of <= 32 bits take the 8,192-pair kernel."""
+    rng = np.random.default_rng(end)
+    sizes = np.array([0, 1, 2, 33, cap, 700, 0, cap - 1, 3000, 5], dtype=np.int64)
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    n = int(starts[-1])
+    hi = 1 << min(end, 63)
+    keys = rng.integers(0, hi, n, dtype=np.uint64)
+    keys[rng.integers(0, n, n // 4)] = keys[3]  # ties keep input order
+    vals = np.arange(n, dtype=np.int32)[::-1].copy()
+    gk, gv = _seg_sort(gpu, keys, vals, starts, 0, end)
+    for a, b in zip(starts[:-1], starts[1:]):
+        o = np.argsort(keys[a:b], kind="stable")
+        assert np.array_equal(gk[a:b], keys[a:b][o])
+        assert np.array_equal(gv[a:b], vals[a:b][o])
