@@ -128,13 +128,14 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
 
     const int ec = eval_class(ev->fn);
     const int64_t npairs = (children->n + 1) / 2;
-    // hot path: native RNG, float rows of 65..1024 genes, fused tournament / random
-    // selection -> per-pair decision kernel + rolling-pipeline kernel on a
-    // persistent grid (generation_pipe.hpp)
+    // hot path: native RNG, float rows of more than 64 genes, fused tournament /
+    // random selection -> per-pair decision kernel + rolling-pipeline kernel on
+    // a persistent grid (generation_pipe.hpp); rows past 1,024 genes take its
+    // run-time chunk count (nch 0)
     if (mode == DM_RNG_NATIVE && parents->gtype != DM_BITS && parents->dim > 64 &&
-        parents->dim <= 1024 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
+        parents->dim <= 65535 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
         ec != EC_MO && !ctx->knobs.disable_pipe) {
-        const int nch = parents->dim <= 512 ? 2 : 4;
+        const int nch = parents->dim <= 512 ? 2 : parents->dim <= 1024 ? 4 : 0;
         // parent order: the plans sorted by a key parent -- of
         // the two, the one in more pair slots of this generation (a greedy
         // vertex cover of the pairs) -- so the pairs that share that row are
@@ -216,6 +217,24 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
             launch_gen_pipe_f64(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
         else
             launch_gen_pipe_f32(q, ec, a.cx, a.mut, nch, ctx->num_cus, ctx->stream);
+        timing_end(ctx);
+        DM_LAUNCH_CHECK();
+        return DM_OK;
+    }
+    // short float rows (at most 64 genes, any objective count): the per-pair
+    // decision kernel + the lane-group streaming kernel (generation_rows.hpp)
+    if (mode == DM_RNG_NATIVE && parents->gtype != DM_BITS && parents->dim <= 64 &&
+        (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) && !ctx->knobs.disable_pipe) {
+        PairPlan* plans = (PairPlan*)scratch(ctx, align_up((size_t)npairs * sizeof(PairPlan), 256));
+        if (!plans) return DM_ERR_NOMEM;
+        const bool count = ec != EC_NONE && a.nevals;
+        launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream);
+        DM_LAUNCH_CHECK();
+        timing_begin(ctx);
+        if (parents->gtype == DM_F64)
+            launch_gen_rows_f64(a, plans, ec, ctx->num_cus, ctx->stream);
+        else
+            launch_gen_rows_f32(a, plans, ec, ctx->num_cus, ctx->stream);
         timing_end(ctx);
         DM_LAUNCH_CHECK();
         return DM_OK;

@@ -127,25 +127,23 @@ template <typename T>
 struct ChunkLayout;
 template <>
 struct ChunkLayout<double> {
+    // a chunk of one row as loaded: lane L's two 16-B pieces
+    struct Raw {
+        dm_d2 a, b;
+    };
     __device__ __forceinline__ static int gene(int c, int lane, int k) {
         return (c << 8) + ((k >> 1) << 7) + 2 * lane + (k & 1);
     }
-    // nt: non-temporal loads (the parent rows are read once per launch)
-    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
-                                                double (&x)[4], bool nt = false) {
+    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim, Raw& r) {
         const int g0 = gene(c, lane, 0), g2 = gene(c, lane, 2);
-        if (g0 < dim) {
-            const dm_d2* p = reinterpret_cast<const dm_d2*>(row + (size_t)g0 * 8);
-            const dm_d2 v = nt ? __builtin_nontemporal_load(p) : *p;
-            x[0] = v.x;
-            x[1] = v.y;
-        }
-        if (g2 < dim) {
-            const dm_d2* p = reinterpret_cast<const dm_d2*>(row + (size_t)g2 * 8);
-            const dm_d2 v = nt ? __builtin_nontemporal_load(p) : *p;
-            x[2] = v.x;
-            x[3] = v.y;
-        }
+        if (g0 < dim) r.a = *reinterpret_cast<const dm_d2*>(row + (size_t)g0 * 8);
+        if (g2 < dim) r.b = *reinterpret_cast<const dm_d2*>(row + (size_t)g2 * 8);
+    }
+    __device__ __forceinline__ static void unpack(const Raw& r, double (&x)[4]) {
+        x[0] = r.a.x;
+        x[1] = r.a.y;
+        x[2] = r.b.x;
+        x[3] = r.b.y;
     }
     // streaming store: the child row is not re-read in this launch
     __device__ __forceinline__ static void store_nt(char* row, int c, int lane, int dim,
@@ -157,15 +155,24 @@ struct ChunkLayout<double> {
             __builtin_nontemporal_store(dm_d2{x[2], x[3]}, reinterpret_cast<dm_d2*>(row + (size_t)g2 * 8));
     }
 };
+// fp32 rows: the ring keeps the loaded floats and widens them only where the
+// chunk is used -- a conversion next to the load would wait for it there
+// (vmcnt), and the ring would hold no load in flight
 template <>
 struct ChunkLayout<float> {
+    typedef dm_f4 Raw;
     __device__ __forceinline__ static int gene(int c, int lane, int k) {
         return (c << 8) + 4 * lane + k;
     }
-    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim,
-                                                double (&x)[4], bool nt = false) {
+    __device__ __forceinline__ static void load(const char* row, int c, int lane, int dim, Raw& r) {
         const int g = gene(c, lane, 0);
-        if (g < dim) Vec4<float>::load(row, g, x);
+        if (g < dim) r = *reinterpret_cast<const dm_f4*>(row + (size_t)g * 4);
+    }
+    __device__ __forceinline__ static void unpack(const Raw& r, double (&x)[4]) {
+        x[0] = r.x;
+        x[1] = r.y;
+        x[2] = r.z;
+        x[3] = r.w;
     }
     __device__ __forceinline__ static void store_nt(char* row, int c, int lane, int dim,
                                                     const double (&x)[4]) {
@@ -287,10 +294,15 @@ struct PipeArgs {
 #define DM_PIPE_DEPTH 2
 #endif
 
-template <typename T, int NCH, int CX, int MUT, int EC, int DEPTH = DM_PIPE_DEPTH>
+// DEPTH: ring slots (chunks in flight per row); fp32 chunks are half the bytes,
+// so their ring is twice as deep (the same 8 KiB in flight per wave)
+template <typename T, int NCH, int CX, int MUT, int EC,
+          int DEPTH = sizeof(T) == 4 ? 2 * DM_PIPE_DEPTH : DM_PIPE_DEPTH>
 __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArgs a) {
     typedef ChunkLayout<T> L;
-    constexpr int D = NCH < DEPTH ? NCH : DEPTH;
+    // NCH = 0: rows of any length, the chunk count read at run time (rounded
+    // up to whole rings; chunks past the row load and store nothing)
+    constexpr int D = NCH == 0 ? DEPTH : NCH < DEPTH ? NCH : DEPTH;
     static_assert(NCH % D == 0, "ring depth must divide the chunk count");
     __shared__ double szig[ZIG_N + 1];
     __shared__ double2 cstab[64];
@@ -324,12 +336,13 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
     if (j >= jend) return;
     int64_t evals = 0;
     const int dim = a.dim;
+    const int nchr = NCH > 0 ? NCH : ((dim + 255) / 256 + D - 1) / D * D;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
     PairPlan pl = load_plan(a.plans, j);
     PairPlan nx = load_plan(a.plans, j + jstep < jend ? j + jstep : j);
     // ring of D chunk slots over the chunk sequence (p,0..NCH-1), (p+W,0..), ...
-    double y0[D][4], y1[D][4];
+    typename L::Raw y0[D], y1[D];
 #pragma unroll
     for (int ch = 0; ch < D; ++ch) {
         L::load(a.pgenes + (int64_t)pl.s0 * a.pstride, ch, lane, dim, y0[ch]);
@@ -352,24 +365,21 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
         const char* n0 = a.pgenes + (int64_t)nx.s0 * a.pstride;
         const char* n1 = a.pgenes + (int64_t)nx.s1 * a.pstride;
         double acc0 = 0.0, acc1 = 0.0, carry0 = 0.0, carry1 = 0.0;
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
+        // chunk ch of the pair, its ring slot sl (compile-time after unrolling)
+        auto chunk = [&](const int ch, const int sl) {
             double x0[4], x1[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                x0[k] = y0[ch % D][k];
-                x1[k] = y1[ch % D][k];
-            }
+            L::unpack(y0[sl], x0);
+            L::unpack(y1[sl], x1);
             // ring: the chunk D ahead into the freed slot (this pair's rows or
             // the next pair's)
             {
                 const int ca = ch + D;
-                if (ca < NCH) {
-                    L::load(r0, ca, lane, dim, y0[ch % D]);
-                    L::load(r1, ca, lane, dim, y1[ch % D]);
+                if (ca < nchr) {
+                    L::load(r0, ca, lane, dim, y0[sl]);
+                    L::load(r1, ca, lane, dim, y1[sl]);
                 } else if (more) {
-                    L::load(n0, ca - NCH, lane, dim, y0[ch % D]);
-                    L::load(n1, ca - NCH, lane, dim, y1[ch % D]);
+                    L::load(n0, ca - nchr, lane, dim, y0[sl]);
+                    L::load(n1, ca - nchr, lane, dim, y1[sl]);
                 }
             }
             const uint32_t slot = (uint32_t)((ch << 6) + lane);  // gene_slot of this lane's genes
@@ -458,6 +468,16 @@ __global__ __launch_bounds__(256, DM_PIPE_MINWAVES) void gen_pipe_kernel(PipeArg
             if (EC != EC_NONE && !(DM_PIPE_ABLATE & 1)) {
                 pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x0, cstab, inv0, acc0, carry0);
                 pipe_eval_chunk<T, EC>(a.ev, dim, ch, lane, x1, cstab, inv1, acc1, carry1);
+            }
+        };
+        if constexpr (NCH > 0) {
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) chunk(ch, ch % D);
+        } else {
+#pragma unroll 1
+            for (int cb = 0; cb < nchr; cb += D) {
+#pragma unroll
+                for (int sl = 0; sl < D; ++sl) chunk(cb + sl, sl);
             }
         }
         if (lane == 0) evals += (int64_t)inv0 + (int64_t)inv1;
@@ -574,6 +594,14 @@ void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, in
                          hipStream_t s);
 void launch_gen_pipe_f32(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s);
+// rows of at most 64 genes (any objective count), generation_rows_{f64,f32}.hip
+void launch_gen_rows_f64(const GenArgs& a, const PairPlan* plans, int ec, int num_cus,
+                         hipStream_t s);
+void launch_gen_rows_f32(const GenArgs& a, const PairPlan* plans, int ec, int num_cus,
+                         hipStream_t s);
+// rows of more than 1,024 genes (nch 0: run-time chunk count), generation_pipe_long.hip
+void launch_gen_pipe_long(const PipeArgs& a, bool f64, int ec, int cx, int mut, int num_cus,
+                          hipStream_t s);
 // Packed-bit hot path (generation_pipe_bits.hip): rows of <= 64 words, one objective.
 void launch_gen_bits_pipe(const GenArgs& a, const PairPlan* plans, bool eval, int num_cus,
                           hipStream_t s);

@@ -280,7 +280,9 @@ void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t
 
 void launch_gen_pipe_f64(const PipeArgs& a, int ec, int cx, int mut, int nch, int num_cus,
                          hipStream_t s) {
-    if (nch <= 2)
+    if (nch == 0)
+        launch_gen_pipe_long(a, true, ec, cx, mut, num_cus, s);
+    else if (nch <= 2)
         launch_pipe_ops<double, 2>(a, ec, cx, mut, num_cus, s);
     else
         launch_pipe_ops<double, 4>(a, ec, cx, mut, num_cus, s);

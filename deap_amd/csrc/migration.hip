@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void match_kernel(const char* genes, const dou
     }
 }
 
-// E[e*k + j] = emigrant e == immigrant j (genome)
+// E[j*k + e] = emigrant e == immigrant j (genome), stored per immigrant
 __global__ void em_im_eq_kernel(const void* em_block, const void* im_block, int64_t k,
                                 int64_t stride, int dim, int gtype, int nobj, uint8_t* E) {
     Block em = block_view((void*)em_block, stride, nobj, k);

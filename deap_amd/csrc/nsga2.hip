@@ -912,7 +912,8 @@ static int crowding_impl(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                 crowd_rank_key_kernel<<<g1(T), 256, 0, s>>>(rk + (int64_t)i * T, U,
                                                             weights[i] < 0.0, nullptr, pos, rbits,
                                                             keys, T);
-                int rc = seg_sort_pairs_small(s, keys, pos, fstart_dev, nfronts, 0, rbits);
+                int rc = seg_sort_pairs_small(s, keys, pos, fstart_dev, nfronts, 0, rbits, ktmp,
+                                              vtmp);
                 if (rc) return rc;
                 crowd_update_kernel<<<g1(T), 256, 0, s>>>(pop->wvalues, m, i, wt, order, pos, fid,
                                                           fstart_dev, T, crowd);

@@ -332,19 +332,150 @@ __device__ __forceinline__ int lds_radix(LR& L, int n, int begin, uint64_t mask,
     return cur;
 }
 
+// A workgroup's stable LSD radix sort of cnt pairs through global memory
+// (src <-> dst at the same offsets; the sorted pairs end in dst): chunks of
+// LS_THREADS pairs ranked by wave ballots as in rs_pass_kernel.  The sample
+// sort's fallback for a bucket its sample missed, and the segmented LDS sorts'
+// for a segment over their capacity (slower, same result: never a silently
+// unsorted tail).  L's per-wave counts and index array are its LDS scratch.
+template <bool FULL, class LR>
+__device__ __noinline__ void wg_global_radix(LR& L, int32_t* dbase, uint64_t* __restrict__ ksrc,
+                                             int32_t* __restrict__ vsrc, uint64_t* __restrict__ kdst,
+                                             int32_t* __restrict__ vdst, int cnt, int begin,
+                                             uint64_t mask, int passes) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint64_t* kin = ksrc;
+    int32_t* vin = vsrc;
+    uint64_t* kout = kdst;
+    int32_t* vout = vdst;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        if (tid < RS_BINS) dbase[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < cnt; i += LS_THREADS)
+            atomicAdd(&dbase[(kbits<FULL>(kin[i], begin, mask) >> shift) & 0xFF], 1);
+        __syncthreads();
+        if (wave == 0) {  // exclusive scan of the 256 digit counts, 4 per lane
+            int32_t c[4], run = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = dbase[lane * 4 + q];
+                run += c[q];
+            }
+            int32_t x = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            int32_t e = x - run;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                dbase[lane * 4 + q] = e;
+                e += c[q];
+            }
+        }
+        __syncthreads();
+        for (int c0 = 0; c0 < cnt; c0 += LS_THREADS) {
+            const int i = c0 + tid;
+            const bool ok = i < cnt;
+            const uint64_t k = ok ? kin[i] : 0;
+            const int32_t val = ok ? vin[i] : 0;
+            const int d = ok ? (int)((kbits<FULL>(k, begin, mask) >> shift) & 0xFF) : -1;
+            uint64_t same = __ballot(ok);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+                const uint64_t plane = __ballot(ok && ((d >> bit) & 1));
+                same &= ((d >> bit) & 1) ? plane : ~plane;
+            }
+            const int rk = __popcll(same & below);
+            for (int q = lane; q < RS_BINS; q += 64) L.wc[wave][q] = 0;
+            __syncthreads();
+            if (ok && rk == 0) L.wc[wave][d] = __popcll(same);
+            __syncthreads();
+            if (tid < RS_BINS) {  // digit tid: waves' exclusive offsets, the chunk's total
+                int32_t run = 0;
+#pragma unroll
+                for (int w = 0; w < LS_WAVES; ++w) {
+                    const int32_t t = L.wc[w][tid];
+                    L.wc[w][tid] = run;
+                    run += t;
+                }
+                L.i[0][tid] = (typename LR::Idx)run;
+            }
+            __syncthreads();
+            if (ok) {
+                const int pos = dbase[d] + L.wc[wave][d] + rk;
+                kout[pos] = k;
+                vout[pos] = val;
+            }
+            __syncthreads();
+            if (tid < RS_BINS) dbase[tid] += (int32_t)L.i[0][tid];
+            __syncthreads();
+        }
+        uint64_t* kt = kin;
+        kin = kout;
+        kout = kt;
+        int32_t* vt = vin;
+        vin = vout;
+        vout = vt;
+        __syncthreads();
+    }
+    if ((passes & 1) == 0) {  // the result is back in src
+        for (int i = tid; i < cnt; i += LS_THREADS) {
+            kdst[i] = ksrc[i];
+            vdst[i] = vsrc[i];
+        }
+    }
+}
+
+// a segment over the LDS sorts' capacity: sorted in global memory through
+// the tmp buffers (at the segment's offset), the result copied back; no tmp
+// buffers: flagged, left as it is
+template <bool FULL, class LR>
+__device__ __forceinline__ void seg_oversize(LR& L, int32_t* dbase, uint64_t* k, int32_t* v,
+                                             uint64_t* ktmp, int32_t* vtmp, int64_t base, int n,
+                                             int begin, uint64_t mask, int passes,
+                                             int32_t* oversize) {
+    if (!ktmp || !vtmp) {
+        if (threadIdx.x == 0 && oversize) atomicMax(oversize, n);
+        return;
+    }
+    wg_global_radix<FULL>(L, dbase, k, v, ktmp + base, vtmp + base, n, begin, mask, passes);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += LS_THREADS) {
+        k[i] = ktmp[base + i];
+        v[i] = vtmp[base + i];
+    }
+}
+
 // one workgroup per segment of at most LS_CAP pairs, sorted in place: segment
-// g is [g seglen, (g + 1) seglen), or [starts[g], starts[g + 1]) with starts
+// g is [g seglen, (g + 1) seglen), or [starts[g], starts[g + 1]) with starts.
+// A variable segment over LS_CAP pairs (the caller's bound on it was wrong)
+// is sorted through ktmp / vtmp (same offsets) by wg_global_radix: slower,
+// never a silently unsorted tail; without tmp buffers it is left unsorted
+// and *oversize is set (the callers pass the buffers).
 template <bool FULL>
 __global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restrict__ keys,
                                                              int32_t* __restrict__ vals,
                                                              int64_t seglen, int begin,
                                                              uint64_t mask, int passes,
-                                                             const int32_t* __restrict__ starts) {
+                                                             const int32_t* __restrict__ starts,
+                                                             uint64_t* __restrict__ ktmp = nullptr,
+                                                             int32_t* __restrict__ vtmp = nullptr,
+                                                             int32_t* __restrict__ oversize = nullptr) {
     __shared__ LdsRadix L;
     __shared__ int32_t sv[LS_CAP];
+    __shared__ int32_t dbase[RS_BINS];
     const int64_t base = starts ? (int64_t)starts[blockIdx.x] : (int64_t)blockIdx.x * seglen;
-    const int n = starts ? min(starts[blockIdx.x + 1] - starts[blockIdx.x], LS_CAP) : (int)seglen;
+    const int n = starts ? starts[blockIdx.x + 1] - starts[blockIdx.x] : (int)seglen;
     if (n <= 1) return;  // workgroup-uniform
+    if (n > LS_CAP) {
+        seg_oversize<FULL>(L, dbase, keys + base, vals + base, ktmp, vtmp, base, n, begin, mask,
+                           passes, oversize);
+        return;
+    }
     for (int i = threadIdx.x; i < n; i += LS_THREADS) {
         L.k[0][i] = keys[base + i];
         L.i[0][i] = (uint32_t)i;
@@ -361,15 +492,25 @@ __global__ __launch_bounds__(LS_THREADS) void ls_sort_kernel(uint64_t* __restric
 
 // ls_sort_kernel for keys of at most 32 bits (< 2^32; sorted by bits [0,
 // width)) over segments [starts[g], starts[g + 1]) of at most LS_CAP32 pairs
+// (larger ones as in ls_sort_kernel)
 __global__ __launch_bounds__(LS_THREADS) void ls_sort32_kernel(uint64_t* __restrict__ keys,
                                                                int32_t* __restrict__ vals,
                                                                uint64_t mask, int passes,
-                                                               const int32_t* __restrict__ starts) {
+                                                               const int32_t* __restrict__ starts,
+                                                               uint64_t* __restrict__ ktmp,
+                                                               int32_t* __restrict__ vtmp,
+                                                               int32_t* __restrict__ oversize) {
     __shared__ LdsRadix32 L;
     __shared__ int32_t sv[LS_CAP32];
+    __shared__ int32_t dbase[RS_BINS];
     const int64_t base = starts[blockIdx.x];
-    const int n = min(starts[blockIdx.x + 1] - starts[blockIdx.x], LS_CAP32);
+    const int n = starts[blockIdx.x + 1] - starts[blockIdx.x];
     if (n <= 1) return;  // workgroup-uniform
+    if (n > LS_CAP32) {
+        seg_oversize<false>(L, dbase, keys + base, vals + base, ktmp, vtmp, base, n, 0, mask,
+                            passes, oversize);
+        return;
+    }
     for (int i = threadIdx.x; i < n; i += LS_THREADS) {
         L.k[0][i] = (uint32_t)keys[base + i];
         L.i[0][i] = (uint16_t)i;
@@ -504,93 +645,9 @@ __global__ __launch_bounds__(LS_THREADS) void ss_bucket_kernel(
         }
         return;
     }
-    // fallback: stable LSD radix sort of the bucket by this workgroup, through
-    // global memory (src <-> dst at the same offsets); chunks of LS_THREADS
-    // pairs ranked by wave ballots as in rs_pass_kernel
-    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint64_t* kin = ksrc + off;
-    int32_t* vin = vsrc + off;
-    uint64_t* kout = kdst + off;
-    int32_t* vout = vdst + off;
-    for (int p = 0; p < passes; ++p) {
-        const int shift = 8 * p;
-        if (tid < RS_BINS) dbase[tid] = 0;
-        __syncthreads();
-        for (int i = tid; i < cnt; i += LS_THREADS)
-            atomicAdd(&dbase[(kbits<FULL>(kin[i], begin, mask) >> shift) & 0xFF], 1);
-        __syncthreads();
-        if (wave == 0) {  // exclusive scan of the 256 digit counts, 4 per lane
-            int32_t c[4], run = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                c[q] = dbase[lane * 4 + q];
-                run += c[q];
-            }
-            int32_t x = run;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            int32_t e = x - run;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                dbase[lane * 4 + q] = e;
-                e += c[q];
-            }
-        }
-        __syncthreads();
-        for (int c0 = 0; c0 < cnt; c0 += LS_THREADS) {
-            const int i = c0 + tid;
-            const bool ok = i < cnt;
-            const uint64_t k = ok ? kin[i] : 0;
-            const int32_t val = ok ? vin[i] : 0;
-            const int d = ok ? (int)((kbits<FULL>(k, begin, mask) >> shift) & 0xFF) : -1;
-            uint64_t same = __ballot(ok);
-#pragma unroll
-            for (int bit = 0; bit < 8; ++bit) {
-                const uint64_t plane = __ballot(ok && ((d >> bit) & 1));
-                same &= ((d >> bit) & 1) ? plane : ~plane;
-            }
-            const int rk = __popcll(same & below);
-            for (int q = lane; q < RS_BINS; q += 64) L.wc[wave][q] = 0;
-            __syncthreads();
-            if (ok && rk == 0) L.wc[wave][d] = __popcll(same);
-            __syncthreads();
-            if (tid < RS_BINS) {  // digit tid: waves' exclusive offsets, the chunk's total
-                int32_t run = 0;
-#pragma unroll
-                for (int w = 0; w < LS_WAVES; ++w) {
-                    const int32_t t = L.wc[w][tid];
-                    L.wc[w][tid] = run;
-                    run += t;
-                }
-                L.i[0][tid] = (uint32_t)run;
-            }
-            __syncthreads();
-            if (ok) {
-                const int pos = dbase[d] + L.wc[wave][d] + rk;
-                kout[pos] = k;
-                vout[pos] = val;
-            }
-            __syncthreads();
-            if (tid < RS_BINS) dbase[tid] += (int32_t)L.i[0][tid];
-            __syncthreads();
-        }
-        uint64_t* kt = kin;
-        kin = kout;
-        kout = kt;
-        int32_t* vt = vin;
-        vin = vout;
-        vout = vt;
-        __syncthreads();
-    }
-    if ((passes & 1) == 0) {  // the result is back in src
-        for (int i = tid; i < cnt; i += LS_THREADS) {
-            kdst[off + i] = ksrc[off + i];
-            vdst[off + i] = vsrc[off + i];
-        }
-    }
+    // fallback: the bucket is larger than LS_CAP (a sample that missed a cluster)
+    wg_global_radix<FULL>(L, dbase, ksrc + off, vsrc + off, kdst + off, vdst + off, cnt, begin,
+                          mask, passes);
 }
 
 int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint64_t* keys_tmp,
@@ -684,20 +741,22 @@ int radix_sort_pairs_batched(hipStream_t s, uint64_t* keys, int32_t* vals, uint6
 }
 
 int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int32_t* starts,
-                         int64_t nseg, int begin_bit, int end_bit) {
+                         int64_t nseg, int begin_bit, int end_bit, uint64_t* keys_tmp,
+                         int32_t* vals_tmp) {
     if (nseg <= 0 || end_bit <= begin_bit) return DM_OK;
     DM_CHECK_ARG(nseg <= (1ll << 31) - 1, "too many segments");
     const int width = std::min(64, end_bit - begin_bit);
     const int passes = std::min(RS_MAX_PASSES, (width + 7) / 8);
     const uint64_t mask = width == 64 ? ~0ull : ((1ull << width) - 1);
     if (begin_bit == 0 && width <= 32)
-        ls_sort32_kernel<<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, mask, passes, starts);
+        ls_sort32_kernel<<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, mask, passes, starts,
+                                                               keys_tmp, vals_tmp, nullptr);
     else if (begin_bit == 0 && width == 64)
         ls_sort_kernel<true><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, 0, 0, mask, passes,
-                                                                 starts);
+                                                                 starts, keys_tmp, vals_tmp);
     else
         ls_sort_kernel<false><<<(unsigned)nseg, LS_THREADS, 0, s>>>(keys, vals, 0, begin_bit, mask,
-                                                                  passes, starts);
+                                                                  passes, starts, keys_tmp, vals_tmp);
     DM_LAUNCH_CHECK();
     return DM_OK;
 }
@@ -781,9 +840,13 @@ __global__ void scan_total_kernel(const int32_t* in, const int32_t* ex, int64_t 
 
 // Reduce-then-scan for up to SC_TILE tiles (n <= 4 Mi): block b's aggregate
 // (scan_reduce_kernel), then every block combines the aggregates before it
-// -- at most SC_TILE ints, from the L2 -- and scans its tile from that
+// -- at most SC_DIRECT ints, from the L2 -- and scans its tile from that
 // prefix (scan_down_kernel).  Two launches and no look-back, where the
-// tile / block-sum / add-back form took three (four with the total).
+// tile / block-sum / add-back form took three (four with the total).  Past
+// SC_DIRECT tiles (1 Mi elements) that combination is O(blocks^2) L2 reads
+// (ADVICE r5): one workgroup scans the aggregates first and each block reads
+// its own prefix (three launches).
+constexpr int64_t SC_DIRECT = 512;
 template <bool MAX>
 __device__ __forceinline__ int32_t sc_block_reduce(int32_t v, int32_t* sh) {
 #pragma unroll
@@ -811,7 +874,8 @@ __global__ __launch_bounds__(SC_THREADS) void scan_reduce_kernel(const int32_t* 
 template <bool MAX, bool INCL>
 __global__ __launch_bounds__(SC_THREADS) void scan_down_kernel(const int32_t* in, int32_t* out,
                                                                int64_t n, const int32_t* sums,
-                                                               int32_t* total) {
+                                                               int32_t* total,
+                                                               const int32_t* pref = nullptr) {
     __shared__ int32_t sh[SC_THREADS];
     __shared__ int32_t shr[SC_THREADS / 64];
     const int32_t ident = MAX ? INT32_MIN : 0;
@@ -825,8 +889,13 @@ __global__ __launch_bounds__(SC_THREADS) void scan_down_kernel(const int32_t* in
         acc = op2<MAX>(acc, v[j]);
     }
     int32_t p = ident;
-    for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += SC_THREADS) p = op2<MAX>(p, sums[b]);
-    p = sc_block_reduce<MAX>(p, shr);
+    if (pref) {
+        p = pref[blockIdx.x];  // the scanned aggregates (exclusive)
+    } else {
+        for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += SC_THREADS)
+            p = op2<MAX>(p, sums[b]);
+        p = sc_block_reduce<MAX>(p, shr);
+    }
     const int32_t incl = block_incl_scan<SC_THREADS, MAX>(acc, sh);
     int32_t run = __shfl_up(incl, 1, 64);
     if ((threadIdx.x & 63) == 0) run = threadIdx.x > 0 ? sh[(threadIdx.x >> 6) - 1] : ident;
@@ -856,13 +925,20 @@ static int scan_impl(hipStream_t s, const int32_t* in, int32_t* out, int64_t n, 
         return DM_OK;
     }
     int32_t* sums = (int32_t*)temp;
+    int32_t* pref = (int32_t*)((char*)temp + align_up((size_t)blocks * 8, 256));
     if (blocks <= SC_TILE) {
         scan_reduce_kernel<MAX><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, n, sums);
-        scan_down_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums, total);
+        if (blocks <= SC_DIRECT) {
+            scan_down_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums,
+                                                                                total);
+        } else {
+            scan_tile_kernel<MAX, false><<<1, SC_THREADS, 0, s>>>(sums, pref, blocks, nullptr);
+            scan_down_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums,
+                                                                                total, pref);
+        }
         DM_LAUNCH_CHECK();
         return DM_OK;
     }
-    int32_t* pref = (int32_t*)((char*)temp + align_up((size_t)blocks * 8, 256));
     void* next = (char*)temp + 2 * align_up((size_t)blocks * 8, 256);
     scan_tile_kernel<MAX, INCL><<<(unsigned)blocks, SC_THREADS, 0, s>>>(in, out, n, sums);
     // exclusive scan of block aggregates
@@ -1334,12 +1410,31 @@ extern "C" int dm_test_sort_pairs(dm_ctx* ctx, uint64_t* keys, int32_t* vals, in
     return DM_OK;
 }
 
-// Test hook: seg_sort_pairs_small over device segment starts (nseg + 1 ints).
+// Test hook: seg_sort_pairs_small over device segment starts (nseg + 1 ints);
+// n = starts[nseg] pairs (the tmp buffers of oversized segments).
 extern "C" int dm_test_seg_sort_pairs(dm_ctx* ctx, uint64_t* keys, int32_t* vals,
                                       const int32_t* starts, int64_t nseg, int begin_bit,
-                                      int end_bit) {
-    DM_CHECK_ARG(ctx && keys && vals && starts, "null argument");
-    int rc = seg_sort_pairs_small(ctx->stream, keys, vals, starts, nseg, begin_bit, end_bit);
+                                      int end_bit, int64_t n) {
+    DM_CHECK_ARG(ctx && keys && vals && starts && n >= 0, "null argument");
+    char* t = (char*)scratch(ctx, align_up((size_t)n * 8, 256) + (size_t)n * 4 + 256);
+    if (!t) return DM_ERR_NOMEM;
+    int rc = seg_sort_pairs_small(ctx->stream, keys, vals, starts, nseg, begin_bit, end_bit,
+                                  (uint64_t*)t, (int32_t*)(t + align_up((size_t)n * 8, 256)));
+    if (rc) return rc;
+    DM_HIP(hipStreamSynchronize(ctx->stream));
+    return DM_OK;
+}
+
+// Test hook: the device scans over n ints (kind 0: exclusive sum with its
+// total in *total, 1: inclusive max) -- one tile, reduce-then-scan with the
+// direct and the scanned-aggregate prefixes, and the block-sum form past 4 Mi.
+extern "C" int dm_test_scan_i32(dm_ctx* ctx, const int32_t* in, int32_t* out, int64_t n, int kind,
+                                int32_t* total) {
+    DM_CHECK_ARG(ctx && in && out && n >= 0 && (kind == 0 || kind == 1), "bad scan arguments");
+    void* t = scratch(ctx, scan_temp_bytes(n));
+    if (!t) return DM_ERR_NOMEM;
+    int rc = kind == 0 ? exclusive_scan_i32(ctx->stream, in, out, n, total, t)
+                       : inclusive_max_scan_i32(ctx->stream, in, out, n, t);
     if (rc) return rc;
     DM_HIP(hipStreamSynchronize(ctx->stream));
     return DM_OK;

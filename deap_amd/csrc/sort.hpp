@@ -42,11 +42,13 @@ constexpr int LDS_SORT_CAP = 4096;
 constexpr int LDS_SORT_CAP32 = 8192;
 // Stable sort of nseg variable-length segments [starts[g], starts[g + 1])
 // (starts on the device), each of at most LDS_SORT_CAP pairs (LDS_SORT_CAP32
-// when begin_bit = 0 and end_bit <= 32, keys then < 2^32) -- the caller
-// guarantees both -- by key bits [begin_bit, end_bit): one workgroup per
-// segment, in LDS, one launch.
+// when begin_bit = 0 and end_bit <= 32, keys then < 2^32) by key bits
+// [begin_bit, end_bit): one workgroup per segment, in LDS, one launch.  A
+// segment over that capacity is still sorted exactly, by its workgroup
+// through keys_tmp / vals_tmp (n entries, same offsets) in global memory.
 int seg_sort_pairs_small(hipStream_t s, uint64_t* keys, int32_t* vals, const int32_t* starts,
-                         int64_t nseg, int begin_bit, int end_bit);
+                         int64_t nseg, int begin_bit, int end_bit, uint64_t* keys_tmp,
+                         int32_t* vals_tmp);
 
 // Inclusive scan (sum, or max when MAX) of a wave through DPP moves: within
 // each row of 16 lanes by row_shr 1, 2, 4, 8, then row 0's / rows 0-1's last

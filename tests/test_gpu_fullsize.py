@@ -31,10 +31,14 @@ CASES = {
     "c3": ("f64", 1000, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
     "c3r": ("f64", 1000, "blend", "gaussian", "rosenbrock", (-1.0,), (-2.048, 2.048)),
     "c2": ("bits", 4096, "twopoint", "flipbit", "onemax", (1.0,), (0, 1)),
+    # round 6: the genome shapes bench.py measures beside the benched ones
+    "c3d30": ("f64", 30, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
+    "c3f32": ("f32", 1000, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
+    "c3d2000": ("f64", 2000, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
 }
 
 
-@pytest.mark.parametrize("cfg", ["c3", "c2", "c3r"])
+@pytest.mark.parametrize("cfg", ["c3", "c2", "c3r", "c3d30", "c3f32", "c3d2000"])
 def test_benched_kernel_at_full_size(gpu, cfg):
     import ctypes
     import torch
@@ -65,7 +69,7 @@ def test_benched_kernel_at_full_size(gpu, cfg):
     step.step(pop, dumped, stream, ctypes.c_void_p(nev.data_ptr() + 8), mode="dump",
               decisions=decs)
     torch.cuda.synchronize()
-    nbytes = (dim + 63) // 64 * 8 if gt == "bits" else dim * 8
+    nbytes = (dim + 63) // 64 * 8 if gt == "bits" else dim * (4 if gt == "f32" else 8)
     # bit-exact genomes over all 2^20 rows (compared as raw bytes on the device)
     assert torch.equal(native.genes[:N, :nbytes], dumped.genes[:N, :nbytes])
     assert bool(native.valid[:N].bool().all()) and bool(dumped.valid[:N].bool().all())

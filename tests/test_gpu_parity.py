@@ -567,6 +567,16 @@ def test_sel_best_large_ties(gpu):
     ("bits", 1000, 999, "twopoint", "flipbit", "onemax", "tournament7"),
     # more than 8 aspirants: the plan kernel + burst kernel form
     ("bits", 500, 2001, "twopoint", "flipbit", "onemax", "tournament9"),
+    # round 6: short float rows (generation_rows.hpp, lane groups of 4 / 8 / 16)
+    ("f64", 30, 5001, "blend", "gaussian", "rastrigin", "tournament"),
+    ("f32", 10, 3001, "twopoint", "gaussian", "rosenbrock", "tournament"),
+    ("f64", 64, 2001, "blend", "gaussian", "sphere", "random"),
+    ("f64", 3, 999, "twopoint", "gaussian", "rastrigin", "tournament7"),
+    # round 6: rows past 1,024 genes (run-time chunk count) and the fp32 ring
+    ("f64", 2000, 3001, "blend", "gaussian", "rastrigin", "tournament"),
+    ("f32", 2500, 2001, "blend", "gaussian", "rosenbrock", "tournament"),
+    ("f32", 300, 3001, "twopoint", "gaussian", "rastrigin", "tournament"),
+    ("f64", 5000, 601, "twopoint", "gaussian", "sphere", "tournament7"),
 ])
 def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
     """The hot path (per-pair plan kernel + rolling-pipeline kernel, native
@@ -589,6 +599,42 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
             tb.register("select", tools.selRandom)
         decs = [] if mode == "dump" else None
         pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.2, 2, verbose=False, decisions=decs,
+                                       mode=mode, stream=stream)
+        outs.append((pop.to_numpy(), log.select("nevals")))
+    (g1, wv1, ok1), nev1 = outs[0]
+    (g2, wv2, ok2), nev2 = outs[1]
+    assert np.array_equal(g1, g2)
+    assert np.array_equal(ok1, ok2)
+    assert _rel_close(wv1, wv2, 1e-12)
+    assert nev1 == nev2
+
+
+@pytest.mark.parametrize("gt,dim,objective,obj", [
+    ("f64", 30, "zdt1", None), ("f32", 12, "dtlz2", 3), ("f64", 64, "zdt3", None),
+    ("f64", 7, "dtlz1", 4)])
+def test_native_short_rows_multiobjective_equal_replay(gpu, gt, dim, objective, obj):
+    """Multi-objective eaSimple on short rows (generation_rows.hpp): the
+    lexicographic tournaments of the plan kernel (selection.py:55-70 through
+    Fitness.__gt__) and the ZDT / DTLZ objectives (deap/benchmarks/__init__.py:
+    391-521) in the lane-group kernel equal the replay kernel's dump mode --
+    genomes bit for bit, fitness within 1e-12 relative."""
+    from deap_amd import algorithms, base, benchmarks, tools
+    from deap_amd.ops import RandomStream
+    m = 2 if objective.startswith("zdt") else obj
+    outs = []
+    for mode in ("native", "dump"):
+        stream = RandomStream(78)
+        pop = tools.initPopulation(n=4001, dim=dim, low=0.2, high=0.8, gtype=gt,
+                                   weights=(-1.0,) * m, stream=stream)
+        kw = {"obj": obj} if obj else {}
+        getattr(benchmarks, objective)(pop, **kw)
+        tb = base.Toolbox()
+        tb.register("mate", tools.cxTwoPoint)
+        tb.register("mutate", tools.mutGaussian, mu=0, sigma=0.01, indpb=0.1)
+        tb.register("evaluate", getattr(benchmarks, objective), **kw)
+        tb.register("select", tools.selTournament, tournsize=3)
+        decs = [] if mode == "dump" else None
+        pop, log = algorithms.eaSimple(pop, tb, 0.6, 0.3, 2, verbose=False, decisions=decs,
                                        mode=mode, stream=stream)
         outs.append((pop.to_numpy(), log.select("nevals")))
     (g1, wv1, ok1), nev1 = outs[0]

@@ -139,13 +139,13 @@ def _seg_sort(gpu, keys, vals, starts, begin, end):
     fn = _lib.load().dm_test_seg_sort_pairs
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                   ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+                   ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64]
     k = torch.from_numpy(keys.view(np.int64).copy()).to(gpu)
     v = torch.from_numpy(vals.copy()).to(gpu)
     st = torch.from_numpy(starts.astype(np.int32)).to(gpu)
     ctx = Context.get(gpu)
     _lib.check(fn(ctx.handle, ctypes.c_void_p(k.data_ptr()), ctypes.c_void_p(v.data_ptr()),
-                  ctypes.c_void_p(st.data_ptr()), len(starts) - 1, begin, end),
+                  ctypes.c_void_p(st.data_ptr()), len(starts) - 1, begin, end, len(keys)),
                "dm_test_seg_sort_pairs")
     return k.cpu().numpy().view(np.uint64), v.cpu().numpy()
 
@@ -168,3 +168,52 @@ def test_segmented_lds_sort_matches_stable_argsort(gpu, end, cap):
         o = np.argsort(keys[a:b], kind="stable")
         assert np.array_equal(gk[a:b], keys[a:b][o])
         assert np.array_equal(gv[a:b], vals[a:b][o])
+
+
+@pytest.mark.parametrize("end,cap", [(18, 8192), (64, LS_CAP)])
+def test_segmented_lds_sort_oversized_segments_are_sorted(gpu, end, cap):
+    """A segment over the LDS sort's capacity (the crowding sort's
+    caller bound the largest front; a wrong bound must not leave a silently
+    unsorted tail): sorted exactly through global memory instead."""
+    rng = np.random.default_rng(100 + end)
+    sizes = np.array([5, cap + 1, 0, 3 * cap + 17, 700], dtype=np.int64)
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    n = int(starts[-1])
+    keys = rng.integers(0, 1 << min(end, 63), n, dtype=np.uint64)
+    keys[rng.integers(0, n, n // 4)] = keys[2]
+    vals = np.arange(n, dtype=np.int32)
+    gk, gv = _seg_sort(gpu, keys, vals, starts, 0, end)
+    for a, b in zip(starts[:-1], starts[1:]):
+        o = np.argsort(keys[a:b], kind="stable")
+        assert np.array_equal(gk[a:b], keys[a:b][o])
+        assert np.array_equal(gv[a:b], vals[a:b][o])
+
+
+@pytest.mark.parametrize("n", [1, 2048, 2049, 512 * 2048, 512 * 2048 + 1, 2048 * 2048,
+                               2048 * 2048 + 5])
+def test_device_scans_match_numpy(gpu, n):
+    """Every scan form (one tile; reduce-then-scan with each block combining
+    the aggregates before it, up to 512 tiles; with the aggregates scanned by
+    one workgroup first, up to 2,048 tiles -- ADVICE r5; the block-sum form
+    beyond), exclusive sum with its total and inclusive max."""
+    import torch
+    from deap_amd import _lib
+    from deap_amd.device import Context
+    fn = _lib.load().dm_test_scan_i32
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                   ctypes.c_void_p]
+    rng = np.random.default_rng(n)
+    x = rng.integers(-50, 100, n, dtype=np.int32)
+    xi = torch.from_numpy(x).to(gpu)
+    out = torch.empty_like(xi)
+    tot = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ctx = Context.get(gpu)
+    _lib.check(fn(ctx.handle, ctypes.c_void_p(xi.data_ptr()), ctypes.c_void_p(out.data_ptr()), n,
+                  0, ctypes.c_void_p(tot.data_ptr())), "dm_test_scan_i32")
+    ex = np.concatenate([[0], np.cumsum(x, dtype=np.int64)[:-1]]).astype(np.int32)
+    assert np.array_equal(out.cpu().numpy(), ex)
+    assert int(tot.cpu()[0]) == int(x.astype(np.int64).sum())
+    _lib.check(fn(ctx.handle, ctypes.c_void_p(xi.data_ptr()), ctypes.c_void_p(out.data_ptr()), n,
+                  1, None), "dm_test_scan_i32")
+    assert np.array_equal(out.cpu().numpy(), np.maximum.accumulate(x))

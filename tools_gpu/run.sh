@@ -69,6 +69,14 @@ for s in ${STEPS:-pytest smoke bench_c3}; do
       step pmc_c5peel 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d $OUT/pmc_c5peel -o run --output-format csv -- python3 bench.py --config c5 --steps 3 --warmup 2 --no-cpu-baseline
       step c5peel_json 60 python3 tools_gpu/c5_peel_pmc.py $OUT/pmc_c5peel $OUT/c5_peel_pmc.json "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU, bench.py --config c5 (gpurun_out/$(basename $OUT))"
       mkdir -p profiles && cp $OUT/c5_peel_pmc.json profiles/c5_peel_pmc.json ;;
+    shapes)  # genome shapes beside the benched ones
+      for c in ${SHAPES:-c3d30 c3d2000 c3f32 c2b8192 zdt1}; do
+        step shape_$c 200 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline
+      done ;;
+    kt_shapes)
+      for c in ${SHAPES:-c3d30 c3d2000 c3f32 c2b8192 zdt1}; do
+        step kt_$c 300 $KT -d $OUT/kt_$c -- python3 bench.py --config $c --steps 10 --warmup 2 --warmup-secs 0 --no-cpu-baseline
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
