@@ -140,12 +140,15 @@ __device__ __forceinline__ double rosen_term(double x, double y) {
 __device__ __forceinline__ double mo_term(int fn, double x) {
     switch (fn) {
         case DM_EVAL_ZDT4: {  // xi**2 - 10*cos(4*pi*xi)                    :447
-            return x * x - 10.0 * cos((4.0 * PI) * x);
+            return x * x - 10.0 * cos_fast((4.0 * PI) * x);
         }
         case DM_EVAL_DTLZ1:
         case DM_EVAL_DTLZ3: {  // (xi-0.5)**2 - cos(20*pi*(xi-0.5))    :489,:544
+            // cos_fast: fdlibm's polynomials (<= 1 ulp, as ocml's cos) with one
+            // small inlined copy; ocml's inlined cos took the lane-group kernels
+            // past 240 VGPRs
             const double d = x - 0.5;
-            return d * d - cos((20.0 * PI) * d);
+            return d * d - cos_fast((20.0 * PI) * d);
         }
         case DM_EVAL_DTLZ2:
         case DM_EVAL_DTLZ4: {  // (xi-0.5)**2                           :518,:574

@@ -242,9 +242,11 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
     // packed-bit hot path (C2): one fused burst kernel for tournaments of at most
     // 8 aspirants (decisions drawn in-kernel), else the plan kernel (which also
     // counts nevals) + the burst kernel (generation_pipe_bits.hip)
-    if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 64 &&
+    if (mode == DM_RNG_NATIVE && parents->gtype == DM_BITS && a.words64 <= 256 &&
         parents->nobj == 1 && (sel == DM_SEL_TOURNAMENT || sel == DM_SEL_RANDOM) &&
-        !ctx->knobs.disable_pipe) {
+        !ctx->knobs.disable_pipe &&
+        (a.words64 <= 64 || ((sel == DM_SEL_RANDOM || tournsize <= 8) && !ctx->knobs.bits_plan))) {
+        // rows of 65-256 words: the fused kernel only (64-word pieces per lane)
         if ((sel == DM_SEL_RANDOM || tournsize <= 8) && !ctx->knobs.bits_plan) {
             // one launch: decisions drawn inside the burst kernel (+ the
             // nevals reduction of its per-workgroup partials)

@@ -1,6 +1,7 @@
 // generation_pipe_bits.hip — hot path of the packed-bit eaSimple generation
 // (OneMax-4096, config C2): native RNG, tournament / random selection, rows
-// of at most 64 u64 words (4096 genes), one objective.
+// of at most 64 u64 words (4096 genes) -- the fused kernel up to 256 words
+// (16,384 genes, round 6) --, one objective.
 //
 // Same two-launch structure as the float hot path (generation_pipe.hpp):
 //  1. pair_plan_kernel (generation_pipe_f64.hip) — one thread per pair draws
@@ -34,6 +35,16 @@ __device__ __forceinline__ uint64_t flip_mask_row(const GenArgs& a, int64_t c, i
     return flip_mask_chunk<64, false>(a, c, 0, lane, st, lds);
 }
 
+// flip_mask_row for rows of WPL x 64 words (lane L: words L + 64 k)
+template <int WPL>
+__device__ __forceinline__ void flip_mask_row_w(const GenArgs& a, int64_t c, int lane,
+                                                uint64_t* lds, uint64_t (&f)[WPL]) {
+    FlipRow<64> st;
+    flip_begin<64>(a, c, lane, st);
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) f[k] = flip_mask_chunk<64, false>(a, c, 64 * k, lane, st, lds);
+}
+
 // The flip masks of every mutated child of a group (bit c of `mut_bits` =
 // child 2 p0 + c) into that child's 64 LDS words: issued right after the
 // group's row loads, so this VALU / LDS work overlaps their latency.
@@ -42,22 +53,30 @@ __device__ __forceinline__ uint64_t flip_mask_row(const GenArgs& a, int64_t c, i
 // mutpb 0.2) plus one scratch slot for the rest, computed in bits_finish.
 constexpr int FLIP_SLOTS = 6;
 
-template <int NCH>
+// Rows of WPL x 64 words: lane L holds words L + 64 k (k < WPL), a slot is
+// 64 WPL words, the row's chunks of 64 words drawn in order from one
+// geometric stream (the same positions as flip_mask_chunk's).
+template <int NCH, int WPL>
 __device__ __forceinline__ void flip_rows_to_lds(const GenArgs& a, int64_t cbase, uint64_t mut_bits,
                                                  int lane, uint64_t* lds) {
     if (a.thr_ind == 0) return;
     int slot = 0;
     for (uint64_t mb = mut_bits; mb && slot < FLIP_SLOTS; mb &= mb - 1, ++slot) {  // wave-uniform
         const int ch = __ffsll((long long)mb) - 1;
-        uint64_t* w = lds + slot * 64;
+        uint64_t* w = lds + slot * 64 * WPL;
         if (a.thr_ind >= (1ull << 32)) {
-            const int nbits = min(64, a.dim - lane * 64);
-            w[lane] = lane >= a.words64 ? 0ull : nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) {
+                const int wi = lane + 64 * k;
+                const int nbits = min(64, a.dim - wi * 64);
+                w[64 * k + lane] = wi >= a.words64 ? 0ull : nbits >= 64 ? ~0ull : ((1ull << nbits) - 1);
+            }
             continue;
         }
         FlipRow<64> st;
         flip_begin<64>(a, cbase + ch, lane, st);
-        flip_chunk_lds<64>(a, cbase + ch, 0, lane, st, w);
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) flip_chunk_lds<64>(a, cbase + ch, 64 * k, lane, st, w + 64 * k);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -263,12 +282,12 @@ struct BitsDraw {
     bool mut_l;
 };
 // A group after its tournament: winners, flags and parent rows in flight.
-template <int PP>
+template <int PP, int WPL>
 struct BitsGroup {
     int64_t p0;
     int32_t s0[PP], s1[PP];
     uint32_t cut[PP], cxf[PP];
-    uint64_t y0[PP], y1[PP];
+    uint64_t y0[PP][WPL], y1[PP][WPL];  // lane L: words L + 64 k
     uint64_t mut_bits;
     double f;      // lane L < 2PP: child L's winner fitness (the clone's)
     uint32_t v;    // ... its validity
@@ -364,9 +383,9 @@ __device__ __forceinline__ void bits_tournament(const BitsDraw& d, int t, int la
     }
 }
 
-template <int PP, bool TOURN>
+template <int PP, int WPL, bool TOURN>
 __device__ __forceinline__ void bits_resolve(const GenArgs& a, const BitsDraw& d, int64_t p0,
-                                             int lane, BitsGroup<PP>& g) {
+                                             int lane, BitsGroup<PP, WPL>& g) {
     constexpr int NCH = 2 * PP;
     constexpr int CXL = 32, MUTL = 32 + 2 * PP;
     const int t = TOURN ? a.tournsize : 1;
@@ -391,37 +410,44 @@ __device__ __forceinline__ void bits_resolve(const GenArgs& a, const BitsDraw& d
     if (live && !(g.cx_c || g.mut))
         g.v = (a.pkeys && a.pkeys[k] != FIT_KEY_NONE) ? 1u : a.pvalid[k];
     const int64_t npairs = (a.nc + 1) / 2;
-    const bool lw = lane < a.words64;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
         g.s0[q] = __builtin_amdgcn_readlane(k, 2 * q);
         g.s1[q] = __builtin_amdgcn_readlane(k, 2 * q + 1);
         g.cut[q] = (uint32_t)__builtin_amdgcn_readlane((int)d.cuts, CXL + q);
         g.cxf[q] = (uint32_t)__builtin_amdgcn_readlane((int)d.cxf_l, CXL + q);
-        g.y0[q] = 0;
-        g.y1[q] = 0;
-        if (lw && p0 + q < npairs) {
-            const uint64_t* r0 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s0[q] * a.pstride);
-            const uint64_t* r1 = reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s1[q] * a.pstride);
+    }
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) {  // every row's first 512 B, then the next ones
+        const bool lw = lane + 64 * w < a.words64;
+#pragma unroll
+        for (int q = 0; q < PP; ++q) {
+            g.y0[q][w] = 0;
+            g.y1[q][w] = 0;
+            if (lw && p0 + q < npairs) {
+                const uint64_t* r0 =
+                    reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s0[q] * a.pstride) + 64 * w;
+                const uint64_t* r1 =
+                    reinterpret_cast<const uint64_t*>(a.pgenes + (int64_t)g.s1[q] * a.pstride) + 64 * w;
 #if DM_BITS_NTLOAD
-            g.y0[q] = __builtin_nontemporal_load(r0 + lane);
-            if (2 * (p0 + q) + 1 < a.nc) g.y1[q] = __builtin_nontemporal_load(r1 + lane);
+                g.y0[q][w] = __builtin_nontemporal_load(r0 + lane);
+                if (2 * (p0 + q) + 1 < a.nc) g.y1[q][w] = __builtin_nontemporal_load(r1 + lane);
 #else
-            g.y0[q] = r0[lane];
-            if (2 * (p0 + q) + 1 < a.nc) g.y1[q] = r1[lane];
+                g.y0[q][w] = r0[lane];
+                if (2 * (p0 + q) + 1 < a.nc) g.y1[q][w] = r1[lane];
 #endif
+            }
         }
     }
 }
 
 // Vary, store and evaluate the group's children; returns how many fitnesses
 // were invalidated (nevals).
-template <int PP, int CX, int MUT, bool EVAL>
-__device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, int lane,
+template <int PP, int WPL, int CX, int MUT, bool EVAL>
+__device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP, WPL>& g, int lane,
                                            uint64_t* flip_lds) {
     constexpr int NCH = 2 * PP;
     const int64_t npairs = (a.nc + 1) / 2;
-    const bool lw = lane < a.words64;
     uint32_t my_count = 0;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
@@ -429,36 +455,55 @@ __device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, i
         if (pq >= npairs) break;
         const int64_t c0 = 2 * pq, c1 = 2 * pq + 1;
         const bool h1 = c1 < a.nc;
-        uint64_t x0 = g.y0[q], x1 = g.y1[q];
-        uint64_t f0 = 0, f1 = 0;  // flip masks: precomputed slot, or drawn now
+        uint64_t f0[WPL], f1[WPL];  // flip masks: precomputed slot, or drawn now
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) f0[w] = f1[w] = 0;
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1)) {
             const uint64_t below = g.mut_bits & ((1ull << (2 * q)) - 1);
             const int r0 = __popcll(below), r1 = r0 + (int)((g.mut_bits >> (2 * q)) & 1);
-            if ((g.mut_bits >> (2 * q)) & 1)
-                f0 = r0 < FLIP_SLOTS ? flip_lds[r0 * 64 + lane]
-                                     : flip_mask_row(a, c0, lane, flip_lds + FLIP_SLOTS * 64);
-            if ((g.mut_bits >> (2 * q + 1)) & 1)
-                f1 = r1 < FLIP_SLOTS ? flip_lds[r1 * 64 + lane]
-                                     : flip_mask_row(a, c1, lane, flip_lds + FLIP_SLOTS * 64);
-        }
-        if (lw) {
-            if (CX == DM_CX_TWOPOINT && g.cxf[q]) {
-                const int cp1 = (int)(g.cut[q] & 0xFFFFu), cp2 = (int)(g.cut[q] >> 16);
-                const uint64_t m = range_mask(cp1 - lane * 64, cp2 - lane * 64);
-                const uint64_t tt = (x0 ^ x1) & m;
-                x0 ^= tt;
-                x1 ^= tt;
+            uint64_t* spare = flip_lds + FLIP_SLOTS * 64 * WPL;
+            if ((g.mut_bits >> (2 * q)) & 1) {
+                if (r0 < FLIP_SLOTS) {
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) f0[w] = flip_lds[(r0 * WPL + w) * 64 + lane];
+                } else {
+                    flip_mask_row_w<WPL>(a, c0, lane, spare, f0);
+                }
             }
-            x0 ^= f0;  // mutation after the crossover (algorithms.py:72-81)
-            x1 ^= f1;
-            uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
-            uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
-            __builtin_nontemporal_store(x0, w0 + lane);
-            if (h1) __builtin_nontemporal_store(x1, w1 + lane);
+            if ((g.mut_bits >> (2 * q + 1)) & 1) {
+                if (r1 < FLIP_SLOTS) {
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) f1[w] = flip_lds[(r1 * WPL + w) * 64 + lane];
+                } else {
+                    flip_mask_row_w<WPL>(a, c1, lane, spare, f1);
+                }
+            }
+        }
+        uint32_t pc_l = 0;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) {
+            const int wi = lane + 64 * w;
+            if (wi < a.words64) {
+                uint64_t x0 = g.y0[q][w], x1 = g.y1[q][w];
+                if (CX == DM_CX_TWOPOINT && g.cxf[q]) {
+                    const int cp1 = (int)(g.cut[q] & 0xFFFFu), cp2 = (int)(g.cut[q] >> 16);
+                    const uint64_t m = range_mask(cp1 - wi * 64, cp2 - wi * 64);
+                    const uint64_t tt = (x0 ^ x1) & m;
+                    x0 ^= tt;
+                    x1 ^= tt;
+                }
+                x0 ^= f0[w];  // mutation after the crossover (algorithms.py:72-81)
+                x1 ^= f1[w];
+                uint64_t* w0 = reinterpret_cast<uint64_t*>(a.cgenes + c0 * a.cstride);
+                uint64_t* w1 = reinterpret_cast<uint64_t*>(a.cgenes + c1 * a.cstride);
+                __builtin_nontemporal_store(x0, w0 + wi);
+                if (h1) __builtin_nontemporal_store(x1, w1 + wi);
+                pc_l += (uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16);
+            }
         }
         if (EVAL) {
-            const uint32_t pc =
-                wave_sum_u32(lw ? ((uint32_t)__popcll(x0) | ((uint32_t)__popcll(x1) << 16)) : 0u);
+            // both children's counts in one 32-bit sum (a row of <= 16,384 genes)
+            const uint32_t pc = wave_sum_u32(pc_l);
             if ((lane >> 1) == q) my_count = (lane & 1) ? (pc >> 16) : (pc & 0xFFFFu);
         }
     }
@@ -482,33 +527,35 @@ __device__ __forceinline__ int bits_finish(const GenArgs& a, BitsGroup<PP>& g, i
 #define DM_BITS_MINW 1  // minimum waves per SIMD the fused kernel is compiled for (A/B)
 #endif
 
-template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
+// WPL: 64-word pieces per row (lane L holds words L + 64 k): rows of up to
+// 4,096 / 8,192 / 16,384 genes
+template <int PP, int CX, int MUT, bool EVAL, bool TOURN, int WPL = 1>
 __global__ __launch_bounds__(256, DM_BITS_MINW) void gen_bits_fused_kernel(GenArgs a,
                                                                            long long* spread) {
     static_assert(PP == 4 || PP == 8, "lane layout: 4 or 8 pairs per wave");
-    // FLIP_SLOTS + 1 flip-mask rows of 64 words per wave (3.5 KiB)
-    __shared__ uint64_t flip_lds_all[4 * (FLIP_SLOTS + 1) * 64];
-    uint64_t* flip_lds = flip_lds_all + (threadIdx.x >> 6) * ((FLIP_SLOTS + 1) * 64);
+    // FLIP_SLOTS + 1 flip-mask rows of 64 WPL words per wave (3.5 KiB per piece)
+    __shared__ uint64_t flip_lds_all[4 * (FLIP_SLOTS + 1) * 64 * WPL];
+    uint64_t* flip_lds = flip_lds_all + (threadIdx.x >> 6) * ((FLIP_SLOTS + 1) * 64 * WPL);
     const int lane = threadIdx.x & 63;
     const int64_t npairs = (a.nc + 1) / 2;
     const int64_t ngroups = (npairs + PP - 1) / PP;
     const int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int evals = 0;
     if (grp < ngroups) {  // one group per wave
-        BitsGroup<PP> g;
+        BitsGroup<PP, WPL> g;
 #if DM_BITS_PRIO
         // the decision chain (Philox -> aspirant keys -> tournament) gates the
         // wave's row loads: it issues ahead of the other waves' streaming work
         __builtin_amdgcn_s_setprio(DM_BITS_PRIO);
 #endif
         const BitsDraw d = bits_draw<PP, CX, MUT, TOURN>(a, grp * PP, lane);
-        bits_resolve<PP, TOURN>(a, d, grp * PP, lane, g);
+        bits_resolve<PP, WPL, TOURN>(a, d, grp * PP, lane, g);
 #if DM_BITS_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
         if (MUT == DM_MUT_FLIPBIT && !(DM_BITS_ABLATE & 1))
-            flip_rows_to_lds<2 * PP>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
-        evals = bits_finish<PP, CX, MUT, EVAL>(a, g, lane, flip_lds);
+            flip_rows_to_lds<2 * PP, WPL>(a, 2 * grp * PP, g.mut_bits, lane, flip_lds);
+        evals = bits_finish<PP, WPL, CX, MUT, EVAL>(a, g, lane, flip_lds);
     }
     if (EVAL && spread) {  // nevals: workgroup count, folded by the last workgroup
         __shared__ int32_t wave_evals[4];
@@ -532,8 +579,13 @@ static int fused_pp(const GenArgs& a) {
 template <int PP, int CX, int MUT, bool EVAL, bool TOURN>
 static void launch_bf(const GenArgs& a, long long* wg, hipStream_t s) {
     const int64_t waves = ((a.nc + 1) / 2 + PP - 1) / PP;
-    gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN><<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(
-        a, wg);
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    if (a.words64 <= 64)
+        gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, 1><<<grid, 256, 0, s>>>(a, wg);
+    else if (a.words64 <= 128)
+        gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, 2><<<grid, 256, 0, s>>>(a, wg);
+    else
+        gen_bits_fused_kernel<PP, CX, MUT, EVAL, TOURN, 4><<<grid, 256, 0, s>>>(a, wg);
 }
 template <int PP, int CX, int MUT>
 static void launch_bf_e(const GenArgs& a, bool eval, long long* wg, hipStream_t s) {

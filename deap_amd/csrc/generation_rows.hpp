@@ -6,10 +6,10 @@
 //     objectives, crossover flag and cuts, mutation flags) into a 32-B plan;
 //  2. gen_rows_kernel — a lane group of G lanes per offspring pair (4 genes
 //     per lane: G = 4 / 8 / 16 for rows of <= 16 / 32 / 64 genes), 64 / G pairs
-//     per wave on a persistent grid.  A group holds the rows of the pair it
-//     varies and of the next one, and the plan of the one after that, in
-//     flight: the only dependent chain per pair is plan -> row loads, and it is
-//     issued two pairs ahead.
+//     per wave on a persistent grid.  A group keeps the rows of PD pairs (the
+//     one it varies and the next PD - 1) and the plan of the pair after them in
+//     flight: the only dependent chain per pair is plan -> row loads, issued
+//     PD pairs ahead.
 // The general kernel (generation.hpp gen_float_kernel) draws the tournaments
 // inside the lane group -- t dependent random fitness loads per child -- and
 // spilled 320-1,000 B per lane to scratch: 0.054 of the HBM roofline on
@@ -131,7 +131,11 @@ __device__ __forceinline__ void rows_eval(const dm_eval& ev, int dim, int g, int
     }
 }
 
-template <typename T, int G, int CX, int MUT, int EC>
+// PD: pairs whose rows are in flight per lane group (the current one included)
+#ifndef DM_ROWS_PD
+#define DM_ROWS_PD 3
+#endif
+template <typename T, int G, int CX, int MUT, int EC, int PD = DM_ROWS_PD>
 __global__ __launch_bounds__(256) void gen_rows_kernel(GenArgs a, const PairPlan* __restrict__ plans) {
     __shared__ double szig[MUT == DM_MUT_GAUSSIAN ? ZIG_N + 1 : 1];
     if (MUT == DM_MUT_GAUSSIAN) {
@@ -149,33 +153,44 @@ __global__ __launch_bounds__(256) void gen_rows_kernel(GenArgs a, const PairPlan
     const bool in = g < dim;
     const double gamma_scale = 1.0 + 2.0 * a.alpha;
 
-    PairPlan pl = load_plan_vec(plans, p);
-    PairPlan nx = load_plan_vec(plans, p + ng < npairs ? p + ng : p);
-    RowRaw<T> r0, r1;
-    if (in) {
-        r0.load(a.pgenes + (int64_t)pl.s0 * a.pstride, g);
-        r1.load(a.pgenes + (int64_t)pl.s1 * a.pstride, g);
+    // ring of PD pairs whose rows are in flight (slot k: pair p + k ng), and
+    // the plan of the pair after them
+    PairPlan plq[PD];
+    RowRaw<T> rq0[PD], rq1[PD];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+        const int64_t pk = p + k * ng;
+        plq[k] = load_plan_vec(plans, pk < npairs ? pk : p);
     }
-    for (; p < npairs; p += ng) {
-        // the next pair's rows and the plan after it, in flight while this
-        // pair is varied
-        const bool more = p + ng < npairs;
-        const int64_t p2 = p + 2 * ng;
-        const PairPlan nn = load_plan_vec(plans, p2 < npairs ? p2 : p);
-        RowRaw<T> q0, q1;
-        if (in && more) {
-            q0.load(a.pgenes + (int64_t)nx.s0 * a.pstride, g);
-            q1.load(a.pgenes + (int64_t)nx.s1 * a.pstride, g);
+#pragma unroll
+    for (int k = 0; k < PD; ++k)
+        if (in && p + k * ng < npairs) {
+            rq0[k].load(a.pgenes + (int64_t)plq[k].s0 * a.pstride, g);
+            rq1[k].load(a.pgenes + (int64_t)plq[k].s1 * a.pstride, g);
+        }
+    PairPlan nx = load_plan_vec(plans, p + PD * ng < npairs ? p + PD * ng : p);
+    // pair p from ring slot sl (compile-time after unrolling)
+    auto pair_step = [&](const int sl) {
+        const PairPlan pl = plq[sl];
+        double y0[4] = {0, 0, 0, 0}, y1[4] = {0, 0, 0, 0};
+        if (in) {
+            rq0[sl].unpack(y0);
+            rq1[sl].unpack(y1);
+        }
+        // refill the slot: the rows of pair p + PD ng, the plan after it
+        {
+            const int64_t pn = p + PD * ng, pn2 = pn + ng;
+            if (in && pn < npairs) {
+                rq0[sl].load(a.pgenes + (int64_t)nx.s0 * a.pstride, g);
+                rq1[sl].load(a.pgenes + (int64_t)nx.s1 * a.pstride, g);
+            }
+            plq[sl] = nx;
+            nx = load_plan_vec(plans, pn2 < npairs ? pn2 : p);
         }
         const int64_t c0 = 2 * p, c1 = 2 * p + 1;
         const uint32_t fl = pl.flags;
         const bool cx = fl & PF_CX, mut0 = fl & PF_MUT0, mut1 = fl & PF_MUT1;
         const bool has1 = fl & PF_HAS1, inv0 = fl & PF_INV0, inv1 = fl & PF_INV1;
-        double y0[4] = {0, 0, 0, 0}, y1[4] = {0, 0, 0, 0};
-        if (in) {
-            r0.unpack(y0);
-            r1.unpack(y1);
-        }
         if (in && CX == DM_CX_BLEND && cx) {
             // gamma = (1. + 2.*alpha)*random() - alpha ; blend   (crossover.py:255-258)
             const u32x4 w = gene4_words<T>(a.rng, ST_BLEND, (uint32_t)p, g);
@@ -285,10 +300,14 @@ __global__ __launch_bounds__(256) void gen_rows_kernel(GenArgs a, const PairPlan
                 a.cvalid[c] = EC != EC_NONE ? 1 : (inv ? 0 : 1);
             }
         }
-        pl = nx;
-        nx = nn;
-        r0 = q0;
-        r1 = q1;
+    };
+    for (;;) {
+#pragma unroll
+        for (int sl = 0; sl < PD; ++sl) {
+            if (p >= npairs) return;  // group-uniform
+            pair_step(sl);
+            p += ng;
+        }
     }
 }
 

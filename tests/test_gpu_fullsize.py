@@ -35,10 +35,11 @@ CASES = {
     "c3d30": ("f64", 30, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
     "c3f32": ("f32", 1000, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
     "c3d2000": ("f64", 2000, "blend", "gaussian", "rastrigin", (-1.0,), (-5.12, 5.12)),
+    "c2b8192": ("bits", 8192, "twopoint", "flipbit", "onemax", (1.0,), (0, 1)),
 }
 
 
-@pytest.mark.parametrize("cfg", ["c3", "c2", "c3r", "c3d30", "c3f32", "c3d2000"])
+@pytest.mark.parametrize("cfg", ["c3", "c2", "c3r", "c3d30", "c3f32", "c3d2000", "c2b8192"])
 def test_benched_kernel_at_full_size(gpu, cfg):
     import ctypes
     import torch

@@ -577,6 +577,10 @@ def test_sel_best_large_ties(gpu):
     ("f32", 2500, 2001, "blend", "gaussian", "rosenbrock", "tournament"),
     ("f32", 300, 3001, "twopoint", "gaussian", "rastrigin", "tournament"),
     ("f64", 5000, 601, "twopoint", "gaussian", "sphere", "tournament7"),
+    # round 6: packed rows of 65-256 words (the fused kernel's 64-word pieces)
+    ("bits", 8192, 3001, "twopoint", "flipbit", "onemax", "tournament"),
+    ("bits", 10000, 1001, "twopoint", "flipbit", "onemax", "random"),
+    ("bits", 16384, 777, "twopoint", "flipbit", "onemax", "tournament7"),
 ])
 def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, objective, sel):
     """The hot path (per-pair plan kernel + rolling-pipeline kernel, native
