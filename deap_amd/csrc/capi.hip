@@ -524,6 +524,7 @@ int dm_ctx_destroy(dm_ctx* ctx) {
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->zig) (void)hipFree(ctx->zig);
     if (ctx->evals_spread) (void)hipFree(ctx->evals_spread);
+    if (ctx->plan_lab) (void)hipFree(ctx->plan_lab);
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     delete ctx;
     return DM_OK;

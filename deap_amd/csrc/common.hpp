@@ -89,6 +89,12 @@ struct dm_ctx {
     int tev_used = 0;  // pairs recorded so far
     int timing_target = 0;  // DM_TIME_GENERATION / DM_TIME_DOMINANCE: which launches
     dm_knobs knobs;
+    // C3 parent order (generation.hip): the parent graph's labels, persistent
+    // and tagged with a per-call epoch in the high 32 bits (nothing zeroes them
+    // between generations: a label of an older epoch reads as unset)
+    uint64_t* plan_lab = nullptr;
+    int64_t plan_lab_n = 0;
+    uint32_t plan_epoch = 0;
     // sortNondominated dominance path (dm_ctx_set_dom_path): DM_DOM_DEFAULT or
     // one of the cross-check paths the parity tests compare against it
     int32_t dom_path = 0;

@@ -40,6 +40,32 @@ int validate_pop(const dm_pop* p, const char* what);
 int validate_eval(const dm_eval* ev, const dm_pop* p);
 int validate_variation(const dm_variation* v, const dm_pop* p);
 
+// The context's persistent parent-graph labels for n rows and this call's
+// epoch (generation_pipe_f64.hip lab_of): grown (and zeroed) on demand, and
+// zeroed again when the 32-bit epoch wraps.
+static uint64_t* plan_labels(dm_ctx* ctx, int64_t n, uint32_t* epoch) {
+    if (n > ctx->plan_lab_n || ctx->plan_epoch == 0xFFFFFFFFu) {
+        if (n > ctx->plan_lab_n) {
+            if (ctx->plan_lab) {
+                if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+                (void)hipFree(ctx->plan_lab);
+                ctx->plan_lab = nullptr;
+                ctx->plan_lab_n = 0;
+            }
+            if (hipMalloc(&ctx->plan_lab, (size_t)n * 8) != hipSuccess) {
+                ctx->plan_lab = nullptr;
+                return nullptr;
+            }
+            ctx->plan_lab_n = n;
+        }
+        if (hipMemsetAsync(ctx->plan_lab, 0, (size_t)ctx->plan_lab_n * 8, ctx->stream) != hipSuccess)
+            return nullptr;
+        ctx->plan_epoch = 0;
+    }
+    *epoch = ++ctx->plan_epoch;
+    return ctx->plan_lab;
+}
+
 int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int32_t sel,
                       int32_t tournsize, const int32_t* sel_index, const dm_variation* var,
                       const dm_eval* ev, dm_rng rng, int32_t mode, const dm_decisions* dec,
@@ -160,19 +186,29 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
             int32_t* tick = (int32_t*)(w + 2 * pb + 2 * hb + kb);
             void* stemp = w + 2 * pb + 2 * hb + 2 * kb;
             const unsigned zg = (unsigned)std::min<int64_t>(2048, (a.np / 4 + 255) / 256 + 1);
-            if (!ctx->knobs.pipe_key_fitter) {
-                int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
+            if (!ctx->knobs.pipe_key_fitter && ctx->knobs.pipe_label_rounds > 0) {
                 // bins: labels of the parent graph's neighbourhoods (round 1
-                // inside the plan kernel, further rounds after it), or with
-                // DM_PIPE_LABEL_ROUNDS=0 the degree keys
-                const int rounds = ctx->knobs.pipe_label_rounds;
-                int32_t* lab = rounds > 0 ? deg : nullptr;  // zeroed: labels unset
-                zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, deg, a.np);
-                int2* pairs2 = lab ? (int2*)((char*)deg + hb) : nullptr;  // 2 kb
+                // inside the plan kernel, further rounds after it), persistent
+                // and epoch-tagged; the plan kernel clears the bins' ticket
+                // counters (hist) for the key kernel: no fill launch
+                uint32_t epoch = 0;
+                uint64_t* lab64 = plan_labels(ctx, a.np, &epoch);
+                if (!lab64) return DM_ERR_NOMEM;
+                int2* pairs2 = (int2*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));  // 2 kb
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
-                                  nullptr, lab ? nullptr : deg, nullptr, lab, pairs2);
-                if (rounds > 1) launch_plan_labels(pairs2, lab, npairs, rounds - 1, ctx->stream);
-                launch_plan_degree_keys(plans, pairs2, deg, lab, keys, tick, hist, npairs,
+                                  nullptr, nullptr, nullptr, lab64, epoch, pairs2, hist, a.np + 1);
+                if (ctx->knobs.pipe_label_rounds > 1)
+                    launch_plan_labels(pairs2, lab64, epoch, npairs, ctx->knobs.pipe_label_rounds - 1,
+                                       ctx->stream);
+                launch_plan_degree_keys(plans, pairs2, nullptr, lab64, epoch, keys, tick, hist,
+                                        npairs, ctx->stream);
+            } else if (!ctx->knobs.pipe_key_fitter) {
+                // DM_PIPE_LABEL_ROUNDS=0: degree keys (counted into the zeroed deg)
+                int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
+                zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, deg, a.np);
+                launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
+                                  nullptr, deg);
+                launch_plan_degree_keys(plans, nullptr, deg, nullptr, 0, keys, tick, hist, npairs,
                                         ctx->stream);
             } else {
                 zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, nullptr, a.np);

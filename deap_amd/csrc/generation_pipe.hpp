@@ -570,11 +570,13 @@ void launch_pipe_ops(const PipeArgs& a, int ec, int cx, int mut, int num_cus, hi
 // keys / hist (zeroed, one counter per parent row): key[p] = the plan's sort
 // key (its fitter parent), tick[p] = its place among the plans of that key
 // (the counter's old value) and hist[key] their count.
-// lab (with hist): the first label-propagation round of the parent order
+// lab64 / epoch: the first label-propagation round of the parent order
+// (epoch-tagged labels, generation_pipe_f64.hip lab_of); zero / nzero: ints
+// the launch clears for a later launch of the generation
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
                        int32_t* keys = nullptr, int32_t* hist = nullptr,
-                       int32_t* tick = nullptr, int32_t* lab = nullptr,
-                       int2* pairs2 = nullptr);
+                       int32_t* tick = nullptr, uint64_t* lab64 = nullptr, uint32_t epoch = 0,
+                       int2* pairs2 = nullptr, int32_t* zero = nullptr, int64_t nzero = 0);
 // Parent order: ordered[start[key[p]] + tick[p]] = plans[p] with p in its
 // flags (start = the exclusive scan of hist).
 void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
@@ -583,10 +585,10 @@ void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t
 // the plan kernel instead): after launch_pair_plans(..., hist = deg) counted
 // every parent slot, key[p] = the parent of more slots, ticketed into hist2.
 void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
-                             const int32_t* lab, int32_t* keys, int32_t* tick, int32_t* hist2,
-                             int64_t npairs, hipStream_t s);
-void launch_plan_labels(const int2* pairs2, int32_t* lab, int64_t npairs, int rounds,
-                        hipStream_t s);
+                             const uint64_t* lab64, uint32_t epoch, int32_t* keys, int32_t* tick,
+                             int32_t* hist2, int64_t npairs, hipStream_t s);
+void launch_plan_labels(const int2* pairs2, uint64_t* lab64, uint32_t epoch, int64_t npairs,
+                        int rounds, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);
 void launch_fit_keys(const GenArgs& a, int16_t* keys, hipStream_t s);
 // num_cus: CUs of the device (the persistent grid is sized from it).

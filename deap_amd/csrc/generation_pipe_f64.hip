@@ -11,11 +11,30 @@ namespace dm {
 // flags (algorithms.py:78-81) and which children need evaluation
 // (algorithms.py:75-81 `del fitness.values`, algorithms.py:155-158).
 // Decisions of pair p -> plans[p]; returns the plan's flags.
+// Parent-graph labels (the parent order's bins): lab64[r] = (epoch << 32) |
+// (INT32_MAX - label); an entry of another epoch is unset, so the persistent
+// array needs no zeroing between generations (ctx->plan_lab).  A row's label
+// is min(that label, r).
+__device__ __forceinline__ int32_t lab_of(const uint64_t* lab64, int32_t r, uint32_t epoch) {
+    const uint64_t u = lab64[r];
+    return (uint32_t)(u >> 32) == epoch ? min(INT32_MAX - (int32_t)(uint32_t)u, r) : r;
+}
+// Profiling-only ablations (product build: 0): bit 0 skips the label
+// atomics, bit 1 replaces the aspirants' fitness loads by a hash.
+#ifndef DM_PLAN_ABLATE
+#define DM_PLAN_ABLATE 0
+#endif
+__device__ __forceinline__ void lab_lower(uint64_t* lab64, int32_t r, int32_t m, uint32_t epoch) {
+    if (DM_PLAN_ABLATE & 1) return;
+    atomicMax((unsigned long long*)(lab64 + r),
+              ((unsigned long long)epoch << 32) | (uint32_t)(INT32_MAX - m));
+}
+
 __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
                                              int64_t p, int32_t* __restrict__ keys,
                                              int32_t* __restrict__ hist,
                                              int32_t* __restrict__ tick,
-                                             int32_t* __restrict__ lab,
+                                             uint64_t* __restrict__ lab64, uint32_t epoch,
                                              int2* __restrict__ pairs2) {
     const int64_t c0 = 2 * p, c1 = 2 * p + 1;
     const bool has1 = c1 < a.nc;
@@ -23,10 +42,13 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     const uint32_t np = (uint32_t)a.np;
     int32_t s[2];
     // One objective, t <= 8 (C3, C4): every aspirant of both tournaments is
-    // drawn first and their fitnesses / validities loaded together, then the
-    // tournaments run in registers -- one round of random loads instead of a
-    // chain of 2t dependent ones (the same aspirants, the same first-drawn-wins
-    // rule).
+    // drawn first and their fitnesses loaded together, then the tournaments run
+    // in registers -- one round of random loads instead of a chain of 2t
+    // dependent ones (the same aspirants, the same first-drawn-wins rule).  A
+    // winner's validity is read afterwards and only for a clone (no crossover
+    // and no mutation: 0.4 of the children at cxpb 0.5, mutpb 0.2): the 2t
+    // validity bytes loaded beside the fitnesses were half of the kernel's
+    // random requests (round 6).
     bool fast = a.sel == DM_SEL_TOURNAMENT && m == 1 && a.tournsize >= 1 && a.tournsize <= 8;
     double fw[2] = {0.0, 0.0};
     uint8_t vw[2] = {1, 1};
@@ -35,7 +57,6 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         const int t = a.tournsize;
         int32_t kk[2][TM];
         double ff[2][TM];
-        uint8_t vv[2][TM];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t c = (uint32_t)(h ? c1 : c0);
@@ -54,25 +75,20 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < TM; ++j)
-                if (j < t && (h == 0 || has1)) {
-                    ff[h][j] = a.pwv[kk[h][j]];
-                    vv[h][j] = a.pvalid[kk[h][j]];
-                }
+                if (j < t && (h == 0 || has1))
+                    ff[h][j] = (DM_PLAN_ABLATE & 2) ? (double)(kk[h][j] & 1023) : a.pwv[kk[h][j]];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             int32_t best = kk[h][0];
             double fb = ff[h][0];
-            uint8_t vb = vv[h][0];
 #pragma unroll
             for (int j = 1; j < TM; ++j)
                 if (j < t && (h == 0 || has1) && !(ff[h][j] == fb) && !(ff[h][j] <= fb)) {
                     best = kk[h][j];
                     fb = ff[h][j];
-                    vb = vv[h][j];
                 }
             s[h] = best;
             fw[h] = fb;
-            vw[h] = vb;
         }
     }
     for (int h = 0; h < (has1 ? 2 : 1) && !fast; ++h) {
@@ -124,9 +140,14 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         vw[1] = a.pvalid[s[1]];
         fw[0] = a.pwv[(int64_t)s[0] * m];
         fw[1] = a.pwv[(int64_t)s[1] * m];
-    } else if (!has1) {
-        vw[1] = vw[0];
-        fw[1] = fw[0];
+    } else {
+        // a varied child is invalid whatever its parent was: only clones read it
+        if (!cx && !(fl & PF_MUT0)) vw[0] = a.pvalid[s[0]];
+        if (has1 && !cx && !(fl & PF_MUT1)) vw[1] = a.pvalid[s[1]];
+        if (!has1) {
+            vw[1] = vw[0];
+            fw[1] = fw[0];
+        }
     }
     if (cx || (fl & PF_MUT0) || !vw[0]) fl |= PF_INV0;
     if (has1 && (cx || (fl & PF_MUT1) || !vw[1])) fl |= PF_INV1;
@@ -144,16 +165,16 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
         const int32_t key = pl.f1 > pl.f0 ? s[1] : s[0];
         keys[p] = key;
         tick[p] = atomicAdd(hist + key, 1);
-    } else if (lab) {
+    } else if (lab64) {
         // neighbourhood bins: the first label-propagation round (plan_label_kernel);
         // the pair's parents also go to a compact array the label rounds and
         // the bin kernel read (8 B per pair instead of 32-B plans)
         if (pairs2) pairs2[p] = make_int2(s[0], s[1]);
-        if (has1) {
-            const int32_t m = min(s[0], s[1]);
-            atomicMax(lab + s[0], INT32_MAX - m);
-            atomicMax(lab + s[1], INT32_MAX - m);
-        }
+        // only the larger row can take a smaller label from this pair (a row's
+        // label is at most the row itself): one random atomic per pair, not two
+        // (each is a memory-side round trip: the two took 23 of the kernel's
+        // 68 us, profiles/r06_prelude)
+        if (has1 && s[0] != s[1]) lab_lower(lab64, max(s[0], s[1]), min(s[0], s[1]), epoch);
     } else if (hist) {
         // degree keys (plan_degree_key_kernel): count both parents' slots
         atomicAdd(hist + s[0], 1);
@@ -166,19 +187,25 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
 // counts the generation's `nevals` (children whose fitness is invalidated,
 // algorithms.py:171-174) into a.nevals: one ballot per wave, evals_fold per
 // workgroup.
+// zero (nullable): nzero ints this launch clears for a later one (the parent
+// order's ticket counters: no separate fill launch)
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
                                                         long long* __restrict__ count_evals,
                                                         int32_t* __restrict__ keys,
                                                         int32_t* __restrict__ hist,
                                                         int32_t* __restrict__ tick,
-                                                        int32_t* __restrict__ lab,
-                                                        int2* __restrict__ pairs2) {
+                                                        uint64_t* __restrict__ lab64,
+                                                        uint32_t epoch,
+                                                        int2* __restrict__ pairs2,
+                                                        int32_t* __restrict__ zero, int64_t nzero) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npairs = (a.nc + 1) / 2;
+    if (zero)
+        for (int64_t i = p; i < nzero; i += (int64_t)gridDim.x * blockDim.x) zero[i] = 0;
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab, pairs2);
+        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -188,14 +215,15 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab, pairs2);
+    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
 }
 
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
-                       int32_t* keys, int32_t* hist, int32_t* tick, int32_t* lab, int2* pairs2) {
+                       int32_t* keys, int32_t* hist, int32_t* tick, uint64_t* lab64,
+                       uint32_t epoch, int2* pairs2, int32_t* zero, int64_t nzero) {
     const int64_t npairs = (a.nc + 1) / 2;
     pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        a, plans, count_evals, keys, hist, tick, lab, pairs2);
+        a, plans, count_evals, keys, hist, tick, lab64, epoch, pairs2, zero, nzero);
 }
 
 // Counting-sort placement of the plans by key: slot start[key] + tick of pair
@@ -227,7 +255,8 @@ __global__ __launch_bounds__(256) void plan_order_kernel(const PairPlan* __restr
 __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __restrict__ plans,
                                                               const int2* __restrict__ pairs2,
                                                               const int32_t* __restrict__ deg,
-                                                              const int32_t* __restrict__ lab,
+                                                              const uint64_t* __restrict__ lab64,
+                                                              uint32_t epoch,
                                                               int32_t* __restrict__ keys,
                                                               int32_t* __restrict__ tick,
                                                               int32_t* __restrict__ hist2,
@@ -236,40 +265,41 @@ __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __
     if (p >= npairs) return;
     const int2 pr = pairs2 ? pairs2[p] : make_int2(plans[p].s0, plans[p].s1);
     const int32_t s0 = pr.x, s1 = pr.y;
-    const int32_t bin = lab ? min(min(INT32_MAX - lab[s0], s0), min(INT32_MAX - lab[s1], s1))
-                            : (deg[s1] > deg[s0] ? s1 : s0);
+    const int32_t bin = lab64 ? min(lab_of(lab64, s0, epoch), lab_of(lab64, s1, epoch))
+                              : (deg[s1] > deg[s0] ? s1 : s0);
     keys[p] = bin;
     tick[p] = atomicAdd(hist2 + bin, 1);
 }
 void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
-                             const int32_t* lab, int32_t* keys, int32_t* tick, int32_t* hist2,
-                             int64_t npairs, hipStream_t s) {
+                             const uint64_t* lab64, uint32_t epoch, int32_t* keys, int32_t* tick,
+                             int32_t* hist2, int64_t npairs, hipStream_t s) {
     plan_degree_key_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        plans, pairs2, deg, lab, keys, tick, hist2, npairs);
+        plans, pairs2, deg, lab64, epoch, keys, tick, hist2, npairs);
 }
 
 // One round of label propagation over the parent graph (rows = vertices, a
 // pair's two parents = an edge): every parent takes the smallest label among
-// itself and its pair partner.  lab holds INT32_MAX - label, zeroed = unset
-// (one memset with the degree counts): a row's label is
-// min(INT32_MAX - lab[row], row).  In place -- the rounds are a heuristic for
-// locality, any interleaving of the atomics is a valid labelling and the
-// order never changes a child.  The first round runs inside the plan kernel.
+// itself and its pair partner (lab_of / lab_lower above: epoch-tagged, never
+// zeroed).  In place -- the rounds are a heuristic for locality, any
+// interleaving of the atomics is a valid labelling and the order never changes
+// a child.  The first round runs inside the plan kernel.
 __global__ __launch_bounds__(256) void plan_label_kernel(const int2* __restrict__ pairs2,
-                                                         int32_t* __restrict__ lab, int64_t npairs) {
+                                                         uint64_t* __restrict__ lab64,
+                                                         uint32_t epoch, int64_t npairs) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npairs) return;
     const int2 pr = pairs2[p];
     const int32_t s0 = pr.x, s1 = pr.y;
-    const int32_t l0 = min(INT32_MAX - lab[s0], s0), l1 = min(INT32_MAX - lab[s1], s1);
+    const int32_t l0 = lab_of(lab64, s0, epoch), l1 = lab_of(lab64, s1, epoch);
     const int32_t m = min(l0, l1);
-    if (m < l0) atomicMax(lab + s0, INT32_MAX - m);
-    if (m < l1) atomicMax(lab + s1, INT32_MAX - m);
+    if (m < l0) lab_lower(lab64, s0, m, epoch);
+    if (m < l1) lab_lower(lab64, s1, m, epoch);
 }
-void launch_plan_labels(const int2* pairs2, int32_t* lab, int64_t npairs, int rounds,
-                        hipStream_t s) {
+void launch_plan_labels(const int2* pairs2, uint64_t* lab64, uint32_t epoch, int64_t npairs,
+                        int rounds, hipStream_t s) {
     for (int r = 0; r < rounds; ++r)
-        plan_label_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(pairs2, lab, npairs);
+        plan_label_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(pairs2, lab64,
+                                                                                 epoch, npairs);
 }
 
 void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t* tick,
