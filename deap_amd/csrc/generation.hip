@@ -197,19 +197,22 @@ int launch_generation(dm_ctx* ctx, const dm_pop* parents, dm_pop* children, int3
                 int2* pairs2 = (int2*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));  // 2 kb
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
                                   nullptr, nullptr, nullptr, lab64, epoch, pairs2, hist, a.np + 1);
-                if (ctx->knobs.pipe_label_rounds > 1)
-                    launch_plan_labels(pairs2, lab64, epoch, npairs, ctx->knobs.pipe_label_rounds - 1,
-                                       ctx->stream);
-                launch_plan_degree_keys(plans, pairs2, nullptr, lab64, epoch, keys, tick, hist,
-                                        npairs, ctx->stream);
+                // DM_PIPE_LABEL_ROUNDS = r: round 1 in the plan kernel; r >= 2: r - 2
+                // scatter rounds (plan_label_kernel, atomics) and the gather jump in
+                // the key kernel (the default r = 2: no label kernel)
+                const int rounds = ctx->knobs.pipe_label_rounds;
+                if (rounds > 2)
+                    launch_plan_labels(pairs2, lab64, epoch, npairs, rounds - 2, ctx->stream);
+                launch_plan_degree_keys(plans, pairs2, nullptr, lab64, epoch, rounds >= 2, keys,
+                                        tick, hist, npairs, ctx->stream);
             } else if (!ctx->knobs.pipe_key_fitter) {
                 // DM_PIPE_LABEL_ROUNDS=0: degree keys (counted into the zeroed deg)
                 int32_t* deg = (int32_t*)((char*)stemp + align_up(scan_temp_bytes(a.np), 256));
                 zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, deg, a.np);
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream,
                                   nullptr, deg);
-                launch_plan_degree_keys(plans, nullptr, deg, nullptr, 0, keys, tick, hist, npairs,
-                                        ctx->stream);
+                launch_plan_degree_keys(plans, nullptr, deg, nullptr, 0, false, keys, tick, hist,
+                                        npairs, ctx->stream);
             } else {
                 zero2_kernel<<<zg, 256, 0, ctx->stream>>>(hist, nullptr, a.np);
                 launch_pair_plans(a, plans, count ? ctx->evals_spread : nullptr, ctx->stream, keys,

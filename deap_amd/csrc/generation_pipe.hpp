@@ -584,9 +584,11 @@ void launch_plan_order(const PairPlan* plans, const int32_t* keys, const int32_t
 // Degree keys (the default; DM_PIPE_KEY_FITTER keys by the fitter parent in
 // the plan kernel instead): after launch_pair_plans(..., hist = deg) counted
 // every parent slot, key[p] = the parent of more slots, ticketed into hist2.
+// jump: the bin also takes the labels of the parents' labels (one more
+// propagation round as gathers)
 void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
-                             const uint64_t* lab64, uint32_t epoch, int32_t* keys, int32_t* tick,
-                             int32_t* hist2, int64_t npairs, hipStream_t s);
+                             const uint64_t* lab64, uint32_t epoch, bool jump, int32_t* keys,
+                             int32_t* tick, int32_t* hist2, int64_t npairs, hipStream_t s);
 void launch_plan_labels(const int2* pairs2, uint64_t* lab64, uint32_t epoch, int64_t npairs,
                         int rounds, hipStream_t s);
 void launch_gen_bits_fused(const GenArgs& a, bool eval, long long* spread, hipStream_t s);

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __
                                                               const int2* __restrict__ pairs2,
                                                               const int32_t* __restrict__ deg,
                                                               const uint64_t* __restrict__ lab64,
-                                                              uint32_t epoch,
+                                                              uint32_t epoch, int jump,
                                                               int32_t* __restrict__ keys,
                                                               int32_t* __restrict__ tick,
                                                               int32_t* __restrict__ hist2,
@@ -265,16 +265,27 @@ __global__ __launch_bounds__(256) void plan_degree_key_kernel(const PairPlan* __
     if (p >= npairs) return;
     const int2 pr = pairs2 ? pairs2[p] : make_int2(plans[p].s0, plans[p].s1);
     const int32_t s0 = pr.x, s1 = pr.y;
-    const int32_t bin = lab64 ? min(lab_of(lab64, s0, epoch), lab_of(lab64, s1, epoch))
-                              : (deg[s1] > deg[s0] ? s1 : s0);
+    int32_t bin;
+    if (lab64) {
+        const int32_t l0 = lab_of(lab64, s0, epoch), l1 = lab_of(lab64, s1, epoch);
+        bin = min(l0, l1);
+        // jump: the labels of the two labels (rows themselves) -- a second
+        // propagation round as gathers, no atomics: the label kernel's round
+        // took 27 us, 22 of them its random atomics (profiles/r06_prelude),
+        // and a jump groups the pairs as well (tools_gpu/plan_order_sim.py:
+        // 0.657 of the parent reads left at runs of 64, as a second round)
+        if (jump) bin = min(bin, min(lab_of(lab64, l0, epoch), lab_of(lab64, l1, epoch)));
+    } else {
+        bin = deg[s1] > deg[s0] ? s1 : s0;
+    }
     keys[p] = bin;
     tick[p] = atomicAdd(hist2 + bin, 1);
 }
 void launch_plan_degree_keys(const PairPlan* plans, const int2* pairs2, const int32_t* deg,
-                             const uint64_t* lab64, uint32_t epoch, int32_t* keys, int32_t* tick,
-                             int32_t* hist2, int64_t npairs, hipStream_t s) {
+                             const uint64_t* lab64, uint32_t epoch, bool jump, int32_t* keys,
+                             int32_t* tick, int32_t* hist2, int64_t npairs, hipStream_t s) {
     plan_degree_key_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        plans, pairs2, deg, lab64, epoch, keys, tick, hist2, npairs);
+        plans, pairs2, deg, lab64, epoch, jump ? 1 : 0, keys, tick, hist2, npairs);
 }
 
 // One round of label propagation over the parent graph (rows = vertices, a

@@ -426,7 +426,8 @@ def test_c4_migration_at_full_size(gpu):
 
 
 @pytest.mark.parametrize("knob", ["DM_PIPE_NOORDER", "DM_PIPE_LABEL_ROUNDS=0",
-                                  "DM_PIPE_LABEL_ROUNDS=3", "DM_PIPE_KEY_FITTER"])
+                                  "DM_PIPE_LABEL_ROUNDS=1", "DM_PIPE_LABEL_ROUNDS=3",
+                                  "DM_PIPE_KEY_FITTER"])
 def test_plan_orders_give_identical_children(gpu, knob):
     """The C3 hot kernel's plan order -- label-propagation bins (default),
     degree keys, fitter-parent keys, pair order -- only changes which pairs
