@@ -905,12 +905,17 @@ __device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const 
     const int32_t r = pos[u];
     return make_int2(r, nseg[r / (64 * TD_WPW)]);
 }
+// gsq (nullable): gsize[sigma[q]] per q, so the table peel's prologue loads
+// it without a dependent second load
 __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t* nseg, int64_t U,
-                                  int4* qrec, unsigned long long* lastq) {
+                                  int4* qrec, unsigned long long* lastq,
+                                  const int32_t* sigma = nullptr, const int32_t* gsize = nullptr,
+                                  int32_t* gsq = nullptr) {
     DGRID_LOOP(q, U) {
         const int4 s = S[q];
         qrec[q] = make_int4(nseg[q / (64 * TD_WPW)], span[q].y, s.x, s.y);
         if (lastq) lastq[q] = 0;  // the sliced peels' (front, last position) per v
+        if (gsq) gsq[q] = gsize[sigma[q]];
     }
 }
 
@@ -1290,6 +1295,7 @@ struct TabArgs {
     const uint16_t* BK;
     const int4* qrec;
     const int32_t* gsize;
+    const int32_t* gsq;  // gsize[sigma[q]] per q (member_rec_kernel)
     const int32_t* sigma;
     const int32_t* pos;  // U index -> q
     int32_t* countq;
@@ -1587,8 +1593,28 @@ __device__ void tab_sort_front(const TabArgs& a, int32_t j, char* smem, TabScala
 }
 
 // Search workgroup aw of launch j >= 1 (see the top of this section).
+#ifdef DM_PEEL_PROF
+// search workgroup stamps (diagnostic builds): aw, j, n, start, state read,
+// search done, end (after the sort for the last arriver), 1 + 2 last
+__device__ void sprof_rec(int aw, int32_t j, int32_t n, unsigned long long t0,
+                          unsigned long long t1, unsigned long long t2, bool last) {
+    const unsigned long long t3 = wall_clock64();
+    if (threadIdx.x != 0) return;
+    const unsigned int e = atomicAdd(&g_pprof_n, 1u);
+    if (e < (1u << 17)) {
+        unsigned long long* o = g_pprof + (size_t)e * 8;
+        o[0] = aw; o[1] = j; o[2] = n; o[3] = t0; o[4] = t1; o[5] = t2; o[6] = t3;
+        o[7] = 1 + 2 * (unsigned long long)last + ((unsigned long long)j << 8);
+    }
+}
+#define SPROF(last) sprof_rec(aw, j, sc.n, st0, st1, st2, last)
+#else
+#define SPROF(last)
+#endif
+
 template <int F>
 __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabScalars& sc) {
+    PPROF_T(st0);
     const int tid = threadIdx.x;
     const int buf = j % 3;
     if (tid == 0) {
@@ -1598,6 +1624,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
     }
     __syncthreads();
     if (!sc.go) return;
+    PPROF_T(st1);
     const int32_t n = sc.n;
     if (n == 0) {  // nothing released: every fit is in a front
         if (aw == 0 && tid == 0) {
@@ -1684,12 +1711,16 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
     }
     // every key stored (coherently) before this workgroup counts itself in
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PPROF_T(st2);
     __syncthreads();
     if (tid == 0)
         sc.last = __hip_atomic_fetch_add(a.sum->arrive + buf, 1, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) == TAB_NA - 1;
     __syncthreads();
-    if (!sc.last) return;
+    if (!sc.last) {
+        SPROF(false);
+        return;
+    }
     if (!BD_OK(sc.sf.ustart + (int64_t)n - 1, a.U, "tab front end")) return;
     if (n > TAB_ORDER_CAP) {
         if (tid == 0) sc.smax = 0;
@@ -1705,6 +1736,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
         return;
     }
     tab_sort_front<TAB_NT>(a, j, smem, sc);
+    SPROF(true);
 }
 
 // The members [wb, we) of the front being peeled (member i at slot bbase +
@@ -1773,13 +1805,18 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
         }
     }
     const int64_t v = c * BD_CW + tid;
+    // v's count, U index, individuals and record, all in flight with the state
+    // read (no dependent second load: the record is needed only if v is
+    // released, but a load after the count update would lengthen the release)
     int32_t pcnt = 0, pvu = 0, pgs = 0;
+    int4 rq = make_int4(0, 0, 0, 0);
     if (v < U) {
         pcnt = a.countq[v];
         pvu = a.sigma[v];
-        if (!BD_OK(pvu, U, "tab sigma")) pvu = 0;
-        pgs = a.gsize[pvu];
+        pgs = a.gsq[v];
+        rq = a.qrec[v];
     }
+    if (!BD_OK(pvu, U, "tab sigma")) pvu = 0;
     __syncthreads();
     if (!sc.go) return;
     const int32_t n = sc.n;
@@ -1860,8 +1897,6 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
             fresh = old == d;
         }
     }
-    int4 rq = make_int4(0, 0, 0, 0);
-    if (fresh) rq = a.qrec[v];  // in flight across the slot reservation
     const uint64_t fm = __ballot(fresh);
     int64_t gs = fresh ? pgs : 0;
 #pragma unroll
@@ -1901,7 +1936,8 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
         const unsigned int e = atomicAdd(&g_pprof_n, 1u);
         if (e < (1u << 17)) {
             unsigned long long* o = g_pprof + (size_t)e * 8;
-            o[0] = c; o[1] = y; o[2] = n; o[3] = pt0; o[4] = pt1; o[5] = pt2; o[6] = pt3; o[7] = 0;
+            o[0] = c; o[1] = y; o[2] = n; o[3] = pt0; o[4] = pt1; o[5] = pt2; o[6] = pt3;
+            o[7] = (unsigned long long)j << 8;
         }
     }
 #endif
@@ -2234,9 +2270,12 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
         a.epoch = ++epochs;
     } while (a.epoch == 0);
     DM_HIP(hipMemsetAsync(p + W.pages, 0, CAND_PAGE * (1 + 3 * CAND_BUCKETS), s));
+    // gsq: gsize[sigma[q]] in the D peel's member-row area (unused by this peel)
+    int32_t* gsq = (int32_t*)(ws + L.mrow);
+    a.gsq = gsq;
     member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
                                              (const int32_t*)(ws + L.nseg), U, (int4*)(ws + L.qrec),
-                                             nullptr);
+                                             nullptr, a.sigma, gsize, gsq);
     tab_front0_kernel<<<dg1(U), 256, 0, s>>>(a, F0, sorted0);
     char* hbuf = (char*)pinned(ctx, 2048);
     if (!hbuf) return DM_ERR_NOMEM;
