@@ -618,7 +618,7 @@ def peel_work(wv, fronts, peel_us):
             "by_front": [[a, b, round(b / c, 1) if c else None] for a, b, c in rows]}
 
 
-def peel_report(peel_us, usz, m=3):
+def peel_report(peel_us, usz, m=3, chain_ms=None):
     """C5's dominant kernel, the table-fed front peel (dominance.hip
     peel_order_kernel): one launch per front; launch i peels front i (usz[i]
     unique fitnesses), releasing front i + 1, and -- in its search workgroups
@@ -628,14 +628,19 @@ def peel_report(peel_us, usz, m=3):
     SIMD x 2.4 GHz / 2 clk per wave64 instruction on SIMD-32): the
     instructions per selection come from the PMC pass committed in
     profiles/c5_peel_pmc.json (SQ_INSTS_VALU summed over one selection's peel
-    launches), the time from the live events.  Also: microseconds per launch
-    against the front size (floor + slope)."""
+    launches), the time from live events: chain_ms, the batches of launches
+    each bracketed by ONE event pair (launches plus the ~2 us gaps between
+    them; round 6), when given -- the per-launch pairs behind peel_us add ~5
+    us to every launch (profiles/r06_c5), so they give the per-front shape
+    (floor + slope) but overstate the time."""
     import numpy as np
     nf = len(usz)
     work = [(usz[i], peel_us[i]) for i in range(min(nf, len(peel_us)))]
-    tot_ms = sum(peel_us) / 1e3
+    ev_ms = sum(peel_us) / 1e3
+    tot_ms = chain_ms if chain_ms else ev_ms
     fit = np.polyfit([w[0] for w in work], [w[1] for w in work], 1) if len(work) > 2 else (0, 0)
     fronts = {"launches": len(peel_us), "fronts": nf, "ms_per_selection": round(tot_ms, 4),
+              "ms_per_selection_per_launch_events": round(ev_ms, 4),
               "us_per_launch_mean": round(sum(peel_us) / max(1, len(peel_us)), 2),
               "us_floor": round(float(fit[1]), 2), "us_per_1000_members": round(float(fit[0]) * 1e3, 2),
               "by_front": [[int(a), round(b, 1)] for a, b in work]}
@@ -856,10 +861,23 @@ def bench_nsga2(args, world=1, rank=0, local=0):
     _lib.call("dm_ctx_set_timing", ctx, 0)
     _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_GENERATION)
     peel_us = [t * 1e3 for t in ptimes[:min(cap, pcnt.value)]]
+    # the chain without per-launch events (an event pair around each batch of
+    # launches: the GPU time of the launches and the gaps between them; the
+    # per-launch pairs above add ~5 us to each launch, profiles/r06_c5)
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_PEEL_CHAIN)
+    _lib.call("dm_ctx_set_timing", ctx, 64)
+    tools.selNSGA2(two, n)
+    torch.cuda.synchronize()
+    ctimes = (ctypes.c_float * 64)()
+    ccnt = ctypes.c_int32(0)
+    _lib.call("dm_ctx_kernel_times", ctx, ctimes, 64, ctypes.byref(ccnt))
+    _lib.call("dm_ctx_set_timing", ctx, 0)
+    _lib.call("dm_ctx_set_timing_target", ctx, _lib.DM_TIME_GENERATION)
+    chain_ms = sum(ctimes[:min(64, ccnt.value)])
     sel_fronts = tools.sortNondominated(two, n)
     wvh = two.wvalues[:2 * n].cpu().numpy()
     usz = [int(len(np.unique(wvh[f.cpu().numpy()], axis=0))) for f in sel_fronts]
-    peel = peel_report(peel_us, usz, m)
+    peel = peel_report(peel_us, usz, m, chain_ms)
     peel["fronts"]["work"] = peel_work(wvh, sel_fronts, peel_us)
     fronts = tools.sortNondominated(two, 2 * n)
     wv = two.wvalues[:2 * n]
@@ -912,7 +930,7 @@ def bench_nsga2(args, world=1, rank=0, local=0):
                          "what": "whole selNSGA2(2N -> N): ranks, bitset tables, counts, peel, "
                                  "crowding, last-front selection"},
            "cpu_baseline": None}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("c3", "c3r", "c2"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_nsga2(wv.cpu().numpy(), (-1.0,) * m, n)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -1017,7 +1035,7 @@ def bench_nsga2_example(args, world=1, rank=0, local=0):
                         "kernel": "bounded_vary_kernel (varBounded)",
                         "kernel_ms": round(v_ms, 5)},
            "cpu_baseline": None}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("c3", "c3r", "c2"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the loop's CPU cost is its selNSGA2 (selTournamentDCD and the bounded
         # operators of 2^17 individuals take seconds): the C5 baseline applies
         out["cpu_baseline"] = cpu_baseline_nsga2(two.wvalues[:2 * n].cpu().numpy(), (-1.0,) * m,

@@ -23,7 +23,7 @@ DM_CX_NONE, DM_CX_TWOPOINT, DM_CX_BLEND = 0, 1, 2
 DM_MUT_NONE, DM_MUT_FLIPBIT, DM_MUT_GAUSSIAN = 0, 1, 2
 DM_SEL_IDENTITY, DM_SEL_INDEX, DM_SEL_TOURNAMENT, DM_SEL_RANDOM = 0, 1, 2, 3
 DM_RNG_NATIVE, DM_RNG_INJECT, DM_RNG_DUMP = 0, 1, 2
-DM_TIME_GENERATION, DM_TIME_DOMINANCE, DM_TIME_PEEL = 0, 1, 2
+DM_TIME_GENERATION, DM_TIME_DOMINANCE, DM_TIME_PEEL, DM_TIME_PEEL_CHAIN = 0, 1, 2, 3
 # enum dm_dom_path: sortNondominated's default path and its cross-check paths
 DM_DOM_PATHS = {"default": 0, "compare": 1, "peel_d": 2, "ballot": 3, "lds": 4}
 (DM_EVAL_NONE, DM_EVAL_ONEMAX, DM_EVAL_RASTRIGIN, DM_EVAL_ROSENBROCK, DM_EVAL_ZDT1,

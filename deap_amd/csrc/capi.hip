@@ -545,7 +545,7 @@ int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches) {
 }
 
 int dm_ctx_set_timing_target(dm_ctx* ctx, int32_t target) {
-    DM_CHECK_ARG(ctx != nullptr && (target >= DM_TIME_GENERATION && target <= DM_TIME_PEEL),
+    DM_CHECK_ARG(ctx != nullptr && (target >= DM_TIME_GENERATION && target <= DM_TIME_PEEL_CHAIN),
                  "bad timing target %d", target);
     ctx->timing_target = target;
     return DM_OK;

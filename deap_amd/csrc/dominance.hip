@@ -2293,6 +2293,7 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
     const unsigned grid = (unsigned)(TAB_NA + a.gx * PEEL_SLICES);
     int32_t j = 0;  // the next launch's front
     for (;;) {
+        timing_begin(ctx, DM_TIME_PEEL_CHAIN);
         for (int b = 0; b < batch; ++b) {
             timing_begin(ctx, DM_TIME_PEEL);
             if (m == 2)
@@ -2301,6 +2302,7 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
                 peel_order_kernel<2><<<grid, TAB_NT, 0, s>>>(a, j + b);
             timing_end(ctx, DM_TIME_PEEL);
         }
+        timing_end(ctx, DM_TIME_PEEL_CHAIN);
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hsum, a.sum, sizeof(FrontSum), hipMemcpyDeviceToHost, s));
         DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));
@@ -2407,6 +2409,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
     const int trend = hinted ? std::max(0, std::min(ctx->peel_trend, 4)) : 0;
     int batch = std::max(2, std::min(hint + 1 + trend, PEEL_BATCH_MAX));
     for (;;) {
+        timing_begin(ctx, DM_TIME_PEEL_CHAIN);
         for (int b = 0; b < batch; ++b) {
             timing_begin(ctx, DM_TIME_PEEL);
             peel_owned_kernel<<<dim3((unsigned)L.NQ, PEEL_SLICES), PEEL_WAVES * 64, 0, s>>>(
@@ -2414,6 +2417,7 @@ int fast_fronts(dm_ctx* ctx, const uint64_t* D, int m, int64_t n, int64_t U, con
             timing_end(ctx, DM_TIME_PEEL);
             front_order_kernel<<<1, 1024, 0, s>>>(st, ckey, cq, ulist, mrow, pos, nseg, fstarts, 0);
         }
+        timing_end(ctx, DM_TIME_PEEL_CHAIN);
         DM_LAUNCH_CHECK();
         DM_HIP(hipMemcpyAsync(hst, st, sizeof(FrontState), hipMemcpyDeviceToHost, s));
         DM_HIP(hipMemcpyAsync(hfs, fstarts, (size_t)npre * 4, hipMemcpyDeviceToHost, s));

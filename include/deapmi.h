@@ -159,10 +159,17 @@ int dm_ctx_set_timing(dm_ctx* ctx, int32_t max_launches);
 int dm_ctx_kernel_times(dm_ctx* ctx, float* ms, int32_t cap, int32_t* count);
 /* Which launches the event pairs bracket: DM_TIME_GENERATION (default, the
  * dm_generation kernel), DM_TIME_DOMINANCE (the all-pairs dominance kernel of
- * dm_sort_nondominated / dm_sel_nsga2) or DM_TIME_PEEL (every front-peel
+ * dm_sort_nondominated / dm_sel_nsga2), DM_TIME_PEEL (every front-peel
  * launch of the bitset path, in front order; launches issued after the last
- * front exit at once). */
-enum dm_time_target { DM_TIME_GENERATION = 0, DM_TIME_DOMINANCE = 1, DM_TIME_PEEL = 2 };
+ * front exit at once) or DM_TIME_PEEL_CHAIN (each batch of peel launches as
+ * one pair). */
+enum dm_time_target {
+    DM_TIME_GENERATION = 0,
+    DM_TIME_DOMINANCE = 1,
+    DM_TIME_PEEL = 2,
+    DM_TIME_PEEL_CHAIN = 3 /* each batch of front-peel launches as one pair: the chain's GPU time
+                              without per-launch events (each event pair adds ~5 us) */
+};
 int dm_ctx_set_timing_target(dm_ctx* ctx, int32_t target);
 /* Dominance path of dm_sort_nondominated / dm_sel_nsga2 (and the log
  * versions): DM_DOM_DEFAULT (bitset tables + table-fed peel for 2-3
