@@ -351,6 +351,7 @@ __global__ void set_fitness_kernel(double* wv, uint8_t* valid, int nobj, int64_t
 struct StatAcc {
     double mn, mx, mean, m2, sum;
     int64_t amn, amx, cnt, nan;
+    int64_t anan;  // first row holding NaN (numpy's argmin / argmax return it), -1: none
 };
 __device__ __forceinline__ void stat_merge(StatAcc& x, const StatAcc& y) {
     if (y.amn >= 0 && (x.amn < 0 || y.mn < x.mn || (y.mn == x.mn && y.amn < x.amn))) {
@@ -370,19 +371,21 @@ __device__ __forceinline__ void stat_merge(StatAcc& x, const StatAcc& y) {
     }
     x.sum += y.sum;
     x.nan += y.nan;
+    if (y.anan >= 0 && (x.anan < 0 || y.anan < x.anan)) x.anan = y.anan;
 }
 __global__ __launch_bounds__(256) void stats_kernel(const double* wv, const uint8_t* valid,
                                                     int64_t n, int nobj, dm_eval w, StatAcc* part,
                                                     int64_t nparts) {
     // w.weights: the fitness weights (values = wvalues / weights, base.py:184-185)
     const int o = blockIdx.y;
-    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0};
+    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0, -1};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (!valid[i]) continue;
         const double v = wv[i * nobj + o] / w.weights[o];
         if (v != v) {
             ++a.nan;
+            if (a.anan < 0) a.anan = i;  // rows ascend per thread
             continue;
         }
         if (a.amn < 0 || v < a.mn) {
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(256) void stats_combine_kernel(const StatAcc* part,
                                                             int nobj, double* out) {
     const int o = blockIdx.x;
     __shared__ StatAcc sh[256];
-    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0};
+    StatAcc a{INFINITY, -INFINITY, 0.0, 0.0, 0.0, -1, -1, 0, 0, -1};
     for (int64_t b = threadIdx.x; b < nparts; b += blockDim.x)  // nparts <= 1024
         stat_merge(a, part[(int64_t)o * nparts + b]);
     sh[threadIdx.x] = a;
@@ -434,8 +437,8 @@ __global__ __launch_bounds__(256) void stats_combine_kernel(const StatAcc* part,
     q[2] = nan || a.cnt == 0 ? qnan : a.mean;
     q[3] = nan || a.cnt == 0 ? qnan : a.m2;
     q[4] = nan ? qnan : a.sum;
-    q[5] = (double)a.amn;
-    q[6] = (double)a.amx;
+    q[5] = (double)(nan ? a.anan : a.amn);  // numpy: the first NaN is both arg-extrema
+    q[6] = (double)(nan ? a.anan : a.amx);
     q[7] = (double)(a.cnt + a.nan);
 }
 

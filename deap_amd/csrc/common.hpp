@@ -186,7 +186,7 @@ enum Stage : uint32_t {
     ST_VAROR = 8,   // varOr op choice + indices: item = child
     ST_INIT = 9,    // initial population
     ST_DCD = 10,    // selTournamentDCD: tie coins (item = tournament slot, sub = 2),
-                    // permutation q's Feistel rounds (item = half-word, sub = 3 + 4 q + round)
+                    // permutation q's sort keys (item = index, sub = 4 + q)
     ST_SBX_PAIR = 11,  // NSGA-II loop pair random() <= cxpb: item = pair
     ST_SBX = 12,       // cxSimulatedBinaryBounded per gene: item = pair, sub = gene
                        // (| 1 << 24 for the swap coin)

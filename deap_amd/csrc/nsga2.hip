@@ -1184,35 +1184,22 @@ __device__ __forceinline__ bool dominates_wv(const double* a, const double* b, i
     return not_equal;
 }
 
-// random.sample(individuals, len(individuals)) twice (emo.py:186-187):
-// permutation q of [0, n) as a keyed pseudo-random permutation -- a 4-round
-// balanced Feistel network on 2 hb bits (2^(2 hb) >= n) whose round
-// functions are Philox draws (stage ST_DCD, item = the right half, sub =
-// 3 + 4 q + round), cycle-walked into [0, n) (x = F(x) until x < n: a
-// bijection of [0, n), expected under four steps since 2^(2 hb) < 4 n).  One
-// pass where sorting 2 n 64-bit Philox keys took a batched 8-pass radix sort.
-__device__ __forceinline__ uint32_t dcd_feistel(const Rng& rng, uint32_t q, uint32_t x, int hb,
-                                                uint32_t mask) {
-    uint32_t L = x >> hb, R = x & mask;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t f = rng(ST_DCD, R, 3u + 4u * q + (uint32_t)r).x & mask;
-        const uint32_t t = L ^ f;
-        L = R;
-        R = t;
-    }
-    return (L << hb) | R;
-}
-__global__ void dcd_perm_kernel(Rng rng, int64_t n, int hb, int32_t* p1, int32_t* p2) {
-    const uint32_t mask = (1u << hb) - 1u;
+// random.sample(individuals, len(individuals)) twice (emo.py:186-187): the
+// permutations are the orders of 2 n Philox keys (stage ST_DCD, item = i, sub
+// = 4 + q), sorted as ONE batched radix sort of two segments (stable: a tie of
+// two 64-bit keys keeps index order).  Uniform random keys give uniformly
+// distributed permutations, as random.sample's are.  (Round 5 used a keyed
+// 4-round Feistel network cycle-walked into [0, n) instead -- one pass, but a
+// simulation of it with ideal round functions (tools_gpu/dcd_perm_sim.py) puts
+// the position-of-i histogram 11-31 % off uniform at n = 5..33 (chi-square p
+// < 1e-12): not random.sample's distribution; removed in round 6.)
+__global__ void dcd_keys_kernel(Rng rng, int64_t n, uint64_t* keys, int32_t* vals) {
     GRID_LOOP(t, 2 * n) {
         const uint32_t q = t >= n ? 1u : 0u;
         const int64_t i = t - (int64_t)q * n;
-        uint32_t x = (uint32_t)i;
-        do {
-            x = dcd_feistel(rng, q, x, hb, mask);
-        } while ((int64_t)x >= n);
-        (q ? p2 : p1)[i] = (int32_t)x;
+        const u32x4 w = rng(ST_DCD, (uint32_t)i, 4u + q);
+        keys[t] = ((uint64_t)w.x << 32) | w.y;
+        vals[t] = (int32_t)i;
     }
 }
 
@@ -1286,18 +1273,28 @@ extern "C" int dm_sel_tournament_dcd(dm_ctx* ctx, const dm_pop* pop, const doubl
     if (k == 0) return DM_OK;
     hipStream_t s = ctx->stream;
     if (mode != DM_RNG_INJECT) {
-        // random.sample(individuals, len(individuals)) twice (dcd_perm_kernel)
-        int d = 1;
-        while ((1ll << d) < n) ++d;
-        const int hb = (d + 1) / 2;
-        int32_t* w = nullptr;
-        if (!perm1 || !perm2) {
-            w = (int32_t*)scratch(ctx, 2 * align_up((size_t)n * 4, 256));
-            if (!w) return DM_ERR_NOMEM;
+        // random.sample(individuals, len(individuals)) twice: the two segments'
+        // key orders (dcd_keys_kernel + one batched radix sort)
+        const size_t kb = align_up((size_t)2 * n * 8, 256), vb = align_up((size_t)2 * n * 4, 256);
+        char* w = (char*)scratch(ctx, 2 * kb + 2 * vb + radix_sort_batched_temp_bytes(2, n));
+        if (!w) return DM_ERR_NOMEM;
+        uint64_t* keys = (uint64_t*)w;
+        uint64_t* ktmp = (uint64_t*)(w + kb);
+        int32_t* vals = (int32_t*)(w + 2 * kb);
+        int32_t* vtmp = (int32_t*)(w + 2 * kb + vb);
+        dcd_keys_kernel<<<g1(2 * n), 256, 0, s>>>(Rng(rng), n, keys, vals);
+        bool in_tmp = false;
+        int rc = radix_sort_pairs_batched(s, keys, vals, ktmp, vtmp, 2, n, 0, 64, w + 2 * kb + 2 * vb,
+                                          &in_tmp);
+        if (rc) return rc;
+        const int32_t* sorted = in_tmp ? vtmp : vals;
+        if (perm1 && perm2) {  // dump mode: the caller's buffers
+            DM_HIP(hipMemcpyAsync(perm1, sorted, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+            DM_HIP(hipMemcpyAsync(perm2, sorted + n, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        } else {
+            perm1 = const_cast<int32_t*>(sorted);
+            perm2 = const_cast<int32_t*>(sorted + n);
         }
-        if (!perm1) perm1 = w;
-        if (!perm2) perm2 = (int32_t*)((char*)w + align_up((size_t)n * 4, 256));
-        dcd_perm_kernel<<<g1(2 * n), 256, 0, s>>>(Rng(rng), n, hb, perm1, perm2);
     }
     dcd_kernel<<<g1(k4), 256, 0, s>>>(pop->wvalues, pop->nobj, crowd, perm1, perm2, k4, Rng(rng),
                                       mode, coin, out_idx);

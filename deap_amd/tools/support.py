@@ -89,9 +89,14 @@ class Statistics:
                 out[name] = functools.partial(kstats.value, fn.func, axis)
                 continue
             # any other reducer: the reference's call on host values (one copy
-            # of the weighted fitness, divided by the weights on the host)
+            # of the weighted fitness, divided by the weights on the host) of the
+            # VALID rows, as dm_fitness_stats reduces them (an invalid
+            # individual's fitness.values is (), which the reference's numpy
+            # reducers cannot combine with the others at all)
             if host is None:
-                host = tuple(tuple(r) for r in pop.fitness_values().numpy().tolist())
+                vals = pop.fitness_values().numpy()
+                ok = pop.valid[:len(pop)].cpu().numpy().astype(bool)
+                host = tuple(tuple(r) for r in vals[ok].tolist())
             out[name] = fn(host)
         return out
 
@@ -153,8 +158,11 @@ def _combined(func, rows, nobj):
     total = np.sum(cnt)
     if func in (np.argmin, np.argmax):
         ext, arg = (mn, amn) if func is np.argmin else (mx, amx)
-        best = np.min(ext) if func is np.argmin else np.max(ext)
-        flat = [int(arg[o]) * nobj + o for o in range(nobj) if ext[o] == best]
+        if np.isnan(ext).any():  # numpy: the first NaN in flattened order
+            flat = [int(arg[o]) * nobj + o for o in range(nobj) if np.isnan(ext[o])]
+        else:
+            best = np.min(ext) if func is np.argmin else np.max(ext)
+            flat = [int(arg[o]) * nobj + o for o in range(nobj) if ext[o] == best]
         return np.int64(min(flat)) if flat else np.int64(0)
     if not total:
         return np.float64("nan")

@@ -438,7 +438,8 @@ int dm_mig_ring_rccl(dm_ctx* ctx, dm_comm* comm, int32_t n_local, dm_pop* demes,
  * m2 = sum of squared deviations from the mean (np.var = m2 / count,
  * np.std = sqrt(np.var)), combined pairwise (Chan et al.); argmin / argmax
  * are first occurrences; a NaN value makes min / max / mean / m2 / sum NaN
- * as numpy's reducers do.  weights: host [nobj].  Asynchronous. */
+ * and argmin / argmax the first NaN row, as numpy's reducers do.  weights:
+ * host [nobj].  Asynchronous. */
 int dm_fitness_stats(dm_ctx* ctx, const dm_pop* pop, const double* weights,
                      double* out);
 

@@ -860,13 +860,46 @@ def test_sel_tournament_dcd_native_replays_in_oracle(gpu):
     assert np.array_equal(again, got)
     # each individual appears at most twice per permutation pass (4 per call)
     assert np.bincount(got, minlength=n).max() <= 4
-    # the permutations (keyed Feistel networks, cycle-walked into [0, n)) carry
-    # no trace of the identity or of each other
+    # the permutations (orders of Philox keys) carry no trace of the identity
+    # or of each other
     idx = np.arange(n)
     for p in (p1, p2):
         assert abs(np.corrcoef(idx, p)[0, 1]) < 0.02
         assert (p == idx).sum() < 10
     assert abs(np.corrcoef(p1, p2)[0, 1]) < 0.02
+
+
+@pytest.mark.parametrize("n", [5, 12, 33])
+def test_sel_tournament_dcd_permutations_are_uniform(gpu, n):
+    """random.sample(individuals, len(individuals)) draws uniform permutations
+    (emo.py:186-187): over 3,000 streams the position-of-i histogram of both
+    permutations passes a chi-square test against the uniform one, and every
+    pair (i, j) comes in either order half of the time.  (Round 5's Feistel
+    permutations failed this at p < 1e-12, tools_gpu/dcd_perm_sim.py.)"""
+    from scipy.stats import chi2
+    from deap_amd import tools
+    from deap_amd.ops import RandomStream
+    rng = np.random.default_rng(n)
+    pop = _dcd_pop(rng.random((n, 2)), rng.random(n))
+    S = 3000
+    h = np.zeros((2, n, n))
+    before = np.zeros((n, n))
+    k = n - n % 4
+    for s in range(S):
+        dec = {}
+        tools.selTournamentDCD(pop, k, mode="dump", decisions=dec, stream=RandomStream(1000 + s))
+        for q, key in enumerate(("perm1", "perm2")):
+            p = dec[key].cpu().numpy()
+            h[q, np.arange(n), p] += 1
+            if q == 0:
+                inv = np.argsort(p)
+                before += inv[:, None] < inv[None, :]
+    e = S / n
+    for q in range(2):
+        stat = ((h[q] - e) ** 2 / e).sum()
+        assert chi2.sf(stat, (n - 1) ** 2) > 1e-4, (q, stat)
+    freq = before[np.triu_indices(n, 1)] / S
+    assert np.all(np.abs(freq - 0.5) < 5 * np.sqrt(0.25 / S)), freq
 
 
 def test_sel_tournament_dcd_permutations_small_sizes(gpu):

@@ -108,6 +108,51 @@ def test_fitness_stats_kernel_matches_numpy(gpu, nobj, n):
               (ctypes.c_double * nobj)(*weights), ctypes.c_void_p(out.data_ptr()))
     r = out.cpu().numpy().reshape(nobj, 8)
     assert np.isnan(r[0, [0, 1, 2, 3, 4]]).all()
+    # numpy's argmin / argmax of a column holding NaN: the first NaN
+    assert int(r[0, 5]) == int(r[0, 6]) == np.argmin(wv[:, 0]) == n // 2
+
+
+@pytest.mark.parametrize("nobj", [2, 3])
+@pytest.mark.parametrize("case", ["plain", "nan", "invalid"])
+def test_statistics_over_all_objectives_match_numpy(gpu, nobj, case):
+    """Statistics with axis=None on several objectives: the value
+    numpy gives on the flattened fitness values of the valid rows -- min, max,
+    sum, mean, var, std (combined from the per-objective dm_fitness_stats rows)
+    and argmin / argmax as positions row * nobj + objective of the POPULATION
+    (first occurrence; with a NaN, numpy's first NaN).  An invalid row is
+    skipped: its fitness.values is (), which the reference's numpy reducers
+    cannot combine with the other rows."""
+    from deap_amd import tools
+    n = 5000
+    rng = np.random.default_rng(10 * nobj + len(case))
+    weights = (-1.0, 1.0, 2.0)[:nobj]
+    vals = rng.integers(-50, 50, size=(n, nobj)).astype(np.float64)  # many ties
+    valid = np.ones(n, np.uint8)
+    if case == "nan":
+        vals[1234, nobj - 1] = np.nan
+        vals[3000, 0] = np.nan
+    if case == "invalid":
+        valid[[0, 17, 4999]] = 0
+    pop = _dp().from_numpy(np.zeros((n, 1)), weights=weights, wvalues=vals * np.array(weights),
+                           valid=valid)
+    stats = tools.Statistics(key=lambda ind: ind.fitness.values)
+    funcs = {"min": np.min, "max": np.max, "sum": np.sum, "avg": np.mean, "var": np.var,
+             "std": np.std, "amin": np.argmin, "amax": np.argmax}
+    for k, f in funcs.items():
+        stats.register(k, f)
+    got = {k: v() if callable(v) else v for k, v in stats.compile(pop).items()}
+    rows = np.nonzero(valid)[0]
+    flat = vals[rows].ravel()
+    with np.errstate(invalid="ignore"):
+        for k in ("min", "max", "sum", "avg", "var", "std"):
+            want = funcs[k](flat)
+            if np.isnan(want):
+                assert np.isnan(got[k]), k
+            else:
+                assert _rel_close(got[k], want, 1e-12), (k, got[k], want)
+    for k in ("amin", "amax"):
+        p = int(funcs[k](flat))  # position in the valid rows' flattened values
+        assert int(got[k]) == rows[p // nobj] * nobj + p % nobj, (k, got[k])
 
 
 def _stats_registered():
