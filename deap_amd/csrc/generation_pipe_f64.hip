@@ -30,6 +30,9 @@ __device__ __forceinline__ void lab_lower(uint64_t* lab64, int32_t r, int32_t m,
               ((unsigned long long)epoch << 32) | (uint32_t)(INT32_MAX - m));
 }
 
+// MF: objectives the register tournaments take (1, or up to 3 for the ZDT /
+// DTLZ shapes: pair_plan_kernel<3> for 2-3 objectives, t <= 4)
+template <int MF>
 __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restrict__ plans,
                                              int64_t p, int32_t* __restrict__ keys,
                                              int32_t* __restrict__ hist,
@@ -49,11 +52,71 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
     // and no mutation: 0.4 of the children at cxpb 0.5, mutpb 0.2): the 2t
     // validity bytes loaded beside the fitnesses were half of the kernel's
     // random requests (round 6).
-    bool fast = a.sel == DM_SEL_TOURNAMENT && m == 1 && a.tournsize >= 1 && a.tournsize <= 8;
+    // Several objectives (MF = 3): the same with each aspirant's m values
+    // loaded together and compared lexicographically (Fitness.__gt__ on the
+    // wvalues tuples, base.py:231-238), t <= 4.
+    constexpr int TM = MF == 1 ? 8 : 4;
+    bool fast = a.sel == DM_SEL_TOURNAMENT && (MF == 1 ? m == 1 : (m >= 2 && m <= MF)) &&
+                a.tournsize >= 1 && a.tournsize <= TM;
     double fw[2] = {0.0, 0.0};
     uint8_t vw[2] = {1, 1};
-    if (fast) {
-        constexpr int TM = 8;
+    if (fast && MF > 1) {
+        const int t = a.tournsize;
+        int32_t kk[2][TM];
+        double ff[2][TM][MF];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = (uint32_t)(h ? c1 : c0);
+            u32x4 w{};
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                if (j < t && (h == 0 || has1)) {
+                    if (!(j & 1)) w = a.rng(ST_SEL, c, (uint32_t)(j >> 1));
+                    kk[h][j] = (int32_t)((j & 1) ? bounded64(w.z, w.w, np) : bounded64(w.x, w.y, np));
+                } else {
+                    kk[h][j] = 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int o = 0; o < MF; ++o)
+                    ff[h][j][o] = (j < t && (h == 0 || has1) && o < m)
+                                      ? a.pwv[(int64_t)kk[h][j] * m + o] : 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int b = 0;
+#pragma unroll
+            for (int j = 1; j < TM; ++j) {
+                if (!(j < t && (h == 0 || has1))) continue;
+                // fit_gt(ff[h][j], ff[h][b]) over the first m objectives
+                bool gt = false, decided = false;
+#pragma unroll
+                for (int o = 0; o < MF; ++o) {
+                    double x = ff[h][j][o], y = ff[h][0][o];
+#pragma unroll
+                    for (int q = 1; q < TM; ++q) y = b == q ? ff[h][q][o] : y;
+                    if (!decided && o < m && !(x == y)) {
+                        gt = !(x <= y);
+                        decided = true;
+                    }
+                }
+                if (gt) b = j;
+            }
+            int32_t best = kk[h][0];
+            double fb = ff[h][0][0];
+#pragma unroll
+            for (int q = 1; q < TM; ++q) {
+                best = b == q ? kk[h][q] : best;
+                fb = b == q ? ff[h][q][0] : fb;
+            }
+            s[h] = best;
+            fw[h] = fb;
+        }
+    } else if (fast) {
         const int t = a.tournsize;
         int32_t kk[2][TM];
         double ff[2][TM];
@@ -189,6 +252,7 @@ __device__ __forceinline__ uint32_t plan_one(const GenArgs& a, PairPlan* __restr
 // workgroup.
 // zero (nullable): nzero ints this launch clears for a later one (the parent
 // order's ticket counters: no separate fill launch)
+template <int MF>
 __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __restrict__ plans,
                                                         long long* __restrict__ count_evals,
                                                         int32_t* __restrict__ keys,
@@ -205,7 +269,7 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
     if (count_evals) {
         __shared__ int32_t wave_evals[4];
         uint32_t fl = 0;
-        if (p < npairs) fl = plan_one(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
+        if (p < npairs) fl = plan_one<MF>(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
         const int32_t cnt = __popcll(__ballot((fl & PF_INV0) != 0)) +
                             __popcll(__ballot((fl & PF_INV1) != 0));
         if ((threadIdx.x & 63) == 0) wave_evals[threadIdx.x >> 6] = cnt;
@@ -215,15 +279,20 @@ __global__ __launch_bounds__(256) void pair_plan_kernel(GenArgs a, PairPlan* __r
                        (long long)wave_evals[0] + wave_evals[1] + wave_evals[2] + wave_evals[3]);
         return;
     }
-    if (p < npairs) plan_one(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
+    if (p < npairs) plan_one<MF>(a, plans, p, keys, hist, tick, lab64, epoch, pairs2);
 }
 
 void launch_pair_plans(const GenArgs& a, PairPlan* plans, long long* count_evals, hipStream_t s,
                        int32_t* keys, int32_t* hist, int32_t* tick, uint64_t* lab64,
                        uint32_t epoch, int2* pairs2, int32_t* zero, int64_t nzero) {
     const int64_t npairs = (a.nc + 1) / 2;
-    pair_plan_kernel<<<dim3((unsigned)((npairs + 255) / 256)), 256, 0, s>>>(
-        a, plans, count_evals, keys, hist, tick, lab64, epoch, pairs2, zero, nzero);
+    const dim3 grid((unsigned)((npairs + 255) / 256));
+    if (a.nobj >= 2 && a.nobj <= 3)
+        pair_plan_kernel<3><<<grid, 256, 0, s>>>(a, plans, count_evals, keys, hist, tick, lab64, epoch,
+                                                 pairs2, zero, nzero);
+    else
+        pair_plan_kernel<1><<<grid, 256, 0, s>>>(a, plans, count_evals, keys, hist, tick, lab64, epoch,
+                                                 pairs2, zero, nzero);
 }
 
 // Counting-sort placement of the plans by key: slot start[key] + tick of pair
