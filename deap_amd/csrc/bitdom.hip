@@ -186,7 +186,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_rows_kernel(
     const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
     uint64_t* __restrict__ D) {
     constexpr int F = M - 1;
-    static_assert(F <= 2, "the prefix-set tables of 2-3 objectives fit in LDS");
+    static_assert(F <= 3, "the prefix-set tables of 2-4 objectives fit in LDS (110,988 B at F = 3)");
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
     __shared__ uint16_t sB[F][BD_BKN];
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
     int16_t* __restrict__ part) {
     constexpr int F = M - 1;
-    static_assert(F <= 2, "the prefix-set tables of 2-3 objectives fit in LDS");
+    static_assert(F <= 3, "the prefix-set tables of 2-4 objectives fit in LDS (110,988 B at F = 3)");
     __shared__ uint4 sP[F][BD_K * 4];
     __shared__ int32_t sR[F][BD_RP];
     __shared__ uint16_t sB[F][BD_BKN];
@@ -348,7 +348,7 @@ int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64
                  const int32_t* nseg, const int32_t* sigma, uint64_t* D, int32_t* count,
                  int32_t* countq, char* ws) {
     hipStream_t s = ctx->stream;
-    DM_CHECK_ARG(m >= 2 && m <= 3, "bitdom: 2 or 3 objectives");
+    DM_CHECK_ARG(m >= 2 && m <= 4, "bitdom: 2 to 4 objectives");
     const BitdomLayout L = bitdom_layout(U, m);
     int32_t* first = (int32_t*)(ws + L.first);
     int32_t* last = (int32_t*)(ws + L.last);
@@ -362,7 +362,8 @@ int bitdom_build(dm_ctx* ctx, const int4* S, int m, int64_t U, int64_t NQ, int64
                                       (int32_t*)(ws + L.toffD), (int32_t*)(ws + L.toffC));
     switch (m) {
         case 2: bitdom_launch<2>(ctx, S, U, NQ, L, ws, D); break;
-        default: bitdom_launch<3>(ctx, S, U, NQ, L, ws, D); break;
+        case 3: bitdom_launch<3>(ctx, S, U, NQ, L, ws, D); break;
+        default: bitdom_launch<4>(ctx, S, U, NQ, L, ws, D); break;
     }
     bd_sum_kernel<<<dg1(U), 256, 0, s>>>((const int16_t*)(ws + L.part), span, U, L.Upad, L.NG,
                                          sigma, count, countq);

@@ -910,10 +910,11 @@ __device__ __forceinline__ int2 member_row(int32_t u, const int32_t* pos, const 
 __global__ void member_rec_kernel(const int4* S, const int2* span, const int32_t* nseg, int64_t U,
                                   int4* qrec, unsigned long long* lastq,
                                   const int32_t* sigma = nullptr, const int32_t* gsize = nullptr,
-                                  int32_t* gsq = nullptr) {
+                                  int32_t* gsq = nullptr, int32_t* qrec3 = nullptr) {
     DGRID_LOOP(q, U) {
         const int4 s = S[q];
         qrec[q] = make_int4(nseg[q / (64 * TD_WPW)], span[q].y, s.x, s.y);
+        if (qrec3) qrec3[q] = s.z;  // four objectives: S[q].z is rank 3
         if (lastq) lastq[q] = 0;  // the sliced peels' (front, last position) per v
         if (gsq) gsq[q] = gsize[sigma[q]];
     }
@@ -1280,6 +1281,7 @@ struct CandBufs {
     uint64_t* ckey;  // [3][8 cap]: U index, then (last position << 32 | U index)
     int32_t* cq;     // [3][8 cap]: q
     int4* crec;      // [3][8 cap]: the member record (reach, tie-group end, rank 1, rank 2)
+    int32_t* crec3;  // [3][8 cap]: rank 3 of the record (four objectives), else null
     int64_t cap;
     __device__ __forceinline__ int32_t* count(int buf, int b) const {
         return reinterpret_cast<int32_t*>(pages + CAND_PAGE * (buf * CAND_BUCKETS + b));
@@ -1294,6 +1296,7 @@ struct TabArgs {
     const int32_t* R;
     const uint16_t* BK;
     const int4* qrec;
+    const int32_t* qrec3;  // rank 3 per q (four objectives), else null
     const int32_t* gsize;
     const int32_t* gsq;  // gsize[sigma[q]] per q (member_rec_kernel)
     const int32_t* sigma;
@@ -1303,6 +1306,7 @@ struct TabArgs {
     int32_t* ulist;
     int32_t* fstarts;
     int4* mtab;  // [U] member records in front order: front j at [ustart_j, ustart_j + n_j)
+    int32_t* mtab3;  // [U] their rank 3 (four objectives), else null
     int32_t* gslot;  // [U] a large front's members' places in their bins (tab_sort_big)
     int32_t* gtmp;   // [U] ... its U indices binned
     uint64_t* gkey;  // [U] ... and its keys
@@ -1444,6 +1448,7 @@ __device__ bool tab_sort_count(const TabArgs& a, int64_t bbase, const CandMap& c
             for (int32_t q = beg; q < end; ++q) r += lds.cs.tmp[q] < vu ? 1 : 0;
             a.ulist[ustart + r] = vu;
             a.mtab[ustart + r] = a.cb.crec[bbase + sidx[e]];
+            if (a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + sidx[e]];
         }
     }
     return true;
@@ -1464,7 +1469,10 @@ __device__ void tab_sort_bitonic(const TabArgs& a, int64_t bbase, const CandMap&
         if (i < n) {
             const int32_t vu = (int32_t)(uint32_t)k[e];
             a.ulist[ustart + i] = vu;
-            if (BD_OK(vu, a.U, "tab sorted vu")) a.mtab[ustart + i] = a.qrec[a.pos[vu]];
+            if (BD_OK(vu, a.U, "tab sorted vu")) {
+                a.mtab[ustart + i] = a.qrec[a.pos[vu]];
+                if (a.mtab3) a.mtab3[ustart + i] = a.qrec3[a.pos[vu]];
+            }
         }
     }
 }
@@ -1555,6 +1563,7 @@ __device__ bool tab_sort_big(const TabArgs& a, int64_t bbase, const CandMap& cm,
             for (int32_t q = beg; q < end; ++q) r += a.gtmp[q] < vu ? 1 : 0;
             a.ulist[ustart + r] = vu;
             a.mtab[ustart + r] = rec[b];
+            if (a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + cm.slot(i0 + b * NT)];
         }
     }
     return true;
@@ -1640,7 +1649,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
     const int64_t bbase = a.cb.base(buf);
     const int32_t n1 = sc.sf.Fprev;
     const int64_t us0 = (int64_t)sc.sf.ustart - n1;  // front j-1 in mtab
-    int4* sP = reinterpret_cast<int4*>(smem);         // (tie-group end, rank 1, rank 2) per member
+    int4* sP = reinterpret_cast<int4*>(smem);         // (tie-group end, rank 1, rank 2, rank 3) per member
     const int32_t per = (n + TAB_NA - 1) / TAB_NA;
     const int32_t i0 = aw * per, i1 = min(n, i0 + per);
     // the share in chunks of TAB_NT candidates, 64 per wave; a wave tests 64
@@ -1653,7 +1662,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
         const int32_t i = c0 + 8 * lane + (tid >> 6);
         const bool mine = i < i1;
         int64_t sl = 0;
-        int32_t vq = 0, vr1 = 0, vr2 = 0;
+        int32_t vq = 0, vr1 = 0, vr2 = 0, vr3 = 0;
         uint32_t vu = 0;
         if (mine) {
             sl = bbase + cm.slot(i);
@@ -1661,6 +1670,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
             vq = a.cb.cq[sl];
             vr1 = rec.z;
             vr2 = rec.w;
+            if (F == 3) vr3 = a.cb.crec3[sl];
             vu = (uint32_t)a.cb.ckey[sl];
         }
         int32_t last = -1;
@@ -1670,7 +1680,7 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
             const int32_t wb = max(0, wend - TAB_SWIN);
             for (int32_t t = wb + tid; t < wend; t += TAB_NT) {
                 const int4 r = a.mtab[us0 + t];
-                sP[t - wb] = make_int4(r.y, r.z, r.w, 0);
+                sP[t - wb] = make_int4(r.y, r.z, r.w, F == 3 ? a.mtab3[us0 + t] : 0);
             }
             __syncthreads();
             // 512-member segments from the window's end; member k of this lane
@@ -1689,10 +1699,12 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
                     const int32_t cq1 = __builtin_amdgcn_readlane(vq, cl);
                     const int32_t cr1 = __builtin_amdgcn_readlane(vr1, cl);
                     const int32_t cr2 = __builtin_amdgcn_readlane(vr2, cl);
+                    const int32_t cr3 = F == 3 ? __builtin_amdgcn_readlane(vr3, cl) : 0;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         bool dom = cq1 <= mk[k].x && cr1 <= mk[k].y;
-                        if (F == 2) dom = dom && cr2 <= mk[k].z;
+                        if (F >= 2) dom = dom && cr2 <= mk[k].z;
+                        if (F == 3) dom = dom && cr3 <= mk[k].w;
                         const uint64_t hit = __ballot(dom);
                         if (hit) {  // the lowest lane holds the largest position
                             if (lane == cl) last = sb - 1 - 64 * k - (__ffsll((unsigned long long)hit) - 1);
@@ -1742,16 +1754,19 @@ __device__ void tab_search(const TabArgs& a, int32_t j, int aw, char* smem, TabS
 // The members [wb, we) of the front being peeled (member i at slot bbase +
 // cm.slot(i)) whose row reaches chunk c, into LDS: sM = (rank 1, rank 2,
 // tie-group end, 0).  Returns how many.
+template <int F>
 __device__ int tab_window(const TabArgs& a, int64_t bbase, const CandMap& cm, int64_t wb,
                           int64_t we, int64_t c, int4* sM, TabScalars& sc) {
     constexpr int WR = TAB_WIN / TAB_NT;  // members per thread
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t bal[WR];
     int4 mr[WR];
+    int32_t m3[WR];  // rank 3 (four objectives)
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
         const int64_t i = wb + (int64_t)(wave * WR + r) * 64 + lane;
         mr[r] = i < we ? a.cb.crec[bbase + cm.slot((int32_t)i)] : make_int4(0, 0, 0, 0);
+        m3[r] = F == 3 && i < we ? a.cb.crec3[bbase + cm.slot((int32_t)i)] : 0;
     }
     int nw = 0;
 #pragma unroll
@@ -1772,7 +1787,8 @@ __device__ int tab_window(const TabArgs& a, int64_t bbase, const CandMap& cm, in
     const uint64_t below = (1ull << lane) - 1;
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-        if ((bal[r] >> lane) & 1) sM[base + __popcll(bal[r] & below)] = make_int4(mr[r].z, mr[r].w, mr[r].y, 0);
+        if ((bal[r] >> lane) & 1)  // (rank 1, rank 2, tie-group end, rank 3)
+            sM[base + __popcll(bal[r] & below)] = make_int4(mr[r].z, mr[r].w, mr[r].y, m3[r]);
         base += __popcll(bal[r]);
     }
     __syncthreads();
@@ -1810,11 +1826,13 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
     // released, but a load after the count update would lengthen the release)
     int32_t pcnt = 0, pvu = 0, pgs = 0;
     int4 rq = make_int4(0, 0, 0, 0);
+    int32_t rq3 = 0;
     if (v < U) {
         pcnt = a.countq[v];
         pvu = a.sigma[v];
         pgs = a.gsq[v];
         rq = a.qrec[v];
+        if (F == 3) rq3 = a.qrec3[v];
     }
     if (!BD_OK(pvu, U, "tab sigma")) pvu = 0;
     __syncthreads();
@@ -1843,7 +1861,7 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
     for (int w = 0; w < PW; ++w) dec[w] = 0;
     PPROF_T(pt1);
     for (int64_t wb = j0s; wb < Fm; wb += TAB_WIN) {
-        const int total = tab_window(a, bbase, cm, wb, std::min<int64_t>(Fm, wb + TAB_WIN), c, sM, sc);
+        const int total = tab_window<F>(a, bbase, cm, wb, std::min<int64_t>(Fm, wb + TAB_WIN), c, sM, sc);
         for (int g0 = wave * 64; g0 < total; g0 += TAB_NT) {
             const int g = g0 + lane;
             const int4 mA = g < total ? sM[g] : make_int4(0, 0, 0, 0);
@@ -1851,7 +1869,7 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
                 g < total ? (int32_t)std::max<int64_t>(-1, std::min<int64_t>((int64_t)mA.z - v0, BD_CW)) : -1;
             int k[F];
             if (lim >= 0) {
-                bd_row_k<F>(make_int4(mA.x, mA.y, 0, 0), sR, sB, sh, k);
+                bd_row_k<F>(make_int4(mA.x, mA.y, mA.w, 0), sR, sB, sh, k);
 #ifdef DM_BD_CHECK
                 for (int f = 0; f < F; ++f)
                     if (!BD_OK(k[f], BD_K, "tab peel k")) k[f] = 0;
@@ -1927,6 +1945,7 @@ __device__ void tab_peel(const TabArgs& a, int32_t j, int64_t c, int64_t y, int6
             a.cb.ckey[slot] = (uint64_t)(uint32_t)pvu;
             a.cb.cq[slot] = (int32_t)v;
             a.cb.crec[slot] = rq;
+            if (F == 3) a.cb.crec3[slot] = rq3;
             a.rankU[pvu] = j + 1;
         }
     }
@@ -1971,6 +1990,11 @@ __global__ void tab_front0_kernel(TabArgs a, const int32_t* F0p, const int64_t* 
         a.cb.cq[i] = q;
         a.cb.crec[i] = rec;
         a.mtab[i] = rec;
+        if (a.mtab3) {
+            const int32_t r3 = a.qrec3[q];
+            a.cb.crec3[i] = r3;
+            a.mtab3[i] = r3;
+        }
     }
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     const int64_t s0 = *sorted0p;
@@ -2028,6 +2052,7 @@ __global__ __launch_bounds__(1024) void tab_presorted_kernel(TabArgs a, int32_t 
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         a.ulist[sc.sf.ustart + i] = (int32_t)(uint32_t)keys[i];
         a.mtab[sc.sf.ustart + i] = a.cb.crec[bbase + vals[i]];
+        if (a.mtab3) a.mtab3[sc.sf.ustart + i] = a.cb.crec3[bbase + vals[i]];
     }
     if (threadIdx.x == 0) tab_finish(a, j, n, sc.pend, sc.sf);
 }
@@ -2040,6 +2065,7 @@ __global__ __launch_bounds__(1024) void tab_presorted_kernel(TabArgs a, int32_t 
 struct FastLayout {
     int64_t NB, NG, NQ, ngroups, Upad;  // NG: 512-v segments (tri_dom), NQ: TW-word lines (peel)
     size_t part, S, sigma, pos, nseg, toff, counter, mrow, mtab, qrec, crec, countq, cq, work, total;
+    size_t mtab3, qrec3, crec3;  // rank 3 of the records (four objectives)
 };
 // elements of the rank pass's key / value buffers: the population (objective
 // 0's q order) or the M-1 <= 3 objectives' unique values sorted as one batch
@@ -2103,6 +2129,9 @@ static FastLayout fast_layout(int64_t n, int64_t U) {
     L.crec = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 16);
     L.countq = take((size_t)U * 4);
     L.cq = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 4);
+    L.mtab3 = take((size_t)U * 4);
+    L.qrec3 = take((size_t)U * 4);
+    L.crec3 = take((size_t)3 * CAND_BUCKETS * cand_cap(U) * 4);
     L.work = take(std::max(ranks_work_bytes(n, U), fronts_work_bytes(U)));
     L.total = off;
     return L;
@@ -2123,7 +2152,7 @@ int64_t fast_dom_words(int64_t U) {
 // matrix (peel_order_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
 // D peel.
 bool fast_bitset(const dm_ctx* ctx, int m) {
-    return m >= 2 && m <= 3 && ctx->dom_path != DM_DOM_COMPARE;
+    return m >= 2 && (m <= 3 || (m == 4 && ctx->knobs.bd_m4)) && ctx->dom_path != DM_DOM_COMPARE;
 }
 bool fast_table_peel(const dm_ctx* ctx, int m) {
     return fast_bitset(ctx, m) && ctx->dom_path != DM_DOM_PEEL_D;
@@ -2261,6 +2290,10 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
     a.cb.ckey = (uint64_t*)(p + W.ckey);
     a.cb.cq = (int32_t*)(ws + L.cq);
     a.cb.crec = (int4*)(ws + L.crec);
+    // four objectives: rank 3 travels beside every record
+    a.qrec3 = m == 4 ? (const int32_t*)(ws + L.qrec3) : nullptr;
+    a.mtab3 = m == 4 ? (int32_t*)(ws + L.mtab3) : nullptr;
+    a.cb.crec3 = m == 4 ? (int32_t*)(ws + L.crec3) : nullptr;
     a.cb.cap = cand_cap(U);
     a.U = U;
     a.N = N;
@@ -2275,7 +2308,8 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
     a.gsq = gsq;
     member_rec_kernel<<<dg1(U), 256, 0, s>>>((const int4*)(ws + L.S), (const int2*)(tws + TL.span),
                                              (const int32_t*)(ws + L.nseg), U, (int4*)(ws + L.qrec),
-                                             nullptr, a.sigma, gsize, gsq);
+                                             nullptr, a.sigma, gsize, gsq,
+                                             m == 4 ? (int32_t*)(ws + L.qrec3) : nullptr);
     tab_front0_kernel<<<dg1(U), 256, 0, s>>>(a, F0, sorted0);
     char* hbuf = (char*)pinned(ctx, 2048);
     if (!hbuf) return DM_ERR_NOMEM;
@@ -2298,8 +2332,10 @@ static int fast_fronts_tab(dm_ctx* ctx, int m, int64_t n, int64_t U, const int32
             timing_begin(ctx, DM_TIME_PEEL);
             if (m == 2)
                 peel_order_kernel<1><<<grid, TAB_NT, 0, s>>>(a, j + b);
-            else
+            else if (m == 3)
                 peel_order_kernel<2><<<grid, TAB_NT, 0, s>>>(a, j + b);
+            else
+                peel_order_kernel<3><<<grid, TAB_NT, 0, s>>>(a, j + b);
             timing_end(ctx, DM_TIME_PEEL);
         }
         timing_end(ctx, DM_TIME_PEEL_CHAIN);
