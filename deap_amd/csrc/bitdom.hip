@@ -241,10 +241,16 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     const uint32_t* __restrict__ P, const int32_t* __restrict__ R, const uint16_t* __restrict__ BK,
     int16_t* __restrict__ part) {
     constexpr int F = M - 1;
-    static_assert(F <= 3, "the prefix-set tables of 2-4 objectives fit in LDS (110,988 B at F = 3)");
-    __shared__ uint4 sP[F][BD_K * 4];
-    __shared__ int32_t sR[F][BD_RP];
-    __shared__ uint16_t sB[F][BD_BKN];
+    static_assert(F <= 3, "2 to 4 objectives");
+    // objectives 1-2 in LDS (73,992 B, as for three objectives); a fourth
+    // objective's tables are read from the global table, whose chunk slice
+    // (35 KB) stays in the L2: the 110,988-B LDS form of four objectives
+    // faulted on the GPU twice while running clean in the host emulation
+    // ("the m = 4 fault")
+    constexpr int FL = F < 3 ? F : 2;
+    __shared__ uint4 sP[FL][BD_K * 4];
+    __shared__ int32_t sR[FL][BD_RP];
+    __shared__ uint16_t sB[FL][BD_BKN];
     const int sh = bd_bucket_shift(U);
     const int32_t t = blockIdx.x;
     if (t >= toffC[NG]) return;
@@ -255,7 +261,10 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
     int64_t v = vb + threadIdx.x;
     int4 sv = v < ve ? S[v] : make_int4(0, 0, 0, 0);
     int32_t sf = v < ve ? span[v].x : 0;
-    bd_load_tables<F>(P, R, BK, c, sP, sR, sB);
+    bd_load_tables<FL, F>(P, R, BK, c, sP, sR, sB);
+    const uint4* gP3 = reinterpret_cast<const uint4*>(P + (c * F + 2) * BD_K * 16);  // F = 3 only
+    const int32_t* gR3 = R + (c * F + 2) * BD_CW;
+    const uint16_t* gB3 = BK + (c * F + 2) * BD_BKN;
     const int rot = threadIdx.x & 3;
     const int64_t v0 = c * BD_CW;
     const int32_t nvalid = (int32_t)std::min<int64_t>(U - v0, BD_CW);  // positions < nvalid are real rows
@@ -269,7 +278,15 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
         }
         int k[F];
 #pragma unroll
-        for (int f = 0; f < F; ++f) k[f] = bd_count_below<false>(sR[f], sB[f], sh, icomp(cv, f));
+        for (int f = 0; f < FL; ++f) k[f] = bd_count_below<false>(sR[f], sB[f], sh, icomp(cv, f));
+        if constexpr (F == 3) {  // #{j : R_3[j] < r_3(v)} from the global sorted ranks
+            const int32_t x = icomp(cv, 2);
+            const int b = x >> sh;
+            int j = gB3[b];
+            const int e = gB3[b + 1];
+            while (j < e && gR3[j] < x) ++j;
+            k[2] = j;
+        }
         uint32_t cnt = 0;
         const bool edge = lo > 0 || nvalid < BD_CW;
 #pragma unroll
@@ -278,7 +295,7 @@ __global__ __launch_bounds__(BD_THREADS) void bd_count_kernel(
             uint4 o = sP[0][k[0] * 4 + j];
 #pragma unroll
             for (int f = 1; f < F; ++f) {
-                const uint4 y = sP[f][k[f] * 4 + j];
+                const uint4 y = f < FL ? sP[f < FL ? f : 0][k[f] * 4 + j] : gP3[k[f] * 4 + j];
                 o.x |= y.x;
                 o.y |= y.y;
                 o.z |= y.z;
@@ -333,8 +350,12 @@ static void bitdom_launch(dm_ctx* ctx, const int4* S, int64_t U, int64_t NQ, con
     const int32_t* R = (const int32_t*)(ws + L.R);
     const uint16_t* BK = (const uint16_t*)(ws + L.BK);
     const int64_t maxtasks = L.NG * ((U + BD_RT - 1) / BD_RT);
-    if (D)  // D words only for the D-reading peel (the table-fed peel needs none)
-        bd_rows_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
+    // D words only for the D-reading peel (the table-fed peel needs none);
+    // four objectives never write D here (fast_bitset: DM_DOM_PEEL_D at M = 4
+    // takes the compare kernel), so no 110,988-B LDS kernel is ever launched
+    if constexpr (M <= 3)
+        if (D)
+            bd_rows_kernel<M><<<dim3((unsigned)maxtasks), BD_THREADS, 0, s>>>(
         S, span, U, NQ, L.NG, (const int32_t*)(ws + L.rowfirst), (const int32_t*)(ws + L.toffD), P,
         R, BK, D);
     timing_begin(ctx, DM_TIME_DOMINANCE);

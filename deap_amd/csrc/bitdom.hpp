@@ -104,25 +104,26 @@ __device__ __forceinline__ int64_t bd_task_chunk(const int32_t* toff, int64_t NG
     }
     return lo;
 }
-// The chunk's bucket tables (F x BD_BKN uint16) into LDS.
-template <int F>
+// The chunk's bucket tables (F x BD_BKN uint16) into LDS: the first F of the
+// FG objectives the global tables hold per chunk.
+template <int F, int FG = F>
 __device__ __forceinline__ void bd_load_buckets(const uint16_t* BK, int64_t c,
                                                 uint16_t (&sB)[F][BD_BKN]) {
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(BK + c * F * BD_BKN);
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(BK + c * FG * BD_BKN);
     uint32_t* l = reinterpret_cast<uint32_t*>(&sB[0][0]);
     for (int i = threadIdx.x; i < F * BD_BKN / 2; i += blockDim.x) l[i] = g[i];
 }
-template <int F>
+template <int F, int FG = F>
 __device__ __forceinline__ void bd_load_tables(const uint32_t* P, const int32_t* R, const uint16_t* BK,
                                                int64_t c, uint4 (&sP)[F][BD_K * 4],
                                                int32_t (&sR)[F][BD_RP], uint16_t (&sB)[F][BD_BKN]) {
-    bd_load_buckets<F>(BK, c, sB);
+    bd_load_buckets<F, FG>(BK, c, sB);
     // batches of 4 global loads in flight, then their LDS stores: the staging
     // stays in registers (a whole-table register array of up to 13 pieces was
     // placed in scratch memory by the compiler)
     constexpr int NP = F * BD_K * 4, NR = F * BD_CW / 4;
-    const uint4* gP = reinterpret_cast<const uint4*>(P + c * F * BD_K * 16);
-    const int4* gR = reinterpret_cast<const int4*>(R + c * F * BD_CW);
+    const uint4* gP = reinterpret_cast<const uint4*>(P + c * FG * BD_K * 16);
+    const int4* gR = reinterpret_cast<const int4*>(R + c * FG * BD_CW);
     uint4* lP = &sP[0][0];
     for (int i0 = threadIdx.x; i0 < NP; i0 += 4 * BD_THREADS) {
         uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0, t2 = t0, t3 = t0;

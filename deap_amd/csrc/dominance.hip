@@ -2152,7 +2152,8 @@ int64_t fast_dom_words(int64_t U) {
 // matrix (peel_order_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
 // D peel.
 bool fast_bitset(const dm_ctx* ctx, int m) {
-    return m >= 2 && (m <= 3 || (m == 4 && ctx->knobs.bd_m4)) && ctx->dom_path != DM_DOM_COMPARE;
+    return m >= 2 && (m <= 3 || (m == 4 && ctx->knobs.bd_m4 && ctx->dom_path != DM_DOM_PEEL_D)) &&
+           ctx->dom_path != DM_DOM_COMPARE;
 }
 bool fast_table_peel(const dm_ctx* ctx, int m) {
     return fast_bitset(ctx, m) && ctx->dom_path != DM_DOM_PEEL_D;

@@ -238,6 +238,22 @@ __device__ inline void mo_finalize(const dm_eval& ev, int n, double S, const dou
     }
 }
 
+// ZDT1 / ZDT2 / ZDT4 only, the same arithmetic as mo_finalize (square roots
+// and divisions): the short-row kernel's light variant, whose registers are
+// not sized by the sine / power paths of ZDT3 / ZDT6 / DTLZ
+__device__ __forceinline__ void mo_finalize_light(const dm_eval& ev, int n, double S, double h0,
+                                                  double* f) {
+    const double g = ev.fn == DM_EVAL_ZDT4 ? (double)(1 + 10 * (n - 1)) + S
+                                           : 1.0 + 9.0 * S / (double)(n - 1);
+    f[0] = h0;
+    if (ev.fn == DM_EVAL_ZDT2) {
+        const double r = h0 / g;
+        f[1] = g * (1.0 - r * r);
+    } else {
+        f[1] = g * (1.0 - sqrt(h0 / g));
+    }
+}
+
 // Per-row evaluation state carried across the chunks of one row.
 struct EvalState {
     double s;      // running per-lane partial sum

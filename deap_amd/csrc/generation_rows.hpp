@@ -73,6 +73,14 @@ __device__ __forceinline__ PairPlan load_plan_vec(const PairPlan* plans, int64_t
 // ONE copy of each term and of the final formula (an 8-step loop over the two
 // children's genes, the finalisation with per-lane data), so the objective's
 // transcendental code is inlined once.
+// ZDT1 / ZDT2 / ZDT4 on short rows: EC_MO's terms with the light final
+// formula (evals.hpp mo_finalize_light), two objectives
+constexpr int EC_MO_LIGHT = 7;
+__host__ __device__ constexpr bool ec_mo(int ec) { return ec == EC_MO || ec == EC_MO_LIGHT; }
+__host__ __device__ inline bool mo_light(int fn) {
+    return fn == DM_EVAL_ZDT1 || fn == DM_EVAL_ZDT2 || fn == DM_EVAL_ZDT4;
+}
+
 template <int G, int EC>
 __device__ __forceinline__ void rows_eval(const dm_eval& ev, int dim, int g, int sub,
                                           const double (&y0)[4], const double (&y1)[4], bool inv0,
@@ -95,7 +103,7 @@ __device__ __forceinline__ void rows_eval(const dm_eval& ev, int dim, int g, int
             acc1 += rosen_term(y1[3], nb1);
         }
     } else {
-        const int t0 = EC == EC_MO ? mo_tail_start(ev) : 0;
+        const int t0 = ec_mo(EC) ? mo_tail_start(ev) : 0;
 #pragma unroll 1
         for (int k = 0; k < 8; ++k) {
             const int j = k & 3;
@@ -104,7 +112,7 @@ __device__ __forceinline__ void rows_eval(const dm_eval& ev, int dim, int g, int
             const double xb = j == 0 ? y1[0] : j == 1 ? y1[1] : j == 2 ? y1[2] : y1[3];
             const double x = second ? xb : xa;
             if (g + j < dim && g + j >= t0 && (second ? inv1 : inv0)) {
-                const double t = EC == EC_MO ? mo_term(ev.fn, x) : sum_term(ev.fn, x);
+                const double t = ec_mo(EC) ? mo_term(ev.fn, x) : sum_term(ev.fn, x);
                 if (second)
                     acc1 += t;
                 else
@@ -117,6 +125,9 @@ __device__ __forceinline__ void rows_eval(const dm_eval& ev, int dim, int g, int
     const double S = second ? S1 : S0;
     if constexpr (ec_single(EC)) {
         f[0] = ev.fn == DM_EVAL_RASTRIGIN ? (double)(10 * (int64_t)dim) + S : S;  // 10*len + sum
+    } else if constexpr (EC == EC_MO_LIGHT) {
+        const double h0 = __shfl(y0[0], gl0, 64), h1 = __shfl(y1[0], gl0, 64);  // gene 0
+        mo_finalize_light(ev, dim, S, second ? h1 : h0, f);
     } else if constexpr (EC == EC_MO) {
         double h[8];
 #pragma unroll
@@ -291,6 +302,10 @@ __global__ __launch_bounds__(256) void gen_rows_kernel(GenArgs a, const PairPlan
             if (!second || has1) {
                 if constexpr (ec_single(EC)) {
                     a.cwv[c] = inv ? f[0] * a.w0 : (second ? pl.f1 : pl.f0);
+                } else if constexpr (EC == EC_MO_LIGHT) {
+#pragma unroll
+                    for (int o = 0; o < 2; ++o)
+                        a.cwv[c * 2 + o] = inv ? f[o] * a.ev.weights[o] : a.pwv[s * 2 + o];
                 } else if constexpr (EC == EC_MO) {
                     for (int o = 0; o < m; ++o)
                         a.cwv[c * m + o] = inv ? f[o] * a.ev.weights[o] : a.pwv[s * m + o];
@@ -315,6 +330,8 @@ template <typename T, int G, int CX, int MUT>
 void launch_rows_e(const GenArgs& a, const PairPlan* plans, int ec, dim3 grid, hipStream_t s) {
     if (ec_single(ec))
         gen_rows_kernel<T, G, CX, MUT, EC_SUM><<<grid, 256, 0, s>>>(a, plans);
+    else if (ec == EC_MO && mo_light(a.ev.fn) && a.nobj == 2)
+        gen_rows_kernel<T, G, CX, MUT, EC_MO_LIGHT><<<grid, 256, 0, s>>>(a, plans);
     else if (ec == EC_MO)
         gen_rows_kernel<T, G, CX, MUT, EC_MO><<<grid, 256, 0, s>>>(a, plans);
     else
