@@ -463,7 +463,6 @@ static void read_knobs(dm_knobs& kn) {
     kn.bits_nokeys = std::getenv("DM_BITS_NOKEYS") != nullptr;
     kn.lex_full = std::getenv("DM_LEX_FULL") != nullptr;
     kn.lex_no32 = std::getenv("DM_LEX_NO32") != nullptr;
-    kn.bd_m4 = std::getenv("DM_BD_M4") != nullptr;
     kn.pipe_label_rounds = std::max(0, std::min(8, env_int("DM_PIPE_LABEL_ROUNDS", 2)));
     kn.selbest_fullsort = std::getenv("DM_SELBEST_FULLSORT") != nullptr;
     kn.pipe_bpc = std::max(0, env_int("DM_PIPE_BPC", 0));

@@ -59,7 +59,6 @@ struct dm_knobs {
     bool bits_nokeys = false;       // DM_BITS_NOKEYS: C2 tournaments read wvalues, no int16 keys
     bool lex_full = false;          // DM_LEX_FULL: full lexicographic sort in the grouping
     bool lex_no32 = false;          // DM_LEX_NO32: whole-key objective-0 sort in the grouping
-    bool bd_m4 = false;             // DM_BD_M4: four objectives on the bitset tables + table peel
     int32_t pipe_label_rounds = 2;  // DM_PIPE_LABEL_ROUNDS: label propagation rounds of the plan order (2: round 1 + a gather jump)
     bool selbest_fullsort = false;  // DM_SELBEST_FULLSORT: selBest by the full radix sort
     int pipe_bpc = 0;               // DM_PIPE_BPC: C3 workgroups per CU (0 = 32 ordered / 64)

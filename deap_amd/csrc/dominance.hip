@@ -2151,8 +2151,18 @@ int64_t fast_dom_words(int64_t U) {
 // DESIGN.md §8.)  With the bitset pass the peel reads the tables, not a D
 // matrix (peel_order_kernel), unless the DM_DOM_PEEL_D cross-check asks for the
 // D peel.
+// Four objectives on the bitset tables (rank 3 beside the member records) are
+// built only into diagnostic builds (-DDM_BD_M4: tools_cpu/bdemu runs them on
+// the host): on the GPU the path faulted in both of round 6's forms, with the
+// count pass's tables in LDS and out of it, while running clean under ASan in
+// the host emulation ("the m = 4 fault").
+#ifdef DM_BD_M4
+constexpr bool kBitsetM4 = true;
+#else
+constexpr bool kBitsetM4 = false;
+#endif
 bool fast_bitset(const dm_ctx* ctx, int m) {
-    return m >= 2 && (m <= 3 || (m == 4 && ctx->knobs.bd_m4 && ctx->dom_path != DM_DOM_PEEL_D)) &&
+    return m >= 2 && (m <= 3 || (kBitsetM4 && m == 4 && ctx->dom_path != DM_DOM_PEEL_D)) &&
            ctx->dom_path != DM_DOM_COMPARE;
 }
 bool fast_table_peel(const dm_ctx* ctx, int m) {

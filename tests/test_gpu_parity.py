@@ -492,14 +492,13 @@ def test_bitset_dominance_equals_compare_kernel(gpu, m, n):
     chunk.  Two and three objectives: the bitset-table pass with the
     table-fed peel (bitdom.hip) against the same pass writing D for the
     D-reading peel (DM_DOM_PEEL_D) and the integer compare kernel
-    (DM_DOM_COMPARE).  Four objectives: the bitset tables too when the
-    context has DM_BD_M4 (rank 3 beside the member records), else the integer
-    compare kernel + D peel, checked against the fp64 ballot and LDS kernels."""
-    import os
+    (DM_DOM_COMPARE).  Four objectives: the integer compare kernel + D peel,
+    checked against the fp64 ballot and LDS kernels (the four-objective bitset
+    path exists only in diagnostic builds)."""
     from deap_amd import _lib, tools
     from deap_amd.device import Context, dominance_path
     ctx = Context.get()
-    bitset = m <= 3 or bool(os.environ.get("DM_BD_M4"))
+    bitset = m <= 3
     assert _lib.load().dm_ctx_dom_bitset(ctx.handle, m) == (1 if bitset else 0)
     paths = ("default", "compare", "peel_d") if bitset else ("default", "ballot", "lds")
     rng = np.random.default_rng(1000 * m + n)

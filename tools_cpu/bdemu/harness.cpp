@@ -95,8 +95,6 @@ int main(int argc, char** argv) {
     dm_ctx ctx;
 #ifdef EMU_PRE
     ctx.knobs.bd_maxm = getenv("EMU_BD_MAXM") ? atoi(getenv("EMU_BD_MAXM")) : 3;
-#else
-    ctx.knobs.bd_m4 = getenv("DM_BD_M4") != nullptr;  // four objectives on the bitset path
 #endif
     // exact-size "device" buffers, so ASan bounds them as the caller sized them
     double* dwv = (double*)malloc(sizeof(double) * n * m);
