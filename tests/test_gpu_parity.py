@@ -616,7 +616,9 @@ def test_native_hot_kernel_equals_replay_kernel(gpu, gt, dim, n, cx, mut, object
 
 @pytest.mark.parametrize("gt,dim,objective,obj", [
     ("f64", 30, "zdt1", None), ("f32", 12, "dtlz2", 3), ("f64", 64, "zdt3", None),
-    ("f64", 7, "dtlz1", 4)])
+    ("f64", 7, "dtlz1", 4),
+    # ZDT1 / ZDT2 / ZDT4 take the light final formula (mo_finalize_light)
+    ("f64", 20, "zdt2", None), ("f32", 10, "zdt4", None), ("f64", 40, "zdt6", None)])
 def test_native_short_rows_multiobjective_equal_replay(gpu, gt, dim, objective, obj):
     """Multi-objective eaSimple on short rows (generation_rows.hpp): the
     lexicographic tournaments of the plan kernel (selection.py:55-70 through
