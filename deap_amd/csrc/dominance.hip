@@ -1276,6 +1276,13 @@ struct FrontSum {      // read by the host after each batch of launches
     int64_t maxinds;    // individuals of the largest front so far (crowding's segmented sort)
     int32_t arrive[3];  // search workgroups done, per candidate buffer
 };
+// Four objectives on the bitset tables: diagnostic builds only (-DDM_BD_M4,
+// see fast_bitset); the product build compiles the rank-3 copies out.
+#ifdef DM_BD_M4
+constexpr bool kBitsetM4 = true;
+#else
+constexpr bool kBitsetM4 = false;
+#endif
 struct CandBufs {
     char* pages;     // [3][8] counter pages: slot count at +0, released individuals at +64
     uint64_t* ckey;  // [3][8 cap]: U index, then (last position << 32 | U index)
@@ -1448,7 +1455,7 @@ __device__ bool tab_sort_count(const TabArgs& a, int64_t bbase, const CandMap& c
             for (int32_t q = beg; q < end; ++q) r += lds.cs.tmp[q] < vu ? 1 : 0;
             a.ulist[ustart + r] = vu;
             a.mtab[ustart + r] = a.cb.crec[bbase + sidx[e]];
-            if (a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + sidx[e]];
+            if (kBitsetM4 && a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + sidx[e]];
         }
     }
     return true;
@@ -1471,7 +1478,7 @@ __device__ void tab_sort_bitonic(const TabArgs& a, int64_t bbase, const CandMap&
             a.ulist[ustart + i] = vu;
             if (BD_OK(vu, a.U, "tab sorted vu")) {
                 a.mtab[ustart + i] = a.qrec[a.pos[vu]];
-                if (a.mtab3) a.mtab3[ustart + i] = a.qrec3[a.pos[vu]];
+                if (kBitsetM4 && a.mtab3) a.mtab3[ustart + i] = a.qrec3[a.pos[vu]];
             }
         }
     }
@@ -1563,7 +1570,7 @@ __device__ bool tab_sort_big(const TabArgs& a, int64_t bbase, const CandMap& cm,
             for (int32_t q = beg; q < end; ++q) r += a.gtmp[q] < vu ? 1 : 0;
             a.ulist[ustart + r] = vu;
             a.mtab[ustart + r] = rec[b];
-            if (a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + cm.slot(i0 + b * NT)];
+            if (kBitsetM4 && a.mtab3) a.mtab3[ustart + r] = a.cb.crec3[bbase + cm.slot(i0 + b * NT)];
         }
     }
     return true;
@@ -1990,7 +1997,7 @@ __global__ void tab_front0_kernel(TabArgs a, const int32_t* F0p, const int64_t* 
         a.cb.cq[i] = q;
         a.cb.crec[i] = rec;
         a.mtab[i] = rec;
-        if (a.mtab3) {
+        if (kBitsetM4 && a.mtab3) {
             const int32_t r3 = a.qrec3[q];
             a.cb.crec3[i] = r3;
             a.mtab3[i] = r3;
@@ -2052,7 +2059,7 @@ __global__ __launch_bounds__(1024) void tab_presorted_kernel(TabArgs a, int32_t 
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         a.ulist[sc.sf.ustart + i] = (int32_t)(uint32_t)keys[i];
         a.mtab[sc.sf.ustart + i] = a.cb.crec[bbase + vals[i]];
-        if (a.mtab3) a.mtab3[sc.sf.ustart + i] = a.cb.crec3[bbase + vals[i]];
+        if (kBitsetM4 && a.mtab3) a.mtab3[sc.sf.ustart + i] = a.cb.crec3[bbase + vals[i]];
     }
     if (threadIdx.x == 0) tab_finish(a, j, n, sc.pend, sc.sf);
 }
@@ -2156,11 +2163,6 @@ int64_t fast_dom_words(int64_t U) {
 // the host): on the GPU the path faulted in both of round 6's forms, with the
 // count pass's tables in LDS and out of it, while running clean under ASan in
 // the host emulation ("the m = 4 fault").
-#ifdef DM_BD_M4
-constexpr bool kBitsetM4 = true;
-#else
-constexpr bool kBitsetM4 = false;
-#endif
 bool fast_bitset(const dm_ctx* ctx, int m) {
     return m >= 2 && (m <= 3 || (kBitsetM4 && m == 4 && ctx->dom_path != DM_DOM_PEEL_D)) &&
            ctx->dom_path != DM_DOM_COMPARE;
