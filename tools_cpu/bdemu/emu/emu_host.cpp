@@ -8,6 +8,11 @@
 #include <numeric>
 #include <vector>
 
+#if defined(__has_feature)
+#if __has_feature(memory_sanitizer)
+#include <sanitizer/msan_interface.h>
+#endif
+#endif
 #include "common.hpp"
 #include "sort.hpp"
 
@@ -59,6 +64,14 @@ static void* arena_get(Arena& a, size_t bytes) {
         static const int fill =
             getenv("EMU_ARENA_FILL") ? (int)strtol(getenv("EMU_ARENA_FILL"), nullptr, 0) : 0xC3;
         memset(a.p, fill, a.cap);
+#if defined(__has_feature)
+#if __has_feature(memory_sanitizer)
+        // a new device allocation holds no defined values; EMU_MSAN_ARENA=0 keeps
+        // them defined (the epoch-stamped front state is read before it is
+        // written by design: a stale entry never carries the call's epoch)
+        if (!getenv("EMU_MSAN_ARENA") || atoi(getenv("EMU_MSAN_ARENA")) != 0) __msan_poison(a.p, a.cap);
+#endif
+#endif
     }
     EMU_UNPOISON(a.p, a.cap);
     EMU_POISON(a.p + bytes, a.cap - bytes);

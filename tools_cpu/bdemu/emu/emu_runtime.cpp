@@ -10,6 +10,13 @@
 
 #include "hip/hip_runtime.h"
 
+#if defined(__has_feature)
+#if __has_feature(memory_sanitizer)
+#include <sanitizer/msan_interface.h>
+#define EMU_MSAN 1
+#endif
+#endif
+
 thread_local emu_u3 threadIdx, blockIdx, blockDim, gridDim;
 
 namespace emu {
@@ -149,7 +156,13 @@ void launch(const Cfg& c, const char* name, const std::function<void()>& body) {
         if (c.shm) memset(dyn.data(), lds_fill(), c.shm);  // undefined LDS content
         {
             std::lock_guard<std::mutex> lk(g_lds_mu);
-            for (auto& r : g_lds) memset(r.first, lds_fill(), r.second);
+            for (auto& r : g_lds) {
+#ifdef EMU_MSAN
+                __msan_poison(r.first, r.second);  // undefined at workgroup start
+#else
+                memset(r.first, lds_fill(), r.second);
+#endif
+            }
         }
         alarm(budget);
         pool().run(&b);

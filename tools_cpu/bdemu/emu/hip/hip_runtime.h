@@ -320,34 +320,41 @@ inline void emu_writelane(T& old, U val, int L) {
 }
 
 // ---- atomics (sequentially consistent on the host) ----
+// (renamed: clang knows the __hip_atomic_* names as builtins on every target)
+#define __hip_atomic_fetch_add emu__hip_atomic_fetch_add
+#define __hip_atomic_fetch_max emu__hip_atomic_fetch_max
+#define __hip_atomic_fetch_min emu__hip_atomic_fetch_min
+#define __hip_atomic_exchange emu__hip_atomic_exchange
+#define __hip_atomic_load emu__hip_atomic_load
+#define __hip_atomic_store emu__hip_atomic_store
 template <class T>
-inline T __hip_atomic_fetch_add(T* p, T v, int, int) {
+inline T emu__hip_atomic_fetch_add(T* p, T v, int, int) {
     return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
 }
 template <class T>
-inline T __hip_atomic_fetch_max(T* p, T v, int, int) {
+inline T emu__hip_atomic_fetch_max(T* p, T v, int, int) {
     T cur = __atomic_load_n(p, __ATOMIC_SEQ_CST);
     while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
     }
     return cur;
 }
 template <class T>
-inline T __hip_atomic_fetch_min(T* p, T v, int, int) {
+inline T emu__hip_atomic_fetch_min(T* p, T v, int, int) {
     T cur = __atomic_load_n(p, __ATOMIC_SEQ_CST);
     while (cur > v && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
     }
     return cur;
 }
 template <class T>
-inline T __hip_atomic_exchange(T* p, T v, int, int) {
+inline T emu__hip_atomic_exchange(T* p, T v, int, int) {
     return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST);
 }
 template <class T>
-inline T __hip_atomic_load(T* p, int, int) {
+inline T emu__hip_atomic_load(T* p, int, int) {
     return __atomic_load_n(p, __ATOMIC_SEQ_CST);
 }
 template <class T, class U>
-inline void __hip_atomic_store(T* p, U v, int, int) {
+inline void emu__hip_atomic_store(T* p, U v, int, int) {
     __atomic_store_n(p, (T)v, __ATOMIC_SEQ_CST);
 }
 template <class T, class U>
